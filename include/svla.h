@@ -1,0 +1,214 @@
+/*
+ * svla.h — C-ABI of the MI355X (gfx950) SpatialVLA hot-path kernels (libsvla.so).
+ *
+ * Drop-in boundary.  Every entry point replaces one op of the reference's
+ * eager PyTorch/flash-attn/DeepSpeed path; the reference interface each one replaces is cited
+ * next to it.  Conventions (all entry points):
+ *   - plain pointers + sizes, no torch types; caller owns every buffer (incl. workspace),
+ *     kernels never allocate or free;
+ *   - bf16 tensors are raw 16-bit bit patterns (uint16_t), row-major unless stated;
+ *   - launches are asynchronous and stream-ordered on `stream` (a hipStream_t), no host sync;
+ *   - return 0 on success, SVLA_ERR_ARG on a rejected argument, SVLA_ERR_HIP on a launch
+ *     failure; svla_last_error() returns the thread-local message of the last failure;
+ *   - deterministic: no float atomics anywhere, so results are bitwise run-to-run stable.
+ */
+#ifndef SVLA_H_
+#define SVLA_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SVLA_OK = 0, SVLA_ERR_ARG = 1, SVLA_ERR_HIP = 2 };
+
+/* Last error message of the calling thread ("" if none). */
+const char* svla_last_error(void);
+/* Library version string and the gfx target it was built for. */
+const char* svla_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * GEMM  C[M,N] (op)= epilogue( sum_k A(m,k) * B(n,k) ), bf16 in, fp32 accumulate (MFMA 16x16x32).
+ * Replaces every nn.Linear / torch.matmul of the hot path: Gemma2 q/k/v/o and gate/up/down
+ * (reference model/modeling_gemma2.py:86-92, 351-354, 376-408), lm_head (:895, :993),
+ * SigLIP q/k/v/out/fc1/fc2 and patch-embed conv (transformers siglip [3p]), projector
+ * (model/modeling_spatialvla.py:124), Ego3D MLP (:59-64) — forward and both backward GEMMs.
+ * ---------------------------------------------------------------------------------------- */
+enum { SVLA_LAYOUT_KC = 0, /* element (r,k) at ptr[r*ld + k]  (reduction dim contiguous) */
+       SVLA_LAYOUT_RC = 1  /* element (r,k) at ptr[k*ld + r]  (outer dim contiguous)     */ };
+enum { SVLA_SEG_OUTER = 0, SVLA_SEG_K = 1, SVLA_SEG_GEGLU = 2 };
+
+/* One GEMM operand.  r = outer index (m for A, n for B), k = reduction index.
+ * Up to 4 segments along `seg_dim`: segment s covers [seg_start[s], seg_start[s+1]) of that
+ * index and reads ptr[s] with the index rebased to seg_start[s] (lets q/k/v or gate/up weights
+ * that live in separate tensors act as one operand).  Segment starts must be tile aligned
+ * (128 on the outer dim, 64 on k).  SVLA_SEG_GEGLU (B only): outer row n of tile t=n/128 reads
+ * ptr[0] row 64t+(n%128) if n%128<64 else ptr[1] row 64t+(n%128)-64 (gate/up interleave). */
+typedef struct {
+  const void* ptr[4];
+  int64_t seg_start[5];
+  int32_t nseg;
+  int32_t seg_dim;
+  int32_t layout;
+  int32_t _pad;
+  int64_t ld;
+} svla_operand;
+
+enum {
+  SVLA_EPI_STORE = 0,      /* C = alpha*acc                                                  */
+  SVLA_EPI_BIAS = 1,       /* C = alpha*acc + bias[n]                                        */
+  SVLA_EPI_BIAS_GELU = 2,  /* pre = bf16(acc+bias) -> out1;  C = gelu_tanh(pre)               */
+  SVLA_EPI_BIAS_RESID = 3, /* C = bf16(acc+bias) + in0[m,n]   (bias optional)                 */
+  SVLA_EPI_GEGLU = 4,      /* B uses SVLA_SEG_GEGLU; g->out1, u->out2, C = gelu_tanh(g)*u     */
+  SVLA_EPI_GEGLU_BWD = 5,  /* acc = dH; in0=g, in1=u: out1 = dH*u*gelu'(g), out2 = dH*gelu(g) */
+  SVLA_EPI_GELU_BWD = 6,   /* acc = dAct; in0 = pre-activation: C = dAct*gelu'(pre)           */
+  SVLA_EPI_SOFTCAP_CE = 7  /* C = cap*tanh(acc/cap); row_stats[m, tile_n] = {max,sumexp,argmax} */
+};
+
+typedef struct {
+  int32_t kind;
+  int32_t accumulate;        /* 1: C += result (STORE only) */
+  float alpha;
+  float cap;
+  const void* bias;          /* [N] bf16 */
+  const void* in0; int64_t ld_in0;
+  const void* in1; int64_t ld_in1;
+  void* out1; int64_t ld_out1;
+  void* out2; int64_t ld_out2;
+  float* row_stats;          /* [M][ceil(N/128)][3] fp32 (SOFTCAP_CE) */
+} svla_epilogue;
+
+/* C: up to 4 row segments (c_seg_start tile-aligned to 128) — lets dW of q/k/v (or gate/up)
+ * land directly in separate gradient tensors.  c_nseg = 1 for a plain matrix.
+ * Requirements: ld of every operand and of C a multiple of 8 elements; pointers 16-B aligned. */
+int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
+                   void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                   const svla_epilogue* epi, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Attention.  Reference: eager_attention_forward (model/modeling_gemma2.py:169-195) selected via
+ * GEMMA2_ATTENTION_FUNCTION (:317-322) with the prefix-LM additive mask of
+ * _update_causal_mask (model/modeling_spatialvla.py:258-306) and Gemma2 RoPE
+ * (modeling_gemma2.py:95-154); SigLIP eager attention (transformers siglip [3p], no mask).
+ * The [B,1,L,L] mask is never materialised: kv_class[b, j] (uint8) classifies key j:
+ *   0 = visible to every query, 1 = visible to queries i >= j, 2 = never visible;
+ * plus an optional sliding window (key j masked for query i when i - j >= window, 0 = off).
+ * Masked scores take the bf16 minimum (-3.3895e38) exactly as the reference's additive mask.
+ * q/k/v are read in place from projection outputs: element (b, t, h, d) at
+ *   base + (b*L + t)*ld + h*D + d.
+ * rope_cos/rope_sin (optional, [L][D/2] bf16, row stride rope_ld) apply Gemma2 rotate_half RoPE
+ * to q and k on load (forward) and its transpose to dq/dk (backward).
+ * head_dim D in {256, 72}.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t B, L, Hq, Hkv, D;
+  int32_t sliding_window;
+  float scale;      /* query_pre_attn_scalar^-0.5 (Gemma2) or D^-0.5 (SigLIP) */
+  float softcap;    /* 0 = off */
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk;
+  const void* v; int64_t ldv;
+  const uint8_t* kv_class;   /* [B, L] or NULL (= all visible) */
+  const void* rope_cos;      /* [L][D/2] bf16 or NULL */
+  const void* rope_sin;
+  int64_t rope_ld;
+} svla_attn_args;
+
+int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);
+/* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
+ * workspace: B*Hq*L fp32 (row dot(dO, O)). */
+int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                  const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                  float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Norms.  Gemma2RMSNorm (modeling_gemma2.py:60-77): y = bf16(x*rsqrt(mean(x^2)+eps)*(1+w)) in fp32.
+ * Residual form (decoder layer :489-496): h = bf16(res + bf16(rms(y_in; w))).
+ * LayerNorm (SigLIP layer_norm1/2/post, Ego3D head.1): y = bf16((x-mu)*rstd*w + b).
+ * rows of length N (ld = N).  rstd/mean saved per row (fp32) for backward.
+ * ---------------------------------------------------------------------------------------- */
+int svla_rmsnorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, float eps, void* y,
+                     float* rstd, void* stream);
+/* dw_partial: [ceil(rows/rows_per_block)] x N fp32 partial sums, reduced by svla_colsum_f32. */
+int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* rstd,
+                     const void* dy, const void* dres, void* dx, float* dw_partial, int64_t* n_partial,
+                     void* stream);
+int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w, float eps,
+                         void* h, float* rstd, void* stream);
+int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
+                       void* y, float* mean, float* rstd, void* stream);
+int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* mean,
+                       const float* rstd, const void* dy, const void* dres, void* dx, float* dwb_partial,
+                       int64_t* n_partial, void* stream);
+/* out[n] = bf16(sum_p in[p, n]) (+ existing out if accumulate): reduces partial sums. */
+int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate, void* stream);
+/* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients). workspace >= 64*N fp32 */
+int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16, int32_t accumulate,
+                     float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Elementwise / glue.
+ * ---------------------------------------------------------------------------------------- */
+/* Embedding merge (modeling_spatialvla.py:361-387 + modeling_gemma2.py:741-742):
+ * out[b,t] = normalizer * (ids in [a0, a0+na) ? spatial[ids-a0] : (ids == image_id ? img[next] : embed[ids]))
+ * img rows consumed in (b,t) order (masked_scatter); img_pos[b*L+t] = running image index (host computed). */
+int svla_embed_merge(int64_t rows, int64_t H, const int64_t* ids, const int32_t* img_index, const void* embed,
+                     const void* spatial, int64_t a0, int64_t na, const void* img, float normalizer, void* out,
+                     void* stream);
+/* Backward of the merge: spatial-table grad (deterministic per-row segmented sum) and image-feature grad. */
+int svla_embed_merge_bwd(int64_t rows, int64_t H, const int64_t* ids, const int32_t* img_index,
+                         const int32_t* spatial_sorted_rows, const int32_t* spatial_offsets, int64_t na,
+                         const void* dout, float normalizer, void* dspatial, void* dimg, void* stream);
+/* Ego3D (modeling_spatialvla.py:195-223, :74-91): area-pool depth [B,1,Hd,Wd] to (hp*reso)^2, back-project
+ * with inv(K) @ uv_h (uv_h passed in, bf16-quantised as the model buffer), permute per patch,
+ * normalise ((xyz-center)/2 -> bf16), frequency-encode -> feat [B, hp*wp, ldf] bf16 (cols >= 12*(2F+1) zeroed). */
+int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* depth, const float* kinv, const float* uv_h,
+                      int32_t patch, int32_t reso, int32_t n_freqs, void* feat, int64_t ldf, float* xyz_out,
+                      void* stream);
+/* SigLIP patchify (Conv2d k=s=patch): x [B,3,S,S] bf16 already normalised -> cols [B*(S/p)^2, ldc]
+ * with column order (c, ky, kx) as the conv weight flattening; columns >= 3p^2 zeroed. */
+int svla_im2col_patch(int32_t B, int32_t S, int32_t patch, const void* x, void* cols, int64_t ldc,
+                      void* stream);
+/* out = bf16(bf16(x + offset) * scale) elementwise: TF.normalize((x), mean, std) with offset=-mean,
+ * scale=1/std (modeling_spatialvla.py:309; bf16 rounding after the subtraction as torchvision does). */
+int svla_affine_bf16(int64_t n, const void* x, float scale, float offset, void* out, void* stream);
+/* y = relu(x) (Ego3D head.2) fwd/bwd */
+int svla_relu_fwd(int64_t n, const void* x, void* y, void* stream);
+int svla_relu_bwd(int64_t n, const void* x, const void* dy, void* dx, void* stream);
+/* out = bf16(a + b) */
+int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Softcapped lm_head cross-entropy (modeling_gemma2.py:993-997 + modeling_spatialvla.py:415-430,
+ * action argmax train/monkey_patch.py:267-309).  Logits come from svla_gemm_bf16 with
+ * SVLA_EPI_SOFTCAP_CE, which leaves per (row, 128-col tile) {max, sumexp, argmax} in row_stats.
+ * ---------------------------------------------------------------------------------------- */
+/* Reduce row_stats -> lse[m], argmax[m]; loss_rows[m] = lse - logit[m, target[m]] for target >= 0
+ * (else 0); loss_out[0] = sum(loss_rows)/max(n_valid,1) where n_valid = #(target >= 0). */
+int svla_ce_finalize(int64_t M, int64_t N, int64_t ntiles, const float* row_stats, const void* logits, int64_t ldl,
+                     const int64_t* target, float* lse, int64_t* argmax, float* loss_rows, float* loss_out,
+                     void* stream);
+/* dlogits[m, n] = scale*(softmax(y)[n] - [n==target]) * (1 - (y/cap)^2), y = bf16 logits; rows with
+ * target < 0 get 0; columns in [N, ldd) zeroed.  scale = grad_loss / n_valid (device scalar). */
+int svla_ce_bwd(int64_t M, int64_t N, const void* logits, int64_t ldl, const float* lse, const int64_t* target,
+                float cap, const float* grad_scale, void* dlogits, int64_t ldd, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Optimizer (DeepSpeed FusedAdam / torch AdamW semantics, scripts/zero1.json:23-34).
+ * ---------------------------------------------------------------------------------------- */
+/* partial sums of squares of a bf16 vector -> out[0] += sum (single fp32; deterministic tree). */
+int svla_sumsq_bf16(int64_t n, const void* x, float* partial, int64_t n_partial, float* out, void* stream);
+/* AdamW over a flat shard: g = bf16 grad * clip_scale(device scalar);
+ * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= lr*(m/bc1 / (sqrt(v/bc2)+eps) + wd*p);
+ * master fp32 updated, param_bf16 = bf16(master). */
+int svla_adamw(int64_t n, float* master, void* param_bf16, const void* grad_bf16, float* m, float* v, float lr,
+               float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2,
+               const float* clip_scale, void* stream);
+/* clip_scale[0] = min(1, max_norm / (sqrt(sumsq[0]) + 1e-6)); norm_out[0] = sqrt(sumsq[0]). */
+int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float* norm_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVLA_H_ */

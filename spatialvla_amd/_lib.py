@@ -1,0 +1,114 @@
+"""ctypes binding of libsvla.so — the C-ABI declared in include/svla.h.
+
+The library is the only compute path of this package: if it is missing or fails to load,
+`lib()` raises immediately (there is no fallback of any kind).  torch is imported first so the
+HIP runtime that torch already loaded (SONAME libamdhip64.so.7) is the one libsvla.so binds to;
+kernels then run on torch's streams and memory.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsvla.so")
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+# enums mirrored from include/svla.h
+LAYOUT_KC, LAYOUT_RC = 0, 1
+SEG_OUTER, SEG_K, SEG_GEGLU = 0, 1, 2
+EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EPI_GELU_BWD, EPI_SOFTCAP_CE = range(8)
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("ptr", c_vp * 4), ("seg_start", c_i64 * 5), ("nseg", c_i32), ("seg_dim", c_i32),
+                ("layout", c_i32), ("_pad", c_i32), ("ld", c_i64)]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [("kind", c_i32), ("accumulate", c_i32), ("alpha", c_f32), ("cap", c_f32), ("bias", c_vp),
+                ("in0", c_vp), ("ld_in0", c_i64), ("in1", c_vp), ("ld_in1", c_i64), ("out1", c_vp),
+                ("ld_out1", c_i64), ("out2", c_vp), ("ld_out2", c_i64), ("row_stats", c_vp)]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("B", c_i32), ("L", c_i32), ("Hq", c_i32), ("Hkv", c_i32), ("D", c_i32),
+                ("sliding_window", c_i32), ("scale", c_f32), ("softcap", c_f32),
+                ("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
+                ("kv_class", c_vp), ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64)]
+
+
+# name -> (restype, argtypes); every entry point of include/svla.h
+SIGNATURES = {
+    "svla_last_error": (ctypes.c_char_p, []),
+    "svla_version": (ctypes.c_char_p, []),
+    "svla_gemm_bf16": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), ctypes.POINTER(Operand),
+                               ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64,
+                               ctypes.POINTER(Epilogue), c_vp]),
+    "svla_attn_fwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_vp]),
+    "svla_attn_bwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                              c_vp, c_i64, c_vp, c_vp]),
+    "svla_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "svla_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp]),
+    "svla_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "svla_layernorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
+    "svla_layernorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   ctypes.POINTER(c_i64), c_vp]),
+    "svla_colsum_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_i32, c_vp]),
+    "svla_colsum_bf16": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "svla_embed_merge": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
+    "svla_embed_merge_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "svla_ego3d_encode": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp,
+                                  c_vp]),
+    "svla_im2col_patch": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp]),
+    "svla_affine_bf16": (c_i32, [c_i64, c_vp, c_f32, c_f32, c_vp, c_vp]),
+    "svla_relu_fwd": (c_i32, [c_i64, c_vp, c_vp, c_vp]),
+    "svla_relu_bwd": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "svla_add_bf16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "svla_ce_finalize": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "svla_ce_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp]),
+    "svla_sumsq_bf16": (c_i32, [c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "svla_adamw": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
+                           c_vp, c_vp]),
+    "svla_clip_scale": (c_i32, [c_vp, c_f32, c_vp, c_vp, c_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class SvlaError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """dlopen libsvla.so and bind every symbol; raises if anything is missing."""
+    if not os.path.exists(path):
+        raise SvlaError(f"libsvla.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
+                        f"g.build()'` (make -C spatialvla_amd/csrc). There is no fallback path.")
+    cdll = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(cdll, name)  # AttributeError if an export is missing
+        fn.restype = res
+        fn.argtypes = args
+    return cdll
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                _lib = load()
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().svla_last_error().decode(errors="replace")
+        raise SvlaError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,478 @@
+// HBM-bound glue kernels of the hot path: embedding merge, Ego3D back-projection + frequency
+// encoding, SigLIP patchify, elementwise helpers, softcapped-CE finalize/backward, grad-norm and
+// AdamW.  All vectorised 16 B per lane (8 bf16) where the layout allows.
+#include "svla_common.h"
+
+namespace {
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+inline unsigned nblk(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// ------------------------------------------------------------------ embedding merge
+// modeling_spatialvla.py:361-387 + modeling_gemma2.py:741-742 (see svla.h)
+__global__ void embed_merge_kernel(int64_t rows, int64_t H, const int64_t* __restrict__ ids,
+                                   const int32_t* __restrict__ img_index, const bf16_t* __restrict__ embed,
+                                   const bf16_t* __restrict__ spatial, int64_t a0, int64_t na,
+                                   const bf16_t* __restrict__ img, float normalizer, bf16_t* __restrict__ out) {
+  const int64_t row = blockIdx.x;
+  const int64_t id = ids[row];
+  const int ii = img_index ? img_index[row] : -1;
+  const int64_t nch = H >> 3;
+  for (int64_t ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+    float v[8];
+    if (ii >= 0) {
+      unpack8(*reinterpret_cast<const u32x4*>(img + (int64_t)ii * H + ch * 8), v);
+    } else if (spatial && id >= a0 && id < a0 + na) {
+      float e[8];
+      unpack8(*reinterpret_cast<const u32x4*>(embed + id * H + ch * 8), e);
+      unpack8(*reinterpret_cast<const u32x4*>(spatial + (id - a0) * H + ch * 8), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = round_bf(e[j] * 0.0f) + v[j];  // x*0.0 + spatial
+    } else {
+      unpack8(*reinterpret_cast<const u32x4*>(embed + id * H + ch * 8), v);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) * normalizer;
+    *reinterpret_cast<u32x4*>(out + row * H + ch * 8) = pack8(v);
+  }
+}
+
+// image-feature grad: dimg[img_index[row]] = bf16(dout[row]*normalizer)
+__global__ void embed_img_bwd_kernel(int64_t rows, int64_t H, const int32_t* __restrict__ img_index,
+                                     const bf16_t* __restrict__ dout, float normalizer, bf16_t* __restrict__ dimg) {
+  const int64_t row = blockIdx.x;
+  const int ii = img_index[row];
+  if (ii < 0) return;
+  for (int64_t ch = threadIdx.x; ch < (H >> 3); ch += blockDim.x) {
+    float v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(dout + row * H + ch * 8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= normalizer;
+    *reinterpret_cast<u32x4*>(dimg + (int64_t)ii * H + ch * 8) = pack8(v);
+  }
+}
+
+// spatial-table grad: one block per table row, summing its occurrences in sorted (CSR) order
+__global__ void embed_spatial_bwd_kernel(int64_t H, const int32_t* __restrict__ sorted_rows,
+                                         const int32_t* __restrict__ offsets, const bf16_t* __restrict__ dout,
+                                         float normalizer, bf16_t* __restrict__ dspatial) {
+  const int64_t sid = blockIdx.x;
+  const int b = offsets[sid], e = offsets[sid + 1];
+  for (int64_t ch = threadIdx.x; ch < (H >> 3); ch += blockDim.x) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = b; i < e; ++i) {
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dout + (int64_t)sorted_rows[i] * H + ch * 8), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += round_bf(v[j] * normalizer);
+    }
+    *reinterpret_cast<u32x4*>(dspatial + sid * H + ch * 8) = pack8(acc);
+  }
+}
+
+// ------------------------------------------------------------------ Ego3D
+// one block per (b, patch); thread layout: 12 coords x 17 features
+__global__ void ego3d_kernel(int B, int Hd, int Wd, const bf16_t* __restrict__ depth, const float* __restrict__ kinv,
+                             const float* __restrict__ uvh, int patch, int reso, int n_freqs,
+                             bf16_t* __restrict__ feat, int64_t ldf, float* __restrict__ xyz_out) {
+  const int b = blockIdx.y, p = blockIdx.x;
+  const int hp = Hd / patch, wp = Wd / patch;
+  const int py = p / wp, px = p % wp;
+  const int gw = wp * reso, gh = hp * reso;  // area-pooled grid
+  const int ry = Hd / gh, rx = Wd / gw;      // exact pooling window (224/32 = 7)
+  __shared__ float xyz[64];
+  const int npts = reso * reso;
+  if ((int)threadIdx.x < npts) {
+    const int sy = threadIdx.x / reso, sx = threadIdx.x % reso;
+    const int gy = py * reso + sy, gx = px * reso + sx;
+    // F.interpolate(mode="area") == mean over the ry x rx window, result rounded to bf16
+    float s = 0.f;
+    for (int yy = 0; yy < ry; ++yy)
+      for (int xx = 0; xx < rx; ++xx) s += bf2f(depth[((int64_t)b * Hd + gy * ry + yy) * Wd + gx * rx + xx]);
+    const float d = round_bf(s / (float)(ry * rx));
+    const int idx = gy * gw + gx;
+    const float u = uvh[idx], v = uvh[gh * gw + idx], w1 = uvh[2 * gh * gw + idx];
+    const float* K = kinv + b * 9;
+    for (int c = 0; c < 3; ++c) {
+      const float pc = (K[c * 3 + 0] * u + K[c * 3 + 1] * v + K[c * 3 + 2] * w1) * d;
+      xyz[threadIdx.x * 3 + c] = pc;
+    }
+  }
+  __syncthreads();
+  const int ncoord = npts * 3, nf = 2 * n_freqs + 1;
+  bf16_t* frow = feat + ((int64_t)b * hp * wp + p) * ldf;
+  for (int i = threadIdx.x; i < ldf; i += blockDim.x) {
+    float o = 0.f;
+    if (i < ncoord * nf) {
+      const int m = i / nf, f = i % nf;
+      const float center = (m % 3 == 2) ? 2.0f : 0.0f;
+      const float xn = round_bf((xyz[m] - center) / 2.0f);
+      if (f == 0) o = xn;
+      else if (f <= n_freqs) o = sinf(round_bf(xn * (float)(1 << (f - 1))));
+      else o = cosf(round_bf(xn * (float)(1 << (f - 1 - n_freqs))));
+    }
+    frow[i] = f2bf(o);
+  }
+  if (xyz_out && (int)threadIdx.x < ncoord) xyz_out[((int64_t)b * hp * wp + p) * ncoord + threadIdx.x] = xyz[threadIdx.x];
+}
+
+// ------------------------------------------------------------------ SigLIP patchify
+__global__ void im2col_kernel(int B, int S, int P, const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
+                              int64_t ldc) {
+  const int64_t r = blockIdx.x;  // b*np + patch
+  const int np1 = S / P, np = np1 * np1;
+  const int b = (int)(r / np), pi = (int)(r % np);
+  const int py = pi / np1, px = pi % np1;
+  const int K = 3 * P * P;
+  for (int i = threadIdx.x; i < ldc; i += blockDim.x) {
+    bf16_t v = 0;
+    if (i < K) {
+      const int c = i / (P * P), rem = i % (P * P), ky = rem / P, kx = rem % P;
+      v = x[(((int64_t)b * 3 + c) * S + py * P + ky) * S + px * P + kx];
+    }
+    cols[r * ldc + i] = v;
+  }
+}
+
+__global__ void affine_kernel(int64_t n, const bf16_t* __restrict__ x, float scale, float offset,
+                              bf16_t* __restrict__ y) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  if (i + 8 <= n) {
+    float v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + i), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + offset) * scale;
+    *reinterpret_cast<u32x4*>(y + i) = pack8(v);
+  } else {
+    for (int64_t j = i; j < n; ++j) y[j] = f2bf(round_bf(bf2f(x[j]) + offset) * scale);
+  }
+}
+
+__global__ void relu_fwd_kernel(int64_t n, const bf16_t* __restrict__ x, bf16_t* __restrict__ y) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  for (int64_t j = i; j < min(n, i + 8); ++j) {
+    float v = bf2f(x[j]);
+    y[j] = f2bf(v > 0.f ? v : 0.f);
+  }
+}
+__global__ void relu_bwd_kernel(int64_t n, const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                bf16_t* __restrict__ dx) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  for (int64_t j = i; j < min(n, i + 8); ++j) dx[j] = bf2f(x[j]) > 0.f ? dy[j] : (bf16_t)0;
+}
+__global__ void add_kernel(int64_t n, const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                           bf16_t* __restrict__ y) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  if (i + 8 <= n) {
+    float u[8], v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(a + i), u);
+    unpack8(*reinterpret_cast<const u32x4*>(b + i), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u[j] += v[j];
+    *reinterpret_cast<u32x4*>(y + i) = pack8(u);
+  } else {
+    for (int64_t j = i; j < n; ++j) y[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+  }
+}
+
+// ------------------------------------------------------------------ softcapped CE
+__global__ void ce_finalize_kernel(int64_t M, int64_t N, int64_t ntiles, const float* __restrict__ rs,
+                                   const bf16_t* __restrict__ logits, int64_t ldl, const int64_t* __restrict__ target,
+                                   float* __restrict__ lse, int64_t* __restrict__ argmax, float* __restrict__ loss_rows) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float mx = -INFINITY, se = 0.f;
+  int am = 0x7fffffff;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const float* p = rs + (m * ntiles + t) * 3;
+    const float m2 = p[0], s2 = p[1];
+    const int a2 = __float_as_int(p[2]);
+    if (m2 == -INFINITY) continue;
+    const float mn = fmaxf(mx, m2);
+    se = (mx == -INFINITY ? 0.f : se * __expf(mx - mn)) + s2 * __expf(m2 - mn);
+    if (m2 > mx || (m2 == mx && a2 < am)) am = a2;
+    mx = mn;
+  }
+  const float l = mx + __logf(se);
+  lse[m] = l;
+  argmax[m] = am;
+  const int64_t tg = target ? target[m] : -1;
+  loss_rows[m] = (tg >= 0 && tg < N) ? l - bf2f(logits[m * ldl + tg]) : 0.f;
+}
+
+__global__ void ce_loss_kernel(int64_t M, const float* __restrict__ loss_rows, const int64_t* __restrict__ target,
+                               float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f, c = 0.f;
+  for (int64_t m = threadIdx.x; m < M; m += blockDim.x) {
+    s += loss_rows[m];
+    c += (target && target[m] >= 0) ? 1.f : 0.f;
+  }
+  s = block_sum(s, red);
+  c = block_sum(c, red);
+  if (threadIdx.x == 0) {
+    out[0] = s / fmaxf(c, 1.f);
+    out[1] = c;
+  }
+}
+
+// grid: (ceil(ldd/2048), M); each thread 8 columns
+__global__ void ce_bwd_kernel(int64_t M, int64_t N, const bf16_t* __restrict__ logits, int64_t ldl,
+                              const float* __restrict__ lse, const int64_t* __restrict__ target, float cap,
+                              const float* __restrict__ gscale, bf16_t* __restrict__ d, int64_t ldd) {
+  const int64_t m = blockIdx.y;
+  const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (n >= ldd) return;
+  const int64_t tg = target[m];
+  u32x4 outv = {0u, 0u, 0u, 0u};
+  if (tg >= 0 && n < N) {
+    const float l = lse[m], sc = gscale[0];
+    float y[8], o[8];
+    if (n + 8 <= N) unpack8(*reinterpret_cast<const u32x4*>(logits + m * ldl + n), y);
+    else
+      for (int j = 0; j < 8; ++j) y[j] = (n + j < N) ? bf2f(logits[m * ldl + n + j]) : 0.f;
+    const float icap = cap > 0.f ? 1.0f / cap : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (n + j < N) {
+        float g = __expf(y[j] - l) - ((n + j == tg) ? 1.f : 0.f);
+        g *= sc;
+        // reference rounds the fp32 CE grad to bf16 at logits.float() and then differentiates the bf16 softcap
+        g = round_bf(g);
+        const float th = y[j] * icap;
+        o[j] = cap > 0.f ? g * (1.0f - th * th) : g;
+      } else {
+        o[j] = 0.f;
+      }
+    }
+    outv = pack8(o);
+  }
+  if (n + 8 <= ldd) *reinterpret_cast<u32x4*>(d + m * ldd + n) = outv;
+  else {
+    uint16_t tmp[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tmp[2 * j] = outv[j] & 0xffff;
+      tmp[2 * j + 1] = outv[j] >> 16;
+    }
+    for (int j = 0; n + j < ldd; ++j) d[m * ldd + n + j] = tmp[j];
+  }
+}
+
+// ------------------------------------------------------------------ norm + AdamW
+__global__ void sumsq_stage1(int64_t n, const bf16_t* __restrict__ x, float* __restrict__ partial) {
+  __shared__ float red[16];
+  const int64_t per = (((n + gridDim.x - 1) / gridDim.x) + 7) & ~(int64_t)7;
+  const int64_t b0 = (int64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+  float s = 0.f;
+  int64_t i = b0 + (int64_t)threadIdx.x * 8;
+  // aligned vector body (b0 multiple of 8 when per is)
+  for (; i + 8 <= b1; i += (int64_t)blockDim.x * 8) {
+    float v[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + i), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  }
+  for (; i < b1; ++i) {
+    float v = bf2f(x[i]);
+    s += v * v;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+__global__ void sumsq_stage2(int64_t np, const float* __restrict__ partial, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < np; i += blockDim.x) s += partial[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+__global__ void clip_kernel(const float* sumsq, float max_norm, float* clip, float* norm_out) {
+  const float nrm = sqrtf(sumsq[0]);
+  if (norm_out) norm_out[0] = nrm;
+  clip[0] = (max_norm > 0.f) ? fminf(1.0f, max_norm / (nrm + 1e-6f)) : 1.0f;
+}
+
+__global__ void adamw_kernel(int64_t n, float* __restrict__ master, bf16_t* __restrict__ param,
+                             const bf16_t* __restrict__ grad, float* __restrict__ m, float* __restrict__ v, float lr,
+                             float b1, float b2, float eps, float wd, float bc1, float bc2,
+                             const float* __restrict__ clip) {
+  const float cs = clip ? clip[0] : 1.0f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n; i += stride) {
+    if (i + 8 <= n) {
+      float g[8];
+      unpack8(*reinterpret_cast<const u32x4*>(grad + i), g);
+      f32x4 p0 = *reinterpret_cast<const f32x4*>(master + i), p1 = *reinterpret_cast<const f32x4*>(master + i + 4);
+      f32x4 m0 = *reinterpret_cast<const f32x4*>(m + i), m1 = *reinterpret_cast<const f32x4*>(m + i + 4);
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(v + i), v1 = *reinterpret_cast<const f32x4*>(v + i + 4);
+      float pp[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+      float mm[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+      float vv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gg = g[j] * cs;
+        mm[j] = b1 * mm[j] + (1.f - b1) * gg;
+        vv[j] = b2 * vv[j] + (1.f - b2) * gg * gg;
+        const float upd = (mm[j] / bc1) / (sqrtf(vv[j] / bc2) + eps);
+        pp[j] = pp[j] - lr * (upd + wd * pp[j]);
+      }
+      *reinterpret_cast<f32x4*>(master + i) = f32x4{pp[0], pp[1], pp[2], pp[3]};
+      *reinterpret_cast<f32x4*>(master + i + 4) = f32x4{pp[4], pp[5], pp[6], pp[7]};
+      *reinterpret_cast<f32x4*>(m + i) = f32x4{mm[0], mm[1], mm[2], mm[3]};
+      *reinterpret_cast<f32x4*>(m + i + 4) = f32x4{mm[4], mm[5], mm[6], mm[7]};
+      *reinterpret_cast<f32x4*>(v + i) = f32x4{vv[0], vv[1], vv[2], vv[3]};
+      *reinterpret_cast<f32x4*>(v + i + 4) = f32x4{vv[4], vv[5], vv[6], vv[7]};
+      *reinterpret_cast<u32x4*>(param + i) = pack8(pp);
+    } else {
+      for (int64_t k = i; k < n; ++k) {
+        const float gg = bf2f(grad[k]) * cs;
+        m[k] = b1 * m[k] + (1.f - b1) * gg;
+        v[k] = b2 * v[k] + (1.f - b2) * gg * gg;
+        const float upd = (m[k] / bc1) / (sqrtf(v[k] / bc2) + eps);
+        master[k] = master[k] - lr * (upd + wd * master[k]);
+        param[k] = f2bf(master[k]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int svla_embed_merge(int64_t rows, int64_t H, const int64_t* ids, const int32_t* img_index,
+                                const void* embed, const void* spatial, int64_t a0, int64_t na, const void* img,
+                                float normalizer, void* out, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && H % 8 == 0 && ids && embed && out, "embed_merge: bad args");
+  SVLA_CHECK_ARG(!img_index || img, "embed_merge: img_index without img");
+  hipLaunchKernelGGL(embed_merge_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, rows, H, ids,
+                     img_index, (const bf16_t*)embed, (const bf16_t*)spatial, a0, na, (const bf16_t*)img, normalizer,
+                     (bf16_t*)out);
+  return svla::check_launch("embed_merge");
+}
+
+extern "C" int svla_embed_merge_bwd(int64_t rows, int64_t H, const int64_t* ids, const int32_t* img_index,
+                                    const int32_t* spatial_sorted_rows, const int32_t* spatial_offsets, int64_t na,
+                                    const void* dout, float normalizer, void* dspatial, void* dimg, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && H % 8 == 0 && dout, "embed_merge_bwd: bad args");
+  (void)ids;
+  hipStream_t s = (hipStream_t)stream;
+  if (dimg) {
+    SVLA_CHECK_ARG(img_index != nullptr, "embed_merge_bwd: dimg needs img_index");
+    hipLaunchKernelGGL(embed_img_bwd_kernel, dim3((unsigned)rows), dim3(256), 0, s, rows, H, img_index,
+                       (const bf16_t*)dout, normalizer, (bf16_t*)dimg);
+    if (int rc = svla::check_launch("embed_img_bwd")) return rc;
+  }
+  if (dspatial) {
+    SVLA_CHECK_ARG(spatial_sorted_rows && spatial_offsets && na > 0, "embed_merge_bwd: spatial CSR missing");
+    hipLaunchKernelGGL(embed_spatial_bwd_kernel, dim3((unsigned)na), dim3(256), 0, s, H, spatial_sorted_rows,
+                       spatial_offsets, (const bf16_t*)dout, normalizer, (bf16_t*)dspatial);
+    if (int rc = svla::check_launch("embed_spatial_bwd")) return rc;
+  }
+  return 0;
+}
+
+extern "C" int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* depth, const float* kinv,
+                                 const float* uv_h, int32_t patch, int32_t reso, int32_t n_freqs, void* feat,
+                                 int64_t ldf, float* xyz_out, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && depth && kinv && uv_h && feat, "ego3d: null");
+  SVLA_CHECK_ARG(Hd % patch == 0 && Wd % patch == 0 && (Hd / patch * reso) > 0 && Hd % (Hd / patch * reso) == 0 &&
+                     Wd % (Wd / patch * reso) == 0,
+                 "ego3d: area pooling must be an exact integer window");
+  SVLA_CHECK_ARG(reso * reso * 3 <= 64 && n_freqs <= 16 && ldf >= reso * reso * 3 * (2 * n_freqs + 1),
+                 "ego3d: reso/n_freqs/ldf");
+  dim3 grid((Hd / patch) * (Wd / patch), B);
+  hipLaunchKernelGGL(ego3d_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, Hd, Wd, (const bf16_t*)depth, kinv,
+                     uv_h, patch, reso, n_freqs, (bf16_t*)feat, ldf, xyz_out);
+  return svla::check_launch("ego3d");
+}
+
+extern "C" int svla_im2col_patch(int32_t B, int32_t S, int32_t patch, const void* x, void* cols, int64_t ldc,
+                                 void* stream) {
+  SVLA_CHECK_ARG(B > 0 && S % patch == 0 && x && cols && ldc >= 3 * patch * patch, "im2col: bad args");
+  const int64_t rows = (int64_t)B * (S / patch) * (S / patch);
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, B, S, patch,
+                     (const bf16_t*)x, (bf16_t*)cols, ldc);
+  return svla::check_launch("im2col");
+}
+
+extern "C" int svla_affine_bf16(int64_t n, const void* x, float scale, float offset, void* out, void* stream) {
+  SVLA_CHECK_ARG(n > 0 && x && out && al16(x) && al16(out), "affine: bad args");
+  hipLaunchKernelGGL(affine_kernel, dim3(nblk(n, 256 * 8)), dim3(256), 0, (hipStream_t)stream, n, (const bf16_t*)x,
+                     scale, offset, (bf16_t*)out);
+  return svla::check_launch("affine");
+}
+extern "C" int svla_relu_fwd(int64_t n, const void* x, void* y, void* stream) {
+  SVLA_CHECK_ARG(n > 0 && x && y, "relu: bad args");
+  hipLaunchKernelGGL(relu_fwd_kernel, dim3(nblk(n, 256 * 8)), dim3(256), 0, (hipStream_t)stream, n,
+                     (const bf16_t*)x, (bf16_t*)y);
+  return svla::check_launch("relu_fwd");
+}
+extern "C" int svla_relu_bwd(int64_t n, const void* x, const void* dy, void* dx, void* stream) {
+  SVLA_CHECK_ARG(n > 0 && x && dy && dx, "relu_bwd: bad args");
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(nblk(n, 256 * 8)), dim3(256), 0, (hipStream_t)stream, n,
+                     (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx);
+  return svla::check_launch("relu_bwd");
+}
+extern "C" int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream) {
+  SVLA_CHECK_ARG(n > 0 && a && b && out && al16(a) && al16(b) && al16(out), "add: bad args");
+  hipLaunchKernelGGL(add_kernel, dim3(nblk(n, 256 * 8)), dim3(256), 0, (hipStream_t)stream, n, (const bf16_t*)a,
+                     (const bf16_t*)b, (bf16_t*)out);
+  return svla::check_launch("add");
+}
+
+extern "C" int svla_ce_finalize(int64_t M, int64_t N, int64_t ntiles, const float* row_stats, const void* logits,
+                                int64_t ldl, const int64_t* target, float* lse, int64_t* argmax, float* loss_rows,
+                                float* loss_out, void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && row_stats && logits && lse && argmax && loss_rows && loss_out, "ce_finalize: args");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(nblk(M, 256)), dim3(256), 0, s, M, N, ntiles, row_stats,
+                     (const bf16_t*)logits, ldl, target, lse, argmax, loss_rows);
+  if (int rc = svla::check_launch("ce_finalize")) return rc;
+  hipLaunchKernelGGL(ce_loss_kernel, dim3(1), dim3(1024), 0, s, M, loss_rows, target, loss_out);
+  return svla::check_launch("ce_loss");
+}
+
+extern "C" int svla_ce_bwd(int64_t M, int64_t N, const void* logits, int64_t ldl, const float* lse,
+                           const int64_t* target, float cap, const float* grad_scale, void* dlogits, int64_t ldd,
+                           void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && logits && lse && target && grad_scale && dlogits, "ce_bwd: args");
+  SVLA_CHECK_ARG(ldl % 8 == 0 && ldd % 8 == 0 && ldd >= N, "ce_bwd: ld");
+  dim3 grid(nblk(ldd, 256 * 8), (unsigned)M);
+  hipLaunchKernelGGL(ce_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, N, (const bf16_t*)logits, ldl, lse,
+                     target, cap, grad_scale, (bf16_t*)dlogits, ldd);
+  return svla::check_launch("ce_bwd");
+}
+
+extern "C" int svla_sumsq_bf16(int64_t n, const void* x, float* partial, int64_t n_partial, float* out,
+                               void* stream) {
+  SVLA_CHECK_ARG(n > 0 && x && partial && out && n_partial > 0 && n_partial <= 65535 && al16(x), "sumsq: args");
+  hipStream_t s = (hipStream_t)stream;
+  // per-block chunk must stay 8-aligned for the vector body
+  hipLaunchKernelGGL(sumsq_stage1, dim3((unsigned)n_partial), dim3(256), 0, s, n, (const bf16_t*)x, partial);
+  if (int rc = svla::check_launch("sumsq1")) return rc;
+  hipLaunchKernelGGL(sumsq_stage2, dim3(1), dim3(1024), 0, s, n_partial, partial, out);
+  return svla::check_launch("sumsq2");
+}
+
+extern "C" int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float* norm_out, void* stream) {
+  SVLA_CHECK_ARG(sumsq && clip_scale, "clip: args");
+  hipLaunchKernelGGL(clip_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sumsq, max_norm, clip_scale, norm_out);
+  return svla::check_launch("clip");
+}
+
+extern "C" int svla_adamw(int64_t n, float* master, void* param_bf16, const void* grad_bf16, float* m, float* v,
+                          float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2,
+                          const float* clip_scale, void* stream) {
+  SVLA_CHECK_ARG(n > 0 && master && param_bf16 && grad_bf16 && m && v, "adamw: args");
+  SVLA_CHECK_ARG(al16(master) && al16(param_bf16) && al16(grad_bf16) && al16(m) && al16(v), "adamw: alignment");
+  unsigned g = nblk(n, 256 * 8);
+  if (g > 256 * 64) g = 256 * 64;
+  hipLaunchKernelGGL(adamw_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n, master, (bf16_t*)param_bf16,
+                     (const bf16_t*)grad_bf16, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, clip_scale);
+  return svla::check_launch("adamw");
+}

@@ -1,0 +1,364 @@
+// Row normalisations (HBM-bound): Gemma2 RMSNorm (+ residual), LayerNorm, and deterministic
+// column reductions for their weight gradients and for bias gradients.
+//
+// One 256-thread block per row; each thread owns up to MAXC 16-B chunks (8 bf16) of the row in
+// registers, so x is read from HBM exactly once per pass.  Weight-gradient partial sums are
+// written per block (RPB rows) in fp32 and reduced in a fixed order by svla_colsum_f32 —
+// no atomics, bitwise reproducible.
+#include "svla_common.h"
+
+namespace {
+constexpr int NTH = 256;
+constexpr int MAXC = 4;  // rows up to 256*4*8 = 8192 elements
+constexpr int RPB = 16;  // rows per block in the backward kernels
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const u32x4*>(p), f); }
+__device__ __forceinline__ void st8(bf16_t* p, const float* f) { *reinterpret_cast<u32x4*>(p) = pack8(f); }
+
+// ------------------------------------------------------------------ RMSNorm forward
+// RES = false: y = rms(x; w)                 (Gemma2RMSNorm.forward, modeling_gemma2.py:69-74)
+// RES = true : h = bf16(res + bf16(rms(x; w)))  (decoder residual, :489-490 / :495-496)
+template <bool RES>
+__global__ __launch_bounds__(NTH) void rms_fwd_kernel(int64_t N, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
+                                                      float eps, bf16_t* __restrict__ y, float* __restrict__ rstd_out) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int nch = (int)(N >> 3);
+  const bf16_t* xr = x + row * N;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      ld8(xr + ch * 8, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float rstd = rsqrtf(ss / (float)N + eps);
+  if (threadIdx.x == 0 && rstd_out) rstd_out[row] = rstd;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float wf[8], o[8];
+      ld8(w + ch * 8, wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] * rstd) * (1.0f + wf[j]);
+      if (RES) {
+        float r[8];
+        ld8(res + row * N + ch * 8, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r[j] + round_bf(o[j]);
+      }
+      st8(y + row * N + ch * 8, o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ RMSNorm backward
+// dx = rstd*(g - xhat*mean(g*xhat)) + dres,  g = dy*(1+w), xhat = x*rstd;  dw += sum_rows dy*xhat
+__global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ w, const float* __restrict__ rstd,
+                                                      const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dres,
+                                                      bf16_t* __restrict__ dx, float* __restrict__ dw_partial) {
+  __shared__ float red[16];
+  const int nch = (int)(N >> 3);
+  float wf[MAXC][8], dwacc[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[c][j] = 0.f;
+    if (ch < nch) ld8(w + ch * 8, wf[c]);
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * RPB;
+  for (int rr = 0; rr < RPB; ++rr) {
+    const int64_t row = r0 + rr;
+    if (row >= rows) break;
+    const float rs = rstd[row];
+    float xv[MAXC][8], gv[MAXC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float d[8];
+        ld8(x + row * N + ch * 8, xv[c]);
+        ld8(dy + row * N + ch * 8, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float xh = xv[c][j] * rs;
+          xv[c][j] = xh;
+          gv[c][j] = d[j] * (1.0f + wf[c][j]);
+          dot += gv[c][j] * xh;
+          dwacc[c][j] += d[j] * xh;
+        }
+      }
+    }
+    dot = block_sum(dot, red) / (float)N;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gv[c][j] - xv[c][j] * dot);
+        if (dres) {
+          float r[8];
+          ld8(dres + row * N + ch * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]) + r[j];
+        }
+        st8(dx + row * N + ch * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float* p = dw_partial + (int64_t)blockIdx.x * N + ch * 8;
+      *reinterpret_cast<f32x4*>(p) = f32x4{dwacc[c][0], dwacc[c][1], dwacc[c][2], dwacc[c][3]};
+      *reinterpret_cast<f32x4*>(p + 4) = f32x4{dwacc[c][4], dwacc[c][5], dwacc[c][6], dwacc[c][7]};
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm
+__global__ __launch_bounds__(NTH) void ln_fwd_kernel(int64_t N, const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                     float eps, bf16_t* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int nch = (int)(N >> 3);
+  float v[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      ld8(x + row * N + ch * 8, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    }
+  }
+  const float mean = block_sum(s, red) / (float)N;
+  float s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = v[c][j] - mean;
+        s2 += d * d;
+      }
+  }
+  const float var = block_sum(s2, red) / (float)N;
+  const float rstd = rsqrtf(var + eps);
+  if (threadIdx.x == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float wf[8], bf[8], o[8];
+      ld8(w + ch * 8, wf);
+      ld8(b + ch * 8, bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wf[j] + bf[j];
+      st8(y + row * N + ch * 8, o);
+    }
+  }
+}
+
+// dx = rstd*(g - mean(g) - xhat*mean(g*xhat)) + dres, g = dy*w ; dw += dy*xhat ; db += dy
+__global__ __launch_bounds__(NTH) void ln_bwd_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const bf16_t* __restrict__ dy,
+                                                     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                     float* __restrict__ dwb_partial) {
+  __shared__ float red[16];
+  const int nch = (int)(N >> 3);
+  float wf[MAXC][8], dwacc[MAXC][8], dbacc[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dwacc[c][j] = dbacc[c][j] = 0.f;
+    if (ch < nch) ld8(w + ch * 8, wf[c]);
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * RPB;
+  for (int rr = 0; rr < RPB; ++rr) {
+    const int64_t row = r0 + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXC][8], gv[MAXC][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float d[8];
+        ld8(x + row * N + ch * 8, xh[c]);
+        ld8(dy + row * N + ch * 8, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xh[c][j] - mu) * rs;
+          gv[c][j] = d[j] * wf[c][j];
+          sg += gv[c][j];
+          sgx += gv[c][j] * xh[c][j];
+          dwacc[c][j] += d[j] * xh[c][j];
+          dbacc[c][j] += d[j];
+        }
+      }
+    }
+    sg = block_sum(sg, red) / (float)N;
+    sgx = block_sum(sgx, red) / (float)N;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gv[c][j] - sg - xh[c][j] * sgx);
+        if (dres) {
+          float r[8];
+          ld8(dres + row * N + ch * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]) + r[j];
+        }
+        st8(dx + row * N + ch * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float* p = dwb_partial + (int64_t)blockIdx.x * 2 * N + ch * 8;
+      for (int j = 0; j < 8; ++j) {
+        p[j] = dwacc[c][j];
+        p[N + j] = dbacc[c][j];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ column reductions
+__global__ void colsum_f32_kernel(int64_t P, int64_t N, const float* __restrict__ in, bf16_t* __restrict__ out,
+                                  int acc) {
+  int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < P; ++p) s += in[p * N + n];
+  if (acc) s += bf2f(out[n]);
+  out[n] = f2bf(s);
+}
+
+// stage 1: 64 row-chunks, each thread a column pair of 8 consecutive columns
+__global__ void colsum_bf16_stage1(int64_t M, int64_t N, const bf16_t* __restrict__ x, int64_t ldx,
+                                   float* __restrict__ ws) {
+  const int64_t nch = (N + 7) >> 3;
+  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int part = blockIdx.y;  // 0..63
+  if (ch >= nch) return;
+  const int64_t rows_per = (M + 63) / 64;
+  const int64_t r0 = part * rows_per, r1 = min(M, r0 + rows_per);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t n0 = ch * 8;
+  const bool full = n0 + 8 <= N;
+  for (int64_t r = r0; r < r1; ++r) {
+    const bf16_t* p = x + r * ldx + n0;
+    if (full) {
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4*>(p), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    } else {
+      for (int j = 0; j < 8 && n0 + j < N; ++j) s[j] += bf2f(p[j]);
+    }
+  }
+  for (int j = 0; j < 8 && n0 + j < N; ++j) ws[part * N + n0 + j] = s[j];
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+}  // namespace
+
+extern "C" int svla_rmsnorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, float eps, void* y,
+                                float* rstd, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "rmsnorm: bad N=%lld", (long long)N);
+  SVLA_CHECK_ARG(x && w && y && al16(x) && al16(w) && al16(y), "rmsnorm: null/misaligned pointer");
+  hipLaunchKernelGGL((rms_fwd_kernel<false>), dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)x, (const bf16_t*)nullptr, (const bf16_t*)w, eps, (bf16_t*)y, rstd);
+  return svla::check_launch("rmsnorm_fwd");
+}
+
+extern "C" int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w,
+                                    float eps, void* h, float* rstd, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "add_rmsnorm: bad N");
+  SVLA_CHECK_ARG(res && yin && w && h && al16(res) && al16(yin) && al16(h), "add_rmsnorm: null/misaligned");
+  hipLaunchKernelGGL((rms_fwd_kernel<true>), dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w, eps, (bf16_t*)h, rstd);
+  return svla::check_launch("add_rmsnorm_fwd");
+}
+
+extern "C" int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* rstd,
+                                const void* dy, const void* dres, void* dx, float* dw_partial, int64_t* n_partial,
+                                void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "rmsnorm_bwd: bad N");
+  SVLA_CHECK_ARG(x && w && rstd && dy && dx && dw_partial, "rmsnorm_bwd: null pointer");
+  const int64_t nb = (rows + RPB - 1) / RPB;
+  if (n_partial) *n_partial = nb;
+  hipLaunchKernelGGL(rms_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                     (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                     dw_partial);
+  return svla::check_launch("rmsnorm_bwd");
+}
+
+extern "C" int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
+                                  void* y, float* mean, float* rstd, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "layernorm: bad N");
+  SVLA_CHECK_ARG(x && w && b && y && mean && rstd, "layernorm: null pointer");
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N, (const bf16_t*)x,
+                     (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)y, mean, rstd);
+  return svla::check_launch("layernorm_fwd");
+}
+
+extern "C" int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* mean,
+                                  const float* rstd, const void* dy, const void* dres, void* dx, float* dwb_partial,
+                                  int64_t* n_partial, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "layernorm_bwd: bad N");
+  SVLA_CHECK_ARG(x && w && mean && rstd && dy && dx && dwb_partial, "layernorm_bwd: null pointer");
+  const int64_t nb = (rows + RPB - 1) / RPB;
+  if (n_partial) *n_partial = nb;
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                     (const bf16_t*)x, (const bf16_t*)w, mean, rstd, (const bf16_t*)dy, (const bf16_t*)dres,
+                     (bf16_t*)dx, dwb_partial);
+  return svla::check_launch("layernorm_bwd");
+}
+
+extern "C" int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate,
+                               void* stream) {
+  SVLA_CHECK_ARG(P > 0 && N > 0 && in && out_bf16, "colsum_f32: bad args");
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, P,
+                     N, in, (bf16_t*)out_bf16, accumulate);
+  return svla::check_launch("colsum_f32");
+}
+
+extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16,
+                                int32_t accumulate, float* workspace, void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && x && out_bf16 && workspace && ldx % 8 == 0 && al16(x), "colsum_bf16: bad args");
+  const int64_t nch = (N + 7) / 8;
+  hipLaunchKernelGGL(colsum_bf16_stage1, dim3((unsigned)((nch + 255) / 256), 64), dim3(256), 0,
+                     (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace);
+  if (int rc = svla::check_launch("colsum_bf16")) return rc;
+  return svla_colsum_f32(64, N, workspace, out_bf16, accumulate, stream);
+}

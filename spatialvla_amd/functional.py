@@ -1,0 +1,578 @@
+"""autograd Functions of the SpatialVLA hot path, each a thin shell over libsvla kernels.
+
+Every Function documents the reference op(s) it replaces.  All tensors are bf16, 2-D row-major
+[rows, features] on the GPU.  Weight gradients go either to freshly allocated tensors returned to
+autograd (standard HF/torch semantics) or — when the training engine has attached a flat-buffer
+view as `param._svla_grad` — straight into that view (accumulating when `param._svla_accum`),
+in which case autograd receives None for that parameter (no extra copy, no autograd add).
+"""
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from . import kernels as K
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+# ------------------------------------------------------------------------------------ helpers
+def _empty(*shape, dtype=BF16, like=None, device=None):
+    return torch.empty(*shape, dtype=dtype, device=like.device if like is not None else device)
+
+
+def _grad_dest(p: torch.Tensor, needed: bool):
+    """(buffer, accumulate, value returned to autograd) for the gradient of parameter p."""
+    if not needed:
+        return None, False, None
+    g = getattr(p, "_svla_grad", None)
+    if g is not None:
+        return g, bool(getattr(p, "_svla_accum", False)), None
+    buf = torch.empty_like(p)
+    return buf, False, buf
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ------------------------------------------------------------------------------------ norms
+class RMSNormFn(torch.autograd.Function):
+    """Gemma2RMSNorm.forward (reference model/modeling_gemma2.py:69-74)."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        x = _c(x)
+        y = torch.empty_like(x)
+        rstd = _empty(x.shape[0], dtype=F32, like=x)
+        K.rmsnorm_fwd(x, w, eps, y, rstd)
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[1])
+        K.rmsnorm_bwd(x, w, rstd, _c(dy), None, dx, dw, dw_accumulate=acc)
+        return dx, ret, None
+
+
+class AddRMSNormFn(torch.autograd.Function):
+    """h = res + Gemma2RMSNorm(y)  (decoder-layer sandwich norm + residual, modeling_gemma2.py:489-496)."""
+
+    @staticmethod
+    def forward(ctx, res, y, w, eps):
+        res, y = _c(res), _c(y)
+        h = torch.empty_like(y)
+        rstd = _empty(y.shape[0], dtype=F32, like=y)
+        K.add_rmsnorm_fwd(res, y, w, eps, h, rstd)
+        ctx.save_for_backward(y, w, rstd)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        y, w, rstd = ctx.saved_tensors
+        dh = _c(dh)
+        dy = torch.empty_like(y)
+        dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[2])
+        K.rmsnorm_bwd(y, w, rstd, dh, None, dy, dw, dw_accumulate=acc)
+        return dh, dy, ret, None
+
+
+class LayerNormFn(torch.autograd.Function):
+    """nn.LayerNorm (SigLIP layer_norm1/2/post_layernorm [3p]; Ego3D head.1, modeling_spatialvla.py:61)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        x = _c(x)
+        y = torch.empty_like(x)
+        mean = _empty(x.shape[0], dtype=F32, like=x)
+        rstd = _empty(x.shape[0], dtype=F32, like=x)
+        K.layernorm_fwd(x, w, b, eps, y, mean, rstd)
+        ctx.save_for_backward(x, w, b, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, mean, rstd = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        dw, accw, retw = _grad_dest(w, ctx.needs_input_grad[1])
+        db, accb, retb = _grad_dest(b, ctx.needs_input_grad[2])
+        if dw is not None and db is not None and accw != accb:
+            raise RuntimeError("LayerNorm weight/bias grads must share accumulate mode")
+        K.layernorm_bwd(x, w, mean, rstd, _c(dy), None, dx, dw, db, accumulate=accw)
+        return dx, retw, retb, None
+
+
+class ReLUFn(torch.autograd.Function):
+    """nn.ReLU (Ego3D position_embedding_head.2, modeling_spatialvla.py:62)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        y = torch.empty_like(x)
+        K.relu_fwd(x, y)
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        K.relu_bwd(x, _c(dy), dx)
+        return dx
+
+
+# ------------------------------------------------------------------------------------ linear
+def _bias_grad(dy, b, needed):
+    db, acc, ret = _grad_dest(b, needed)
+    if db is not None:
+        K.colsum_bf16(dy, db, accumulate=acc)
+    return ret
+
+
+class LinearFn(torch.autograd.Function):
+    """y = bf16(bf16(x W^T + b) * post_scale) — nn.Linear (+ the projector's / sqrt(H),
+    modeling_spatialvla.py:124,331-332).  With `res`, y = bf16(bf16(x W^T + b) + res): the residual add
+    fused in the epilogue (SigLIP encoder residuals; Ego3D + vision features, modeling_spatialvla.py:328).
+    K may be padded (`k_pad`): the weight is zero-padded per call (patchify, Ego3D 204-wide input)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, res, post_scale):
+        x = _c(x)
+        M = x.shape[0]
+        N, Kw = w.shape
+        wk = w
+        if x.shape[1] != Kw:  # zero-padded reduction dim (ld must be a multiple of 8)
+            wk = torch.zeros(N, x.shape[1], dtype=BF16, device=w.device)
+            wk[:, :Kw] = w
+        y = _empty(M, N, like=x)
+        if res is not None:
+            K.linear_fwd(x, [wk], y, kind=L.EPI_BIAS_RESID, bias=b, in0=_c(res))
+        elif b is not None:
+            K.linear_fwd(x, [wk], y, kind=L.EPI_BIAS, bias=b, alpha=post_scale)
+        else:
+            K.linear_fwd(x, [wk], y, kind=L.EPI_STORE, alpha=post_scale)
+        ctx.save_for_backward(x, w, b)
+        ctx.post_scale = post_scale
+        ctx.has_res = res is not None
+        ctx.wk = wk if wk is not w else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b = ctx.saved_tensors
+        dy = _c(dy)
+        if ctx.post_scale != 1.0:
+            # y = bf16(z * s): dz = bf16(dy * s) (autograd of the reference's division)
+            dy = (dy * ctx.post_scale).to(BF16)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty(*x.shape, like=x)
+            K.linear_dgrad(dy, [ctx.wk if ctx.wk is not None else w], dx)
+        retw = None
+        if ctx.needs_input_grad[1]:
+            if x.shape[1] != w.shape[1]:
+                tmp = _empty(w.shape[0], x.shape[1], like=x)
+                K.linear_wgrad(dy, x, [tmp])
+                dw, acc, retw = _grad_dest(w, True)
+                if acc:
+                    dw.add_(tmp[:, :w.shape[1]])
+                else:
+                    dw.copy_(tmp[:, :w.shape[1]])
+            else:
+                dw, acc, retw = _grad_dest(w, True)
+                K.linear_wgrad(dy, x, [dw], accumulate=acc)
+        retb = _bias_grad(dy, b, b is not None and ctx.needs_input_grad[2])
+        dres = dy if ctx.has_res else None
+        return dx, retw, retb, dres, None
+
+
+# ------------------------------------------------------------------------------------ Gemma2 blocks
+@dataclass
+class GemmaAttnCfg:
+    B: int
+    L: int
+    Hq: int
+    Hkv: int
+    D: int
+    scale: float
+    softcap: float
+    window: int
+
+
+class GemmaAttentionFn(torch.autograd.Function):
+    """Gemma2Attention.forward (modeling_gemma2.py:364-413): q/k/v projections, rotary embedding
+    (:95-154), eager prefix-LM GQA attention with logit softcap (:169-195), o_proj — as one fused
+    QKV GEMM, one attention kernel with RoPE applied on load, one O GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg):
+        x = _c(x)
+        M, H = x.shape
+        qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
+        qkv = _empty(M, qd + 2 * kd, like=x)
+        K.linear_fwd(x, [wq, wk, wv], qkv)
+        attn = _empty(M, qd, like=x)
+        lse = _empty(cfg.B, cfg.Hq, cfg.L, dtype=F32, like=x)
+        a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
+                        qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window,
+                        cos, sin)
+        K.attn_fwd(a, attn, lse)
+        out = _empty(M, wo.shape[0], like=x)
+        K.linear_fwd(attn, [wo], out)
+        ctx.save_for_backward(x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class = ctx.saved_tensors
+        cfg = ctx.cfg
+        dout = _c(dout)
+        M = x.shape[0]
+        qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
+        dattn = _empty(M, qd, like=x)
+        K.linear_dgrad(dout, [wo], dattn)
+        dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
+        if dwo is not None:
+            K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
+        dqkv = torch.empty_like(qkv)
+        a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
+                        qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window,
+                        cos, sin)
+        ld = dqkv.stride(0)
+        K.attn_bwd(a, attn, dattn, lse, dqkv[:, :qd], ld, dqkv[:, qd:qd + kd], ld, dqkv[:, qd + kd:], ld)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            K.linear_dgrad(dqkv, [wq, wk, wv], dx)
+        rets = []
+        dests = [_grad_dest(w, ctx.needs_input_grad[1 + i]) for i, w in enumerate((wq, wk, wv))]
+        if all(d[0] is not None for d in dests) and len({d[1] for d in dests}) == 1:
+            K.linear_wgrad(dqkv, x, [d[0] for d in dests], accumulate=dests[0][1])
+        else:
+            off = 0
+            for (dw, acc_i, _), w in zip(dests, (wq, wk, wv)):
+                n = w.shape[0]
+                if dw is not None:
+                    K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
+                off += n
+        rets = [d[2] for d in dests]
+        return (dx, *rets, ret_wo, None, None, None, None)
+
+
+class GemmaMLPFn(torch.autograd.Function):
+    """Gemma2MLP.forward (modeling_gemma2.py:91-92): down(gelu_tanh(gate x) * up x) — gate/up as one
+    GEMM with the GeGLU in its epilogue; backward fuses the GeGLU derivative into the dH GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, wg, wu, wd):
+        x = _c(x)
+        M = x.shape[0]
+        I = wg.shape[0]
+        h = _empty(M, I, like=x)
+        g = _empty(M, I, like=x)
+        u = _empty(M, I, like=x)
+        K.linear_geglu_fwd(x, wg, wu, h, g, u)
+        out = _empty(M, wd.shape[0], like=x)
+        K.linear_fwd(h, [wd], out)
+        ctx.save_for_backward(x, wg, wu, wd, g, u, h)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, wg, wu, wd, g, u, h = ctx.saved_tensors
+        dout = _c(dout)
+        M, I = g.shape
+        dwd, acc, ret_wd = _grad_dest(wd, ctx.needs_input_grad[3])
+        if dwd is not None:
+            K.linear_wgrad(dout, h, [dwd], accumulate=acc)
+        dgu = _empty(M, 2 * I, like=x)
+        K.linear_dgrad(dout, [wd], dgu[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=dgu[:, :I], out2=dgu[:, I:])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            K.linear_dgrad(dgu, [wg, wu], dx)
+        dg_, accg, retg = _grad_dest(wg, ctx.needs_input_grad[1])
+        du_, accu, retu = _grad_dest(wu, ctx.needs_input_grad[2])
+        if dg_ is not None and du_ is not None and accg == accu:
+            K.linear_wgrad(dgu, x, [dg_, du_], accumulate=accg)
+        else:
+            if dg_ is not None:
+                K.linear_wgrad(_c(dgu[:, :I]), x, [dg_], accumulate=accg)
+            if du_ is not None:
+                K.linear_wgrad(_c(dgu[:, I:]), x, [du_], accumulate=accu)
+        return dx, retg, retu, ret_wd
+
+
+# ------------------------------------------------------------------------------------ SigLIP blocks
+@dataclass
+class SiglipAttnCfg:
+    B: int
+    L: int
+    H: int
+    D: int
+    scale: float
+
+
+class SiglipAttentionFn(torch.autograd.Function):
+    """SiglipAttention.forward + encoder residual (transformers siglip [3p], called from
+    modeling_spatialvla.py:310): q/k/v (bias) as one GEMM, bidirectional softmax attention
+    (head_dim 72), out_proj with bias and the residual add fused in its epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, res, wq, bq, wk, bk, wv, bv, wo, bo, cfg: SiglipAttnCfg):
+        x, res = _c(x), _c(res)
+        M, Hd = x.shape
+        bqkv = torch.cat([bq, bk, bv])
+        qkv = _empty(M, 3 * Hd, like=x)
+        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_BIAS, bias=bqkv)
+        attn = _empty(M, Hd, like=x)
+        lse = _empty(cfg.B, cfg.H, cfg.L, dtype=F32, like=x)
+        a = K.attn_args(cfg.B, cfg.L, cfg.H, cfg.H, cfg.D, qkv[:, :Hd], qkv.stride(0), qkv[:, Hd:2 * Hd],
+                        qkv.stride(0), qkv[:, 2 * Hd:], qkv.stride(0), cfg.scale)
+        K.attn_fwd(a, attn, lse)
+        out = _empty(M, Hd, like=x)
+        K.linear_fwd(attn, [wo], out, kind=L.EPI_BIAS_RESID, bias=bo, in0=res)
+        ctx.save_for_backward(x, wq, bq, wk, bk, wv, bv, wo, bo, qkv, attn, lse)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, wq, bq, wk, bk, wv, bv, wo, bo, qkv, attn, lse = ctx.saved_tensors
+        cfg = ctx.cfg
+        dout = _c(dout)
+        M, Hd = x.shape
+        nig = ctx.needs_input_grad
+        dattn = torch.empty_like(attn)
+        K.linear_dgrad(dout, [wo], dattn)
+        dwo, acc, ret_wo = _grad_dest(wo, nig[8])
+        if dwo is not None:
+            K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
+        ret_bo = _bias_grad(dout, bo, nig[9])
+        dqkv = torch.empty_like(qkv)
+        a = K.attn_args(cfg.B, cfg.L, cfg.H, cfg.H, cfg.D, qkv[:, :Hd], qkv.stride(0), qkv[:, Hd:2 * Hd],
+                        qkv.stride(0), qkv[:, 2 * Hd:], qkv.stride(0), cfg.scale)
+        ld = dqkv.stride(0)
+        K.attn_bwd(a, attn, dattn, lse, dqkv[:, :Hd], ld, dqkv[:, Hd:2 * Hd], ld, dqkv[:, 2 * Hd:], ld)
+        dx = torch.empty_like(x) if nig[0] else None
+        if dx is not None:
+            K.linear_dgrad(dqkv, [wq, wk, wv], dx)
+        rets = []
+        for i, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv))):
+            dw, accw, retw = _grad_dest(w, nig[2 + 2 * i])
+            seg = _c(dqkv[:, i * Hd:(i + 1) * Hd])
+            if dw is not None:
+                K.linear_wgrad(seg, x, [dw], accumulate=accw)
+            retb = _bias_grad(seg, b, nig[3 + 2 * i])
+            rets += [retw, retb]
+        return (dx, dout, *rets, ret_wo, ret_bo, None)
+
+
+class SiglipMLPFn(torch.autograd.Function):
+    """SiglipMLP + residual: res + fc2(gelu_tanh(fc1 x)) (transformers siglip [3p]); fc1 bias+GELU and
+    fc2 bias+residual fused in GEMM epilogues, GELU derivative fused into the fc2 dgrad epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, res, w1, b1, w2, b2):
+        x, res = _c(x), _c(res)
+        M = x.shape[0]
+        I = w1.shape[0]
+        pre = _empty(M, I, like=x)
+        act = _empty(M, I, like=x)
+        K.linear_fwd(x, [w1], act, kind=L.EPI_BIAS_GELU, bias=b1, out1=pre)
+        out = _empty(M, w2.shape[0], like=x)
+        K.linear_fwd(act, [w2], out, kind=L.EPI_BIAS_RESID, bias=b2, in0=res)
+        ctx.save_for_backward(x, w1, b1, w2, b2, pre, act)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w1, b1, w2, b2, pre, act = ctx.saved_tensors
+        dout = _c(dout)
+        nig = ctx.needs_input_grad
+        dw2, acc2, ret_w2 = _grad_dest(w2, nig[4])
+        if dw2 is not None:
+            K.linear_wgrad(dout, act, [dw2], accumulate=acc2)
+        ret_b2 = _bias_grad(dout, b2, nig[5])
+        dpre = torch.empty_like(pre)
+        K.linear_dgrad(dout, [w2], dpre, kind=L.EPI_GELU_BWD, in0=pre)
+        dx = torch.empty_like(x) if nig[0] else None
+        if dx is not None:
+            K.linear_dgrad(dpre, [w1], dx)
+        dw1, acc1, ret_w1 = _grad_dest(w1, nig[2])
+        if dw1 is not None:
+            K.linear_wgrad(dpre, x, [dw1], accumulate=acc1)
+        ret_b1 = _bias_grad(dpre, b1, nig[3])
+        return dx, dout, ret_w1, ret_b1, ret_w2, ret_b2
+
+
+class PatchEmbedFn(torch.autograd.Function):
+    """SiglipVisionEmbeddings.forward (transformers siglip [3p]): Conv2d(3, H, k=s=14) + bias +
+    position embedding, as im2col + one GEMM whose epilogue adds bias and position rows."""
+
+    @staticmethod
+    def forward(ctx, pix, w, b, pos, patch):
+        pix = _c(pix)
+        B, C, S, _ = pix.shape
+        np_ = (S // patch) ** 2
+        Kc = C * patch * patch
+        Kp = K.round_up(Kc, 8)
+        cols = _empty(B * np_, Kp, like=pix)
+        K.im2col_patch(pix, patch, cols)
+        w2 = w.reshape(w.shape[0], Kc)
+        wk = torch.zeros(w.shape[0], Kp, dtype=BF16, device=w.device)
+        wk[:, :Kc] = w2
+        posx = pos.unsqueeze(0).expand(B, np_, pos.shape[1]).reshape(B * np_, pos.shape[1])
+        y = _empty(B * np_, w.shape[0], like=pix)
+        K.linear_fwd(cols, [wk], y, kind=L.EPI_BIAS_RESID, bias=b, in0=_c(posx))
+        ctx.save_for_backward(cols, w, b, pos)
+        ctx.B, ctx.np = B, np_
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, w, b, pos = ctx.saved_tensors
+        dy = _c(dy)
+        Kc = w[0].numel()
+        rw = None
+        if ctx.needs_input_grad[1]:
+            tmp = _empty(w.shape[0], cols.shape[1], like=cols)
+            K.linear_wgrad(dy, cols, [tmp])
+            dw, acc, rw = _grad_dest(w, True)
+            src = tmp[:, :Kc].reshape(w.shape)
+            dw.add_(src) if acc else dw.copy_(src)
+        rb = _bias_grad(dy, b, ctx.needs_input_grad[2])
+        rp = None
+        if ctx.needs_input_grad[3]:
+            dp, acc, rp = _grad_dest(pos, True)
+            K.colsum_bf16(dy.view(ctx.B, ctx.np * pos.shape[1]), dp.view(-1), accumulate=acc)
+        return None, rw, rb, rp, None
+
+
+class EmbedMergeFn(torch.autograd.Function):
+    """Embedding merge of SpatialVLAForConditionalGeneration.forward (modeling_spatialvla.py:361-387)
+    times the Gemma2 normalizer (modeling_gemma2.py:741-742): token embeddings (frozen table), spatial
+    action-token embeddings, image features scattered into the <image> slots in (b, t) order."""
+
+    @staticmethod
+    def forward(ctx, ids, img_index, img_feats, spatial_w, embed_w, a0, normalizer, sort_rows, offsets):
+        ids = _c(ids).view(-1)
+        H = embed_w.shape[1]
+        out = _empty(ids.numel(), H, like=embed_w)
+        na = spatial_w.shape[0] if spatial_w is not None else 0
+        K.embed_merge(ids, img_index, embed_w, spatial_w, a0, na, img_feats, normalizer, out)
+        ctx.save_for_backward(ids, img_index, sort_rows, offsets, spatial_w, img_feats)
+        ctx.normalizer, ctx.na = normalizer, na
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, img_index, sort_rows, offsets, spatial_w, img_feats = ctx.saved_tensors
+        dout = _c(dout)
+        dimg = torch.empty_like(img_feats) if (img_feats is not None and ctx.needs_input_grad[2]) else None
+        dsp, acc, rsp = (None, False, None)
+        if spatial_w is not None and ctx.needs_input_grad[3]:
+            dsp, acc, rsp = _grad_dest(spatial_w, True)
+            if acc:
+                tmp = torch.empty_like(spatial_w)
+                K.embed_merge_bwd(ids, img_index, sort_rows, offsets, ctx.na, dout, ctx.normalizer, tmp, None)
+                dsp.add_(tmp)
+                dsp = None
+        if dimg is not None or dsp is not None:
+            K.embed_merge_bwd(ids, img_index, sort_rows, offsets, ctx.na, dout, ctx.normalizer, dsp, dimg)
+        return None, None, dimg, rsp, None, None, None, None, None
+
+
+class LMHeadCEFn(torch.autograd.Function):
+    """lm_head + final logit softcap (modeling_gemma2.py:993-997) + the shifted, masked cross-entropy of
+    SpatialVLAForConditionalGeneration.forward (modeling_spatialvla.py:415-430).  Logits are written once
+    in bf16 (row stride padded to a multiple of 64 columns); softmax statistics come from the GEMM
+    epilogue, so the fp32 [B, L, V] tensor of the reference is never materialised.
+    Returns (logits [M, V] view, loss scalar fp32); argmax / lse are stashed on ctx-owned tensors."""
+
+    @staticmethod
+    def forward(ctx, h, w, target, cap, stash):
+        h = _c(h)
+        M = h.shape[0]
+        V = w.shape[0]
+        ldv = K.round_up(V, 64)
+        logits_buf = _empty(M, ldv, like=h)
+        ntn = K.ceil_div(V, 128)
+        stats = _empty(M, ntn, 3, dtype=F32, like=h)
+        K.linear_fwd(h, [w], logits_buf[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=stats, cap=cap)
+        lse = _empty(M, dtype=F32, like=h)
+        argmax = _empty(M, dtype=torch.int64, like=h)
+        loss_rows = _empty(M, dtype=F32, like=h)
+        loss2 = _empty(2, dtype=F32, like=h)
+        K.ce_finalize(V, ntn, stats, logits_buf[:, :V], target, lse, argmax, loss_rows, loss2)
+        stash["argmax"] = argmax
+        stash["lse"] = lse
+        stash["n_valid"] = loss2[1:2]
+        ctx.save_for_backward(h, w, logits_buf, lse, target, loss2)
+        ctx.cap, ctx.V = cap, V
+        ctx.mark_non_differentiable(logits_buf)
+        return logits_buf[:, :V], loss2[0]
+
+    @staticmethod
+    def backward(ctx, dlogits_unused, dloss):
+        h, w, logits_buf, lse, target, loss2 = ctx.saved_tensors
+        M, ldv = logits_buf.shape
+        V = ctx.V
+        gscale = (dloss.float() / torch.clamp(loss2[1], min=1.0)).reshape(1).contiguous()
+        dlog = _empty(M, ldv, like=h)
+        K.ce_bwd(V, logits_buf[:, :V], lse, target, ctx.cap, gscale, dlog)
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = torch.empty_like(h)
+            # K dimension = V: B operand = W [V, H] read RC with rows up to V (tail masked), A = dlog (zero-padded)
+            A = K._operand([dlog[:, :V]], L.LAYOUT_KC)
+            Bop = K._operand([w], L.LAYOUT_RC)
+            K.gemm(M, w.shape[1], V, A, Bop, [dh], [0], dh.stride(0), K._epi(L.EPI_STORE))
+        dw, acc, rw = _grad_dest(w, ctx.needs_input_grad[1])
+        if dw is not None:
+            K.linear_wgrad(dlog[:, :V], h, [dw], accumulate=acc)
+        return dh, rw, None, None, None
+
+
+# ------------------------------------------------------------------------------------ attention plug-in
+def hip_attention(q, k, v, scale, softcap=0.0, kv_class=None, window=0):
+    """Reference plug-in signature adapter (GEMMA2_ATTENTION_FUNCTION, modeling_gemma2.py:317-322):
+    q [B, Hq, L, D], k/v [B, Hkv, L, D] (post-RoPE) -> [B, L, Hq, D].  Differentiable."""
+    return _PluginAttnFn.apply(q, k, v, float(scale), float(softcap or 0.0), kv_class, int(window or 0))
+
+
+class _PluginAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, softcap, kv_class, window):
+        B, Hq, Lq, D = q.shape
+        Hkv = k.shape[1]
+        qt = q.transpose(1, 2).contiguous().view(B * Lq, Hq * D)
+        kt = k.transpose(1, 2).contiguous().view(B * Lq, Hkv * D)
+        vt = v.transpose(1, 2).contiguous().view(B * Lq, Hkv * D)
+        out = _empty(B * Lq, Hq * D, like=q)
+        lse = _empty(B, Hq, Lq, dtype=F32, like=q)
+        a = K.attn_args(B, Lq, Hq, Hkv, D, qt, qt.stride(0), kt, kt.stride(0), vt, vt.stride(0), scale, softcap,
+                        kv_class, window)
+        K.attn_fwd(a, out, lse)
+        ctx.save_for_backward(qt, kt, vt, out, lse, kv_class)
+        ctx.meta = (B, Lq, Hq, Hkv, D, scale, softcap, window)
+        return out.view(B, Lq, Hq, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        qt, kt, vt, out, lse, kv_class = ctx.saved_tensors
+        B, Lq, Hq, Hkv, D, scale, softcap, window = ctx.meta
+        do = _c(dout).view(B * Lq, Hq * D)
+        dq, dk, dv = torch.empty_like(qt), torch.empty_like(kt), torch.empty_like(vt)
+        a = K.attn_args(B, Lq, Hq, Hkv, D, qt, qt.stride(0), kt, kt.stride(0), vt, vt.stride(0), scale, softcap,
+                        kv_class, window)
+        K.attn_bwd(a, out, do, lse, dq, dq.stride(0), dk, dk.stride(0), dv, dv.stride(0))
+        tr = lambda t, H: t.view(B, Lq, H, D).transpose(1, 2)  # noqa: E731
+        return tr(dq, Hq), tr(dk, Hkv), tr(dv, Hkv), None, None, None, None

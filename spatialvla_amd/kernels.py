@@ -1,0 +1,341 @@
+"""Tensor-level wrappers over the libsvla C-ABI (include/svla.h).
+
+Every function here takes torch tensors that already live on the GPU, validates the shapes the
+kernel assumes (so a bad call raises on the host instead of faulting the device), and launches on
+torch's current HIP stream.  No function here has a non-HIP path.
+"""
+import ctypes
+import math
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib as L
+
+BF16 = torch.bfloat16
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _req(cond: bool, msg: str):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _chk_bf16(t: torch.Tensor, name: str):
+    _req(t.is_cuda and t.dtype == BF16, f"{name}: expected a bf16 CUDA tensor, got {t.dtype} on {t.device}")
+
+
+def _ld(t: torch.Tensor) -> int:
+    _req(t.dim() == 2 and t.stride(1) == 1, "expected a 2-D row-major matrix view")
+    return t.stride(0)
+
+
+# ---------------------------------------------------------------------------------------- GEMM
+def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUTER, starts=None) -> L.Operand:
+    op = L.Operand()
+    ld = _ld(mats[0])
+    for i, m in enumerate(mats):
+        _chk_bf16(m, "gemm operand")
+        _req(_ld(m) == ld, "gemm: all segments of an operand need the same leading dimension")
+        op.ptr[i] = m.data_ptr()
+    op.nseg = len(mats)
+    op.seg_dim = seg_dim
+    op.layout = layout
+    op.ld = ld
+    if starts is not None:
+        for i, s in enumerate(starts):
+            op.seg_start[i] = int(s)
+    return op
+
+
+def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=None, in1=None, out1=None,
+         out2=None, row_stats=None) -> L.Epilogue:
+    e = L.Epilogue()
+    e.kind = kind
+    e.accumulate = 1 if accumulate else 0
+    e.alpha = alpha
+    e.cap = cap
+    e.bias = _ptr(bias)
+    if in0 is not None:
+        e.in0, e.ld_in0 = in0.data_ptr(), _ld(in0)
+    if in1 is not None:
+        e.in1, e.ld_in1 = in1.data_ptr(), _ld(in1)
+    if out1 is not None:
+        e.out1, e.ld_out1 = out1.data_ptr(), _ld(out1)
+    if out2 is not None:
+        e.out2, e.ld_out2 = out2.data_ptr(), _ld(out2)
+    e.row_stats = _ptr(row_stats)
+    return e
+
+
+def gemm(M: int, N: int, K: int, A: L.Operand, B: L.Operand, c_mats: Sequence[Optional[torch.Tensor]],
+         c_starts: Sequence[int], ldc: int, epi: L.Epilogue):
+    n = len(c_mats)
+    cp = (ctypes.c_void_p * 4)(*([_ptr(c) for c in c_mats] + [None] * (4 - n)))
+    cs = (ctypes.c_int64 * 5)(*([int(s) for s in c_starts] + [0] * (5 - n)))
+    rc = L.lib().svla_gemm_bf16(M, N, K, ctypes.byref(A), ctypes.byref(B), cp, cs, n, ldc, ctypes.byref(epi),
+                                _stream())
+    L.check(rc, "svla_gemm_bf16")
+
+
+def _starts(sizes):
+    out, acc = [], 0
+    for s in sizes:
+        out.append(acc)
+        acc += s
+    return out, acc
+
+
+def _aligned(sizes, mult):
+    st, _ = _starts(sizes)
+    return all(s % mult == 0 for s in st)
+
+
+def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, kind=L.EPI_STORE, bias=None,
+               alpha=1.0, in0=None, out1=None, out2=None, row_stats=None, cap=0.0):
+    """out[M, sum N_i] = epi(x[M,K] @ cat(weights)^T).  Weights [N_i, K] are read in place."""
+    M, K = x.shape
+    sizes = [w.shape[0] for w in weights]
+    for w in weights:
+        _req(w.shape[1] == K, f"linear: weight K {w.shape[1]} != {K}")
+    if len(weights) > 1 and not _aligned(sizes, 128):
+        weights = [torch.cat(weights, 0)]
+        sizes = [weights[0].shape[0]]
+    starts, N = _starts(sizes)
+    A = _operand([x], L.LAYOUT_KC)
+    B = _operand(weights, L.LAYOUT_KC, L.SEG_OUTER, starts)
+    gemm(M, N, K, A, B, [out], [0], _ld(out),
+         _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap))
+
+
+def linear_geglu_fwd(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor, h: torch.Tensor, g: torch.Tensor,
+                     u: torch.Tensor):
+    """h = gelu_tanh(x Wg^T) * (x Wu^T); g, u saved (Gemma2MLP, modeling_gemma2.py:91-92)."""
+    M, K = x.shape
+    I = w_gate.shape[0]
+    _req(I % 64 == 0 and w_up.shape[0] == I, "geglu: intermediate size must be a multiple of 64")
+    A = _operand([x], L.LAYOUT_KC)
+    B = _operand([w_gate, w_up], L.LAYOUT_KC, L.SEG_GEGLU, [0, I])
+    gemm(M, 2 * I, K, A, B, [h], [0], _ld(h), _epi(L.EPI_GEGLU, out1=g, out2=u))
+
+
+def linear_dgrad(dy: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, kind=L.EPI_STORE, in0=None,
+                 in1=None, out1=None, out2=None, accumulate=False):
+    """out[M, K] = epi(dy[M, N] @ cat(weights)[N, K])."""
+    M, N = dy.shape
+    K = weights[0].shape[1]
+    sizes = [w.shape[0] for w in weights]
+    _req(sum(sizes) == N, "dgrad: weight rows must sum to dy columns")
+    if len(weights) > 1 and not _aligned(sizes, 64):
+        weights = [torch.cat(weights, 0)]
+        sizes = [N]
+    starts, _ = _starts(sizes)
+    A = _operand([dy], L.LAYOUT_KC)
+    B = _operand(weights, L.LAYOUT_RC, L.SEG_K, starts)
+    gemm(M, K, N, A, B, [out], [0], _ld(out), _epi(kind, accumulate=accumulate, in0=in0, in1=in1, out1=out1,
+                                                   out2=out2))
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, outs: List[torch.Tensor], accumulate=False):
+    """outs_i[N_i, K] = dy[:, seg_i]^T @ x  (weight gradients, written in place)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    sizes = [o.shape[0] for o in outs]
+    _req(sum(sizes) == N, "wgrad: out rows must sum to dy columns")
+    for o in outs:
+        _req(o.shape[1] == K and o.is_contiguous(), "wgrad: outputs must be contiguous [N_i, K]")
+    if len(outs) > 1 and not _aligned(sizes, 128):
+        tmp = torch.empty(N, K, dtype=BF16, device=dy.device)
+        linear_wgrad(dy, x, [tmp], accumulate=False)
+        off = 0
+        for o in outs:
+            seg = tmp[off:off + o.shape[0]]
+            if accumulate:
+                o.add_(seg)
+            else:
+                o.copy_(seg)
+            off += o.shape[0]
+        return
+    starts, _ = _starts(sizes)
+    A = _operand([dy], L.LAYOUT_RC)
+    B = _operand([x], L.LAYOUT_RC)
+    gemm(N, K, M, A, B, outs, starts, K, _epi(L.EPI_STORE, accumulate=accumulate))
+
+
+# ---------------------------------------------------------------------------------------- norms
+def rmsnorm_fwd(x, w, eps, y, rstd):
+    rows, N = x.shape
+    L.check(L.lib().svla_rmsnorm_fwd(rows, N, x.data_ptr(), w.data_ptr(), eps, y.data_ptr(), rstd.data_ptr(),
+                                     _stream()), "rmsnorm_fwd")
+
+
+def add_rmsnorm_fwd(res, yin, w, eps, h, rstd):
+    rows, N = yin.shape
+    L.check(L.lib().svla_add_rmsnorm_fwd(rows, N, res.data_ptr(), yin.data_ptr(), w.data_ptr(), eps, h.data_ptr(),
+                                         rstd.data_ptr(), _stream()), "add_rmsnorm_fwd")
+
+
+RPB = 16  # rows per block of the norm backward kernels (norms.hip)
+
+
+def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False):
+    rows, N = x.shape
+    nb = (rows + RPB - 1) // RPB
+    part = torch.empty(nb, N, dtype=torch.float32, device=x.device)
+    npart = ctypes.c_int64(0)
+    L.check(L.lib().svla_rmsnorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+                                     _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart), _stream()),
+            "rmsnorm_bwd")
+    if dw_out is not None:
+        L.check(L.lib().svla_colsum_f32(npart.value, N, part.data_ptr(), dw_out.data_ptr(), int(dw_accumulate),
+                                        _stream()), "colsum_f32")
+
+
+def layernorm_fwd(x, w, b, eps, y, mean, rstd):
+    rows, N = x.shape
+    L.check(L.lib().svla_layernorm_fwd(rows, N, x.data_ptr(), w.data_ptr(), b.data_ptr(), eps, y.data_ptr(),
+                                       mean.data_ptr(), rstd.data_ptr(), _stream()), "layernorm_fwd")
+
+
+def layernorm_bwd(x, w, mean, rstd, dy, dres, dx, dw_out, db_out, accumulate=False):
+    rows, N = x.shape
+    nb = (rows + RPB - 1) // RPB
+    part = torch.empty(nb, 2, N, dtype=torch.float32, device=x.device)
+    npart = ctypes.c_int64(0)
+    L.check(L.lib().svla_layernorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                       dy.data_ptr(), _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart),
+                                       _stream()), "layernorm_bwd")
+    # partial layout [nb][2][N]: reduce dw (stride 2N) and db separately via contiguous copies
+    if dw_out is not None:
+        pw = part[:, 0].contiguous()
+        L.check(L.lib().svla_colsum_f32(nb, N, pw.data_ptr(), dw_out.data_ptr(), int(accumulate), _stream()),
+                "colsum_f32")
+    if db_out is not None:
+        pb = part[:, 1].contiguous()
+        L.check(L.lib().svla_colsum_f32(nb, N, pb.data_ptr(), db_out.data_ptr(), int(accumulate), _stream()),
+                "colsum_f32")
+
+
+def colsum_bf16(x, out, accumulate=False):
+    M, N = x.shape
+    ws = torch.empty(64, N, dtype=torch.float32, device=x.device)
+    L.check(L.lib().svla_colsum_bf16(M, N, x.data_ptr(), _ld(x), out.data_ptr(), int(accumulate), ws.data_ptr(),
+                                     _stream()), "colsum_bf16")
+
+
+# ---------------------------------------------------------------------------------------- attention
+def attn_args(B, Lq, Hq, Hkv, D, q, ldq, k, ldk, v, ldv, scale, softcap=0.0, kv_class=None, window=0,
+              cos=None, sin=None) -> L.AttnArgs:
+    a = L.AttnArgs()
+    a.B, a.L, a.Hq, a.Hkv, a.D = B, Lq, Hq, Hkv, D
+    a.sliding_window = int(window)
+    a.scale = float(scale)
+    a.softcap = float(softcap or 0.0)
+    a.q, a.ldq, a.k, a.ldk, a.v, a.ldv = q.data_ptr(), ldq, k.data_ptr(), ldk, v.data_ptr(), ldv
+    a.kv_class = _ptr(kv_class)
+    if cos is not None:
+        a.rope_cos, a.rope_sin, a.rope_ld = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
+    return a
+
+
+def attn_fwd(a: L.AttnArgs, out: torch.Tensor, lse: torch.Tensor):
+    L.check(L.lib().svla_attn_fwd(ctypes.byref(a), out.data_ptr(), _ld(out), lse.data_ptr(), _stream()), "attn_fwd")
+
+
+def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):
+    ws = torch.empty(a.B * a.Hq * a.L, dtype=torch.float32, device=out.device)
+    L.check(L.lib().svla_attn_bwd(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),
+                                  lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv,
+                                  ws.data_ptr(), _stream()), "attn_bwd")
+
+
+# ---------------------------------------------------------------------------------------- glue
+def embed_merge(ids, img_index, embed, spatial, a0, na, img, normalizer, out):
+    rows = ids.numel()
+    H = embed.shape[1]
+    L.check(L.lib().svla_embed_merge(rows, H, ids.data_ptr(), _ptr(img_index), embed.data_ptr(), _ptr(spatial),
+                                     a0, na, _ptr(img), normalizer, out.data_ptr(), _stream()), "embed_merge")
+
+
+def embed_merge_bwd(ids, img_index, sorted_rows, offsets, na, dout, normalizer, dspatial, dimg):
+    rows, H = dout.shape
+    L.check(L.lib().svla_embed_merge_bwd(rows, H, ids.data_ptr(), _ptr(img_index), _ptr(sorted_rows),
+                                         _ptr(offsets), na, dout.data_ptr(), normalizer, _ptr(dspatial), _ptr(dimg),
+                                         _stream()), "embed_merge_bwd")
+
+
+def ego3d_encode(depth, kinv, uv_h, patch, reso, n_freqs, feat, xyz_out=None):
+    B, _, Hd, Wd = depth.shape
+    L.check(L.lib().svla_ego3d_encode(B, Hd, Wd, depth.data_ptr(), kinv.data_ptr(), uv_h.data_ptr(), patch, reso,
+                                      n_freqs, feat.data_ptr(), _ld(feat), _ptr(xyz_out), _stream()), "ego3d_encode")
+
+
+def im2col_patch(x, patch, cols):
+    B, _, S, _ = x.shape
+    L.check(L.lib().svla_im2col_patch(B, S, patch, x.data_ptr(), cols.data_ptr(), _ld(cols), _stream()),
+            "im2col_patch")
+
+
+def affine(x, scale, offset, out):
+    L.check(L.lib().svla_affine_bf16(x.numel(), x.data_ptr(), scale, offset, out.data_ptr(), _stream()), "affine")
+
+
+def relu_fwd(x, y):
+    L.check(L.lib().svla_relu_fwd(x.numel(), x.data_ptr(), y.data_ptr(), _stream()), "relu_fwd")
+
+
+def relu_bwd(x, dy, dx):
+    L.check(L.lib().svla_relu_bwd(x.numel(), x.data_ptr(), dy.data_ptr(), dx.data_ptr(), _stream()), "relu_bwd")
+
+
+def add(a, b, out):
+    L.check(L.lib().svla_add_bf16(a.numel(), a.data_ptr(), b.data_ptr(), out.data_ptr(), _stream()), "add")
+
+
+def ce_finalize(N, ntiles, row_stats, logits, target, lse, argmax, loss_rows, loss_out):
+    M = logits.shape[0]
+    L.check(L.lib().svla_ce_finalize(M, N, ntiles, row_stats.data_ptr(), logits.data_ptr(), _ld(logits),
+                                     _ptr(target), lse.data_ptr(), argmax.data_ptr(), loss_rows.data_ptr(),
+                                     loss_out.data_ptr(), _stream()), "ce_finalize")
+
+
+def ce_bwd(N, logits, lse, target, cap, grad_scale, dlogits):
+    M = logits.shape[0]
+    L.check(L.lib().svla_ce_bwd(M, N, logits.data_ptr(), _ld(logits), lse.data_ptr(), target.data_ptr(), cap,
+                                grad_scale.data_ptr(), dlogits.data_ptr(), _ld(dlogits), _stream()), "ce_bwd")
+
+
+def sumsq(x_flat, out, n_partial=4096):
+    part = torch.empty(n_partial, dtype=torch.float32, device=x_flat.device)
+    L.check(L.lib().svla_sumsq_bf16(x_flat.numel(), x_flat.data_ptr(), part.data_ptr(), n_partial, out.data_ptr(),
+                                    _stream()), "sumsq")
+
+
+def clip_scale(sumsq_t, max_norm, clip, norm_out):
+    L.check(L.lib().svla_clip_scale(sumsq_t.data_ptr(), max_norm, clip.data_ptr(), _ptr(norm_out), _stream()),
+            "clip_scale")
+
+
+def adamw(master, param, grad, m, v, lr, b1, b2, eps, wd, step, clip=None):
+    bc1 = 1.0 - b1 ** step
+    bc2 = 1.0 - b2 ** step
+    L.check(L.lib().svla_adamw(master.numel(), master.data_ptr(), param.data_ptr(), grad.data_ptr(), m.data_ptr(),
+                               v.data_ptr(), lr, b1, b2, eps, wd, bc1, bc2, _ptr(clip), _stream()), "adamw")
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def ceil_div(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+__all__ = [n for n in dir() if not n.startswith("_")] + ["math"]

@@ -1,0 +1,259 @@
+"""Gemma2 decoder (text side of SpatialVLA) on the libsvla HIP kernels.
+
+Module tree, attribute names and therefore state-dict keys are those of the reference
+(model/modeling_gemma2.py: Gemma2RMSNorm :60, Gemma2MLP :80, Gemma2RotaryEmbedding :95,
+Gemma2Attention :325, Gemma2DecoderLayer :436, Gemma2Model :647, Gemma2ForCausalLM :887), so
+reference checkpoints load unchanged.  Compute goes through `spatialvla_amd.functional` only.
+
+The reference's attention plug-in point GEMMA2_ATTENTION_FUNCTION (:317-322) is kept: every key
+("eager", "sdpa", "flash_attention_2", "flex_attention") maps to the one HIP implementation with the
+reference *eager* semantics (prefix-LM mask).  Inside the model the fused
+path (QKV GEMM -> attention with RoPE on load -> O GEMM) is used; the plug-in is for callers that
+hand in already-rotated q/k/v as the reference does.
+"""
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import functional as Fn
+
+
+@dataclass
+class KVMask:
+    """The reference's additive [B,1,L,L] mask (modeling_spatialvla.py:258-306), as per-key classes:
+    0 = visible to every query, 1 = visible to queries at or after the key, 2 = never visible."""
+    kv_class: torch.Tensor  # uint8 [B, L]
+
+    @staticmethod
+    def build(attention_mask: Optional[torch.Tensor], token_type_ids: Optional[torch.Tensor], is_training: bool,
+              B: int, L: int, device) -> "KVMask":
+        if is_training:
+            if attention_mask is None:
+                cls = torch.ones(B, L, dtype=torch.uint8, device=device)  # plain causal
+            else:
+                valid = attention_mask != 0
+                cls = torch.where(valid, 1, 2).to(torch.uint8)
+                # :304-305 — columns with token_type 0 are unmasked for every row (incl. padded ones, Q2)
+                cls = torch.where(token_type_ids == 0, 0, cls).to(torch.uint8)
+        else:
+            # :294 — inference prefill: bidirectional inside the sequence, padded keys masked
+            if attention_mask is None:
+                cls = torch.zeros(B, L, dtype=torch.uint8, device=device)
+            else:
+                cls = torch.where(attention_mask != 0, 0, 2).to(torch.uint8)
+        return KVMask(cls.contiguous())
+
+
+class Gemma2RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-6):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.zeros(dim))
+
+    def forward(self, x):
+        shp = x.shape
+        return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps).view(shp)
+
+    def add_forward(self, residual, y):
+        """residual + self(y) (decoder-layer residual branches)."""
+        shp = y.shape
+        return Fn.AddRMSNormFn.apply(residual.reshape(-1, shp[-1]), y.reshape(-1, shp[-1]), self.weight,
+                                     self.eps).view(shp)
+
+    def extra_repr(self):
+        return f"{tuple(self.weight.shape)}, eps={self.eps}"
+
+
+class Gemma2MLP(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.hidden_size = config.hidden_size
+        self.intermediate_size = config.intermediate_size
+        self.gate_proj = nn.Linear(self.hidden_size, self.intermediate_size, bias=False)
+        self.up_proj = nn.Linear(self.hidden_size, self.intermediate_size, bias=False)
+        self.down_proj = nn.Linear(self.intermediate_size, self.hidden_size, bias=False)
+        act = getattr(config, "hidden_activation", None) or getattr(config, "hidden_act", "gelu_pytorch_tanh")
+        if act not in ("gelu_pytorch_tanh", "gelu_tanh"):
+            raise ValueError(f"Gemma2MLP: activation {act!r} not supported (kernel implements gelu_pytorch_tanh)")
+
+    def forward(self, x):
+        shp = x.shape
+        out = Fn.GemmaMLPFn.apply(x.reshape(-1, shp[-1]), self.gate_proj.weight, self.up_proj.weight,
+                                  self.down_proj.weight)
+        return out.view(*shp[:-1], self.hidden_size)
+
+
+class Gemma2RotaryEmbedding(nn.Module):
+    def __init__(self, dim, max_position_embeddings=2048, base=10000, device=None):
+        super().__init__()
+        self.dim = dim
+        self.max_position_embeddings = max_position_embeddings
+        self.base = base
+        inv_freq = 1.0 / (self.base ** (torch.arange(0, self.dim, 2, dtype=torch.int64).float() / self.dim))
+        self.register_buffer("inv_freq", tensor=inv_freq, persistent=False)
+
+    @torch.no_grad()
+    def tables(self, position_ids: torch.Tensor, dtype) -> tuple:
+        """cos/sin [L, dim/2] in the activation dtype (reference :106-120 rounds them).
+        Positions must be shared by the batch (the kernel reads one table row per token)."""
+        if position_ids.dim() == 2:
+            if position_ids.shape[0] > 1 and not bool((position_ids == position_ids[:1]).all()):
+                raise ValueError("per-row position_ids are not supported by the fused RoPE path")
+            position_ids = position_ids[0]
+        freqs = position_ids.float()[:, None] * self.inv_freq.float().to(position_ids.device)[None, :]
+        return freqs.cos().to(dtype).contiguous(), freqs.sin().to(dtype).contiguous()
+
+
+def _plugin(module, query, key, value, mask, **kw):
+    """GEMMA2_ATTENTION_FUNCTION entry: reference signature (modeling_gemma2.py:169-195, 403-405)."""
+    kv_class = mask.kv_class if isinstance(mask, KVMask) else None
+    if mask is not None and not isinstance(mask, KVMask):
+        raise ValueError("HIP attention takes a KVMask (per-key classes), not a dense additive mask")
+    out = Fn.hip_attention(query, key, value, module.scaling, module.attn_logit_softcapping or 0.0, kv_class,
+                           module.sliding_window or 0)
+    return out, None
+
+
+GEMMA2_ATTENTION_FUNCTION = {"flash_attention_2": _plugin, "flex_attention": _plugin, "eager": _plugin,
+                             "sdpa": _plugin}
+
+
+class Gemma2Attention(nn.Module):
+    def __init__(self, config, layer_idx: Optional[int] = None):
+        super().__init__()
+        self.config = config
+        self.layer_idx = layer_idx
+        self.attention_dropout = config.attention_dropout
+        self.hidden_size = config.hidden_size
+        self.num_heads = config.num_attention_heads
+        self.head_dim = config.head_dim
+        self.num_key_value_heads = config.num_key_value_heads
+        self.num_key_value_groups = self.num_heads // self.num_key_value_heads
+        self.max_position_embeddings = config.max_position_embeddings
+        self.rope_theta = _rope_theta(config)
+        self.is_causal = True
+        self.scaling = config.query_pre_attn_scalar ** -0.5
+        self.sliding_window = config.sliding_window if not bool(layer_idx % 2) else None
+        self.attn_logit_softcapping = config.attn_logit_softcapping
+        bias = getattr(config, "attention_bias", False)
+        if bias:
+            raise ValueError("attention_bias=True is not part of the Gemma2 hot path")
+        self.q_proj = nn.Linear(self.hidden_size, self.num_heads * self.head_dim, bias=False)
+        self.k_proj = nn.Linear(self.hidden_size, self.num_key_value_heads * self.head_dim, bias=False)
+        self.v_proj = nn.Linear(self.hidden_size, self.num_key_value_heads * self.head_dim, bias=False)
+        self.o_proj = nn.Linear(self.num_heads * self.head_dim, self.hidden_size, bias=False)
+        self.rotary_emb = Gemma2RotaryEmbedding(self.head_dim, self.max_position_embeddings, self.rope_theta)
+
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple):
+        B, Lq, H = hidden_states.shape
+        cfg = Fn.GemmaAttnCfg(B, Lq, self.num_heads, self.num_key_value_heads, self.head_dim, self.scaling,
+                              float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
+        cos, sin = rope
+        out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
+                                        self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
+                                        cfg)
+        return out.view(B, Lq, H)
+
+
+def _rope_theta(config):
+    th = getattr(config, "rope_theta", None)
+    if th is None:
+        rp = getattr(config, "rope_parameters", None) or {}
+        th = rp.get("rope_theta", 10000.0)
+    return float(th)
+
+
+class Gemma2DecoderLayer(nn.Module):
+    def __init__(self, config, layer_idx: int):
+        super().__init__()
+        self.hidden_size = config.hidden_size
+        self.config = config
+        self.is_sliding = not bool(layer_idx % 2)
+        self.self_attn = Gemma2Attention(config=config, layer_idx=layer_idx)
+        self.mlp = Gemma2MLP(config)
+        self.input_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.post_attention_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.pre_feedforward_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.post_feedforward_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        self.sliding_window = config.sliding_window
+
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple):
+        # reference :475-496 (sandwich norms + residuals)
+        x = self.input_layernorm(hidden_states)
+        a = self.self_attn(x, attention_mask, rope)
+        h = self.post_attention_layernorm.add_forward(hidden_states, a)
+        x = self.pre_feedforward_layernorm(h)
+        m = self.mlp(x)
+        return self.post_feedforward_layernorm.add_forward(h, m)
+
+
+class Gemma2Model(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.padding_idx = config.pad_token_id
+        self.vocab_size = config.vocab_size
+        self.embed_tokens = nn.Embedding(config.vocab_size, config.hidden_size, self.padding_idx)
+        self.layers = nn.ModuleList([Gemma2DecoderLayer(config, i) for i in range(config.num_hidden_layers)])
+        self.norm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+
+    def get_input_embeddings(self):
+        return self.embed_tokens
+
+    def set_input_embeddings(self, value):
+        self.embed_tokens = value
+
+    def forward(self, hidden_states, attention_mask: KVMask, position_ids, output_hidden_states=False):
+        """hidden_states: inputs_embeds already multiplied by the bf16 normalizer (fused in the merge
+        kernel, reference :741-742)."""
+        rope = self.layers[0].self_attn.rotary_emb.tables(position_ids, hidden_states.dtype)
+        all_h = () if output_hidden_states else None
+        for layer in self.layers[: self.config.num_hidden_layers]:
+            if output_hidden_states:
+                all_h += (hidden_states,)
+            hidden_states = layer(hidden_states, attention_mask, rope)
+        hidden_states = self.norm(hidden_states)
+        if output_hidden_states:
+            all_h += (hidden_states,)
+        return hidden_states, all_h
+
+
+class Gemma2ForCausalLM(nn.Module):
+    _tied_weights_keys = None
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.model = Gemma2Model(config)
+        self.vocab_size = config.vocab_size
+        self.lm_head = nn.Linear(config.hidden_size, config.vocab_size, bias=False)
+
+    def get_input_embeddings(self):
+        return self.model.embed_tokens
+
+    def set_input_embeddings(self, value):
+        self.model.embed_tokens = value
+
+    def get_output_embeddings(self):
+        return self.lm_head
+
+    def set_output_embeddings(self, new_embeddings):
+        self.lm_head = new_embeddings
+
+    def get_decoder(self):
+        return self.model
+
+    def set_decoder(self, decoder):
+        self.model = decoder
+
+    def head(self, hidden_states, target, stash):
+        """lm_head + softcap (reference :993-997) fused with the shifted CE; returns (logits2d, loss)."""
+        cap = float(self.config.final_logit_softcapping or 0.0)
+        if cap <= 0:
+            raise ValueError("final_logit_softcapping must be set for the fused softcap/CE head")
+        return Fn.LMHeadCEFn.apply(hidden_states.reshape(-1, hidden_states.shape[-1]), self.lm_head.weight, target,
+                                   cap, stash)

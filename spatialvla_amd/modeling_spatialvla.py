@@ -1,0 +1,378 @@
+"""SpatialVLAForConditionalGeneration on MI355X: the drop-in model class.
+
+Mirrors the reference's public surface (model/modeling_spatialvla.py:162-526): constructor
+signature, sub-module attribute names (= state-dict keys), `forward(...)`
+arguments and the `SpatialVLACausalLMOutputWithPast` return, `get_image_features`,
+`backproject_patch`, `predict_action`, `from_pretrained` (spatial-embedding tail copy :524-525).
+
+Hot-path compute runs on libsvla (HIP, gfx950) through `spatialvla_amd.functional`:
+SigLIP, Ego3D, projector, embedding merge, 26 Gemma2 layers, softcapped lm_head + CE.
+The frozen ZoeDepth estimator (and its bicubic resampling) stays on stock PyTorch-ROCm ops under
+no_grad — it is not a north-star kernel target.
+"""
+from dataclasses import dataclass
+from typing import List, Optional, Tuple, Union
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from transformers import PreTrainedModel
+from transformers.utils import ModelOutput
+
+from . import functional as Fn
+from . import kernels as K
+from .configuration_spatialvla import SpatialVLAConfig
+from .modeling_gemma2 import Gemma2ForCausalLM, KVMask
+from .modeling_siglip import SiglipVisionModel
+
+SIGLIP_MEAN, SIGLIP_STD = (0.5, 0.5, 0.5), (0.5, 0.5, 0.5)
+ZOE_MEAN, ZOE_STD = (0.5, 0.5, 0.5), (0.5, 0.5, 0.5)
+
+
+class Ego3DPositionEmbeddingMLP(nn.Module):
+    """Reference :41-97.  Frequency encoding is done by the svla_ego3d_encode kernel (fused with the
+    depth back-projection); the MLP head runs on HIP GEMM/LayerNorm/ReLU kernels and its last Linear
+    adds the SigLIP features in its epilogue (:327-328)."""
+
+    def __init__(self, in_channels=3, num_pos_feats=768, n_freqs=8, logscale=True):
+        super().__init__()
+        self.n_freqs = n_freqs
+        self.freq_out_channels = in_channels * (2 * n_freqs + 1)
+        if not logscale:
+            raise ValueError("only logscale frequency bands are used by SpatialVLA")
+        freq_bands = 2 ** torch.linspace(0, n_freqs - 1, n_freqs)
+        center = torch.tensor([0.0, 0.0, 2.0]).repeat(in_channels // 3)
+        self.register_buffer("freq_bands", freq_bands, persistent=False)
+        self.register_buffer("center", center, persistent=False)
+        self.position_embedding_head = nn.Sequential(
+            nn.Linear(self.freq_out_channels, num_pos_feats),
+            nn.LayerNorm(num_pos_feats),
+            nn.ReLU(),
+            nn.Linear(num_pos_feats, num_pos_feats),
+        )
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p, gain=0.01)
+
+    def forward_residual(self, feat_padded, residual2d):
+        """feat_padded [N, round8(F)] (zero tail) -> residual + head(feat)."""
+        h0, ln, _, h3 = self.position_embedding_head
+        x = Fn.LinearFn.apply(feat_padded, h0.weight, h0.bias, None, 1.0)
+        x = Fn.LayerNormFn.apply(x, ln.weight, ln.bias, ln.eps)
+        x = Fn.ReLUFn.apply(x)
+        return Fn.LinearFn.apply(x, h3.weight, h3.bias, residual2d, 1.0)
+
+
+def process_zoe(pixel_values, pad_mode="reflect", output_size=(384, 512)):
+    """Reference :99-110 (ZoeDepth preprocessing), stock torch ops."""
+    ph, pw = 31, 31
+    images = F.pad(pixel_values, (pw, pw, ph, ph), mode=pad_mode)
+    images = F.interpolate(images, size=(384, 384), mode="bicubic", align_corners=True)
+    mean = torch.tensor(ZOE_MEAN, dtype=images.dtype, device=images.device).view(1, -1, 1, 1)
+    std = torch.tensor(ZOE_STD, dtype=images.dtype, device=images.device).view(1, -1, 1, 1)
+    images = (images - mean) / std
+    return images, ph, pw
+
+
+@dataclass
+class SpatialVLACausalLMOutputWithPast(ModelOutput):
+    loss: Optional[torch.FloatTensor] = None
+    logits: torch.FloatTensor = None
+    past_key_values: Optional[Union[List[torch.FloatTensor], object]] = None
+    hidden_states: Optional[Tuple[torch.FloatTensor]] = None
+    attentions: Optional[Tuple[torch.FloatTensor]] = None
+    image_hidden_states: Optional[torch.FloatTensor] = None
+
+
+class SpatialVLAMultiModalProjector(nn.Module):
+    def __init__(self, config: SpatialVLAConfig):
+        super().__init__()
+        self.linear = nn.Linear(config.vision_config.hidden_size, config.vision_config.projection_dim, bias=True)
+
+
+class SpatialVLAPreTrainedModel(PreTrainedModel):
+    config_class = SpatialVLAConfig
+    base_model_prefix = "model"
+    supports_gradient_checkpointing = False
+    _no_split_modules = ["SpatialVLAMultiModalProjector", "ZoeDepthForDepthEstimation", "Ego3DPositionEmbeddingMLP"]
+
+    def _init_weights(self, module):
+        std = getattr(self.config, "initializer_range", None) or self.config.text_config.initializer_range
+        if isinstance(module, (nn.Linear, nn.Conv2d)):
+            module.weight.data.normal_(mean=0.0, std=std)
+            if module.bias is not None:
+                module.bias.data.zero_()
+        elif isinstance(module, nn.Embedding):
+            module.weight.data.normal_(mean=0.0, std=std)
+            if module.padding_idx is not None:
+                module.weight.data[module.padding_idx].zero_()
+
+
+class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
+    def __init__(self, config: SpatialVLAConfig, vision_model=None, vision_zoe_model=None, projector_model=None,
+                 language_model=None):
+        super().__init__(config)
+        self.vision_tower = vision_model or SiglipVisionModel(config.vision_config)
+        self.multi_modal_projector = projector_model or SpatialVLAMultiModalProjector(config)
+        self.vocab_size = config.text_config.vocab_size
+        self.language_model = language_model or Gemma2ForCausalLM(config.text_config)
+        if config.use_vision_zoe:
+            from transformers import ZoeDepthForDepthEstimation  # frozen 3p depth estimator (stock torch ops)
+            self.vision_zoe_model = vision_zoe_model or ZoeDepthForDepthEstimation(config.vision_zoe_config)
+            self.position_embedding_3d = Ego3DPositionEmbeddingMLP(
+                config.ego3d_patch_reso ** 2 * 3, num_pos_feats=config.vision_config.hidden_size,
+                n_freqs=config.n_freqs)
+            patch_size, reso, image_size = (config.vision_config.patch_size, config.ego3d_patch_reso,
+                                            config.vision_config.image_size)
+            y, x = torch.meshgrid(torch.arange(0, image_size, patch_size // reso),
+                                  torch.arange(0, image_size, patch_size // reso), indexing="ij")
+            y, x = y + patch_size / reso / 2, x + patch_size / reso / 2
+            uv_h = torch.stack([x, y, torch.ones_like(x)], dim=0).reshape(3, -1)
+            self.register_buffer("uv_h", uv_h, persistent=False)
+        if config.use_spatial_token:
+            self.spatial_embed_tokens = nn.Embedding(config.spatial_token_num, config.text_config.hidden_size)
+        else:
+            self.spatial_embed_tokens = None
+        self.pad_token_id = config.pad_token_id if config.pad_token_id is not None else -1
+        self.strict_checks = True   # reference raises on an image-token count mismatch (needs a host sync)
+        self.last_stash = {}
+        self.post_init()
+
+    # ------------------------------------------------------------------ reference accessors
+    def get_input_embeddings(self):
+        return self.language_model.get_input_embeddings()
+
+    def set_input_embeddings(self, value):
+        self.language_model.set_input_embeddings(value)
+
+    def get_output_embeddings(self):
+        return self.language_model.get_output_embeddings()
+
+    def set_output_embeddings(self, new_embeddings):
+        self.language_model.set_output_embeddings(new_embeddings)
+
+    def get_decoder(self):
+        return self.language_model.get_decoder()
+
+    def set_decoder(self, decoder):
+        self.language_model.set_decoder(decoder)
+
+    def tie_weights(self, *args, **kwargs):
+        return None  # SpatialVLA unties lm_head (spatialvla_pretrain.py:321-325)
+
+    # ------------------------------------------------------------------ image path
+    @torch.no_grad()
+    def predict_depth(self, pixel_values):
+        """Zoe depth at image resolution (reference :314-323), frozen, stock torch ops."""
+        zoe_pv, ph, pw = process_zoe(pixel_values, pad_mode="reflect")
+        pvh, pvw = pixel_values.shape[-2:]
+        depth = self.vision_zoe_model(pixel_values=zoe_pv).predicted_depth
+        depth = F.interpolate(depth.unsqueeze(1), size=(pvh + 2 * ph, pvw + 2 * pw), mode="bicubic",
+                              align_corners=True)[..., ph:-ph, pw:-pw]
+        return depth.contiguous()
+
+    @torch.no_grad()
+    def ego3d_features(self, intrinsic, depth):
+        """backproject_patch (:195-223) + frequency_encoding (:74-91) in one kernel -> [B*np, round8(F)]."""
+        cfg = self.config
+        B = depth.shape[0]
+        np_ = (cfg.vision_config.image_size // cfg.vision_config.patch_size) ** 2
+        nfeat = self.position_embedding_3d.freq_out_channels
+        feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=depth.dtype, device=depth.device)
+        kinv = torch.linalg.inv(intrinsic.float()).contiguous()
+        K.ego3d_encode(depth.to(feat.dtype).contiguous(), kinv, self.uv_h.float().contiguous(),
+                       cfg.vision_config.patch_size, cfg.ego3d_patch_reso, cfg.n_freqs, feat)
+        return feat
+
+    def backproject_patch(self, K_: torch.Tensor, depth: torch.Tensor, patch_size=14, reso=2) -> torch.Tensor:
+        """Reference :195-223 — returns xyz [B, np, 3*reso^2] (fp32), computed by the HIP kernel."""
+        B = depth.shape[0]
+        np_ = (depth.shape[-2] // patch_size) * (depth.shape[-1] // patch_size)
+        nfeat = 3 * reso * reso * (2 * self.config.n_freqs + 1)
+        feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=torch.bfloat16, device=depth.device)
+        xyz = torch.empty(B, np_, 3 * reso * reso, dtype=torch.float32, device=depth.device)
+        K.ego3d_encode(depth.to(torch.bfloat16).contiguous(), torch.linalg.inv(K_.float()).contiguous(),
+                       self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
+        return xyz
+
+    def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor):
+        """Reference :308-333 -> [B, np, H_text]."""
+        dt = self.multi_modal_projector.linear.weight.dtype
+        pv = pixel_values.to(dt).contiguous()
+        sig_in = torch.empty_like(pv)
+        K.affine(pv, 1.0 / SIGLIP_STD[0], -SIGLIP_MEAN[0], sig_in)  # TF.normalize (:309)
+        B = pv.shape[0]
+        feats = self.vision_tower(sig_in)                           # [B, np, Hv]
+        Hv = feats.shape[-1]
+        sel = feats.reshape(-1, Hv)
+        if self.config.use_vision_zoe:
+            depth = self.predict_depth(pixel_values.to(dt))
+            enc = self.ego3d_features(intrinsic, depth)
+            sel = self.position_embedding_3d.forward_residual(enc, sel)
+        lin = self.multi_modal_projector.linear
+        img = Fn.LinearFn.apply(sel, lin.weight, lin.bias, None, 1.0 / (self.config.text_config.hidden_size ** 0.5))
+        return img.view(B, -1, img.shape[-1])
+
+    # ------------------------------------------------------------------ forward
+    def _merge_inputs(self, input_ids, image_features):
+        cfg = self.config
+        B, Lq = input_ids.shape
+        dev = input_ids.device
+        embed_w = self.get_input_embeddings().weight
+        if embed_w.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("training embed_tokens is not supported: freeze it as the reference does "
+                                      "(freeze_llm_embed, spatialvla_pretrain.py:341-342)")
+        ids = input_ids.reshape(-1).contiguous()
+        img_index = None
+        if image_features is not None:
+            img_mask = ids == cfg.image_token_index
+            if self.strict_checks:
+                n_tok = int(img_mask.sum().item())
+                if n_tok * image_features.shape[-1] != image_features.numel():
+                    raise ValueError(
+                        "Number of images does not match number of special image tokens in the input text. "
+                        f"Got {n_tok} image tokens in the text but {image_features.shape[0] * image_features.shape[1]} "
+                        "tokens from image embeddings.")
+            img_index = torch.where(img_mask, torch.cumsum(img_mask.to(torch.int32), 0) - 1, -1).to(torch.int32)
+        spatial_w, sort_rows, offsets, a0 = None, None, None, 0
+        if cfg.use_spatial_token:
+            spatial_w = self.spatial_embed_tokens.weight
+            a0, na = int(cfg.action_token_begin_idx), spatial_w.shape[0]
+            sel = (ids >= a0) & (ids < a0 + na)
+            key = torch.where(sel, ids - a0, na)
+            sort_rows = torch.argsort(key, stable=True).to(torch.int32)
+            counts = torch.zeros(na + 1, dtype=torch.int32, device=dev).scatter_add_(
+                0, key, torch.ones_like(key, dtype=torch.int32))
+            offsets = torch.zeros(na + 2, dtype=torch.int32, device=dev)
+            offsets[1:] = torch.cumsum(counts, 0)
+            offsets = offsets[: na + 1].contiguous()
+        hidden = cfg.text_config.hidden_size
+        normalizer = float(torch.tensor(hidden ** 0.5, dtype=embed_w.dtype))
+        img2d = image_features.reshape(-1, image_features.shape[-1]) if image_features is not None else None
+        out = Fn.EmbedMergeFn.apply(ids, img_index, img2d, spatial_w, embed_w, a0, normalizer, sort_rows, offsets)
+        return out.view(B, Lq, hidden)
+
+    @staticmethod
+    def _targets(labels, attention_mask, B, Lq, dev, pad_mask=None):
+        """Shifted CE targets per row (reference :415-430): target[b,t] = labels[b,t+1] where
+        attention_mask[b,t+1] != 0 and label != -100, else -1 (ignored); last position ignored."""
+        t = torch.full((B, Lq), -1, dtype=torch.int64, device=dev)
+        if labels is None:
+            return t.reshape(-1)
+        sl = labels[:, 1:].clone()
+        if attention_mask is not None:
+            sl = torch.where(attention_mask[:, 1:] != 0, sl, -100)
+        sl = torch.where(sl == -100, -1, sl)
+        t[:, :-1] = sl
+        return t.reshape(-1).contiguous()
+
+    def forward(
+        self,
+        input_ids: torch.LongTensor = None,
+        pixel_values: torch.FloatTensor = None,
+        actions: Optional[torch.FloatTensor] = None,
+        intrinsic: Optional[torch.Tensor] = None,
+        attention_mask: Optional[torch.Tensor] = None,
+        position_ids: Optional[torch.LongTensor] = None,
+        past_key_values=None,
+        token_type_ids: Optional[torch.LongTensor] = None,
+        cache_position: Optional[torch.LongTensor] = None,
+        inputs_embeds: Optional[torch.FloatTensor] = None,
+        labels: Optional[torch.LongTensor] = None,
+        use_cache: Optional[bool] = None,
+        output_attentions: Optional[bool] = None,
+        output_hidden_states: Optional[bool] = None,
+        return_dict: Optional[bool] = None,
+        num_logits_to_keep: int = 0,
+        kv_mask: Optional[KVMask] = None,
+    ) -> Union[Tuple, SpatialVLACausalLMOutputWithPast]:
+        if past_key_values is not None or use_cache:
+            if past_key_values is not None:
+                raise NotImplementedError("KV-cached decoding is SURVEY §8(f)#2 (next); use predict_action()")
+        if inputs_embeds is not None:
+            raise NotImplementedError("inputs_embeds input is not supported on the HIP path; pass input_ids")
+        if output_attentions:
+            raise NotImplementedError("output_attentions is not available from the fused attention kernel")
+        return_dict = True if return_dict is None else return_dict
+        is_training = token_type_ids is not None and labels is not None  # reference :359
+        B, Lq = input_ids.shape
+        dev = input_ids.device
+
+        image_features = None
+        if pixel_values is not None:
+            image_features = self.get_image_features(pixel_values, intrinsic)
+
+        if labels is not None and (labels == self.pad_token_id).any():  # reference :390-395 (BC path)
+            labels = torch.where(input_ids == self.pad_token_id, -100, labels)
+
+        hidden = self._merge_inputs(input_ids, image_features)
+        if position_ids is None:
+            start = 0 if cache_position is None else int(cache_position[0])
+            position_ids = (torch.arange(start, start + Lq, device=dev) + 1)[None]  # 1-indexed (:372)
+        mask = kv_mask or KVMask.build(attention_mask, token_type_ids, is_training, B, Lq, dev)
+        h, all_h = self.language_model.model(hidden, mask, position_ids, output_hidden_states=bool(output_hidden_states))
+
+        target = self._targets(labels, attention_mask, B, Lq, dev)
+        stash = {}
+        logits2d, loss = self.language_model.head(h, target, stash)
+        self.last_stash = stash
+        logits = logits2d.view(B, Lq, -1)
+        if num_logits_to_keep:
+            logits = logits[:, -num_logits_to_keep:]
+        if labels is None:
+            loss = None
+        if not return_dict:
+            out = (logits,)
+            return (loss,) + out if loss is not None else out
+        return SpatialVLACausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=None, hidden_states=all_h,
+                                                attentions=None, image_hidden_states=image_features)
+
+    def action_argmax(self):
+        """argmax over V of the last forward's logits [B*L] (int64), computed in the lm_head epilogue
+        (train/monkey_patch.py:267 uses logits[..., :-1, :].argmax(-1))."""
+        return self.last_stash.get("argmax")
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def predict_action(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
+        """Greedy decode (reference :484-492).  Mathematically identical to the reference's
+        HybridCache decode: the prompt attends bidirectionally (:294) and every generated token attends to
+        the prompt and to earlier generated tokens only — realised as full re-forwards with per-key
+        classes (prompt keys class 0, generated keys class 1).  KV caching is §8(f)#2 (next)."""
+        ids = model_inputs["input_ids"]
+        dev = self.language_model.lm_head.weight.device
+        ids = ids.to(dev)
+        pv = model_inputs.get("pixel_values")
+        pv = pv.to(dev, torch.bfloat16) if pv is not None else None
+        intr = model_inputs.get("intrinsic")
+        intr = intr.to(dev, torch.bfloat16) if intr is not None else None
+        am = model_inputs.get("attention_mask")
+        eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
+        B, P = ids.shape
+        feats = self.get_image_features(pv, intr) if pv is not None else None
+        out = []
+        cur = ids
+        for _ in range(max_new_tokens):
+            Lc = cur.shape[1]
+            cls = torch.ones(B, Lc, dtype=torch.uint8, device=dev)
+            cls[:, :P] = 0 if am is None else torch.where(am.to(dev) != 0, 0, 2).to(torch.uint8)
+            hidden = self._merge_inputs(cur, feats)
+            pos = (torch.arange(Lc, device=dev) + 1)[None]
+            h, _ = self.language_model.model(hidden, KVMask(cls.contiguous()), pos)
+            stash = {}
+            tgt = torch.full((B * Lc,), -1, dtype=torch.int64, device=dev)
+            self.language_model.head(h, tgt, stash)
+            nxt = stash["argmax"].view(B, Lc)[:, -1:]
+            out.append(nxt)
+            cur = torch.cat([cur, nxt], 1)
+            if eos is not None and bool((nxt == eos).all()):
+                break
+        return torch.cat(out, 1)
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path, *model_args, **kwargs):
+        model = super().from_pretrained(pretrained_model_name_or_path, *model_args, **kwargs)
+        if model.config.use_spatial_token:  # reference :524-525
+            model.language_model.model.embed_tokens.weight.data[-model.config.spatial_token_num:] = \
+                model.spatial_embed_tokens.weight.data
+        return model

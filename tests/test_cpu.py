@@ -1,0 +1,187 @@
+"""CPU suite: the oracle pinned against the reference's golden vectors, the C-ABI surface, host logic."""
+import ctypes
+import json
+import os
+import re
+
+import pytest
+import torch
+
+import harness as H
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _load(name):
+    from safetensors.torch import load_file
+    return load_file(os.path.join(GOLD, name))
+
+
+# ------------------------------------------------------------------------------ oracle vs reference goldens
+@pytest.fixture(scope="module")
+def tiny_oracle():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    cfgd = H.cfg_dict("tiny")
+    P, zoe = H.build_oracle(cfgd)
+    return cfgd, P, zoe
+
+
+def test_oracle_matches_reference_tiny_train_bitexact(tiny_oracle):
+    cfgd, P, zoe = tiny_oracle
+    g = _load("tiny_train.safetensors")
+    batch = {k[3:]: v for k, v in g.items() if k.startswith("in.")}
+    loss, logits, grads, cap = H.run_oracle(P, zoe, cfgd, batch)
+    assert torch.equal(cap["depth"], g["out.depth"])
+    assert torch.equal(cap["image_features"], g["out.image_features"])
+    assert torch.equal(logits.to(torch.bfloat16), g["out.logits"])
+    assert float(loss) == float(g["out.loss"][0])
+    for k, v in g.items():
+        if k.startswith("grad."):
+            assert torch.equal(grads[k[5:]].to(torch.bfloat16), v), k
+
+
+def test_oracle_matches_reference_prefill(tiny_oracle):
+    import spatialvla_oracle as O
+    cfgd, P, zoe = tiny_oracle
+    g, gp = _load("tiny_train.safetensors"), _load("tiny_prefill.safetensors")
+    b = {k[3:]: v for k, v in g.items() if k.startswith("in.")}
+    b.pop("labels")
+    b.pop("token_type_ids")
+    with torch.no_grad():
+        _, logits = O.forward(P, cfgd, b, zoe, depth=g["out.depth"])
+    assert torch.equal(logits, gp["out.logits"])
+
+
+def test_oracle_matches_reference_ragged(tiny_oracle):
+    cfgd, P, zoe = tiny_oracle
+    g = _load("tiny_ragged.safetensors")
+    b = {k[3:]: v for k, v in g.items() if k.startswith("in.")}
+    assert (b["attention_mask"] == 0).any(), "fixture must contain padding"
+    loss, logits, grads, _ = H.run_oracle(P, zoe, cfgd, b)
+    assert float(loss) == float(g["out.loss"][0])
+    assert torch.equal(logits.to(torch.bfloat16), g["out.logits"])
+    for k, v in g.items():
+        if k.startswith("gradnorm."):
+            assert abs(grads[k[9:]].norm().item() - v.item()) <= 1e-6 * max(1.0, v.item()), k
+
+
+def test_oracle_gemma_layer_4b_matches_reference():
+    import spatialvla_oracle as O
+    from spatialvla_amd import presets
+    from spatialvla_amd.detinit import det_tensor
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = _load("layer4b.safetensors")
+    cfgd = json.loads(json.dumps(presets.spatialvla_4b(use_vision_zoe=False)))
+    tc = cfgd["text_config"]
+    shapes = O.param_shapes(cfgd)
+    P = {}
+    for n, s in shapes.items():
+        if n.startswith("language_model.model.layers.1."):
+            P[n] = det_tensor(n, s, H.SEED).to(torch.bfloat16).requires_grad_(True)
+    L, Pf = 312, 299
+    h = g["gemma.in"].clone().requires_grad_(True)
+    am = torch.ones(1, L, dtype=torch.long)
+    tt = torch.zeros(1, L, dtype=torch.long)
+    tt[:, Pf:] = 1
+    mask = O.prefix_mask(am, tt, True, L, torch.bfloat16)
+    cos, sin = O.rope_tables((torch.arange(L) + 1)[None], 256, torch.bfloat16)
+    y = O.gemma_layer(P, tc, 1, h, mask, cos, sin)
+    gout = det_tensor("gemma.gout", (1, L, 2304), H.SEED, scale=1.0).to(torch.bfloat16)
+    (y.float() * gout.float()).sum().backward()
+    assert torch.equal(y.detach(), g["gemma1.out"])
+    assert torch.equal(h.grad, g["gemma1.dx"])
+
+
+# ------------------------------------------------------------------------------ C-ABI surface
+def test_header_symbols_exported_by_library():
+    """libsvla.so loads (no GPU needed) and exports every entry point declared in include/svla.h."""
+    from spatialvla_amd import _lib
+    hdr = open(os.path.join(REPO, "include", "svla.h")).read()
+    names = set(re.findall(r"^\s*(?:const char\*|int)\s+(svla_\w+)\s*\(", hdr, re.M))
+    assert len(names) >= 20
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert names == set(_lib.SIGNATURES), "python binding must cover exactly the header"
+    _lib.load()
+    assert b"gfx950" in _lib.lib().svla_version()
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(REPO, "spatialvla_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(root, f)).read()
+                assert "spatialvla_oracle" not in src and "ref_shim" not in src and "/root/reference" not in src, f
+
+
+# ------------------------------------------------------------------------------ host logic
+@pytest.mark.parametrize("training", [True, False])
+@pytest.mark.parametrize("ragged", [False, True])
+def test_kvmask_matches_reference_additive_mask(training, ragged):
+    import spatialvla_oracle as O
+    from spatialvla_amd import presets
+    from spatialvla_amd.modeling_gemma2 import KVMask
+    cfgd = H.cfg_dict("tiny")
+    b = presets.synthetic_batch(cfgd, batch=3, seed=5, ragged=ragged)
+    am, tt = torch.from_numpy(b["attention_mask"]), torch.from_numpy(b["token_type_ids"])
+    B, L = am.shape
+    dense = O.prefix_mask(am, tt, training, L, torch.bfloat16)[:, 0]
+    visible_ref = dense == 0
+    cls = KVMask.build(am, tt, training, B, L, "cpu").kv_class.long()
+    i = torch.arange(L)[:, None]
+    j = torch.arange(L)[None, :]
+    visible = (cls[:, None, :] == 0) | ((cls[:, None, :] == 1) & (j <= i))
+    assert torch.equal(visible, visible_ref)
+
+
+def test_ce_targets_match_reference_shift():
+    from spatialvla_amd import presets
+    from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration as M
+    cfgd = H.cfg_dict("tiny")
+    b = presets.synthetic_batch(cfgd, batch=3, seed=9, ragged=True)
+    labels, am = torch.from_numpy(b["labels"]), torch.from_numpy(b["attention_mask"])
+    B, L = labels.shape
+    t = M._targets(labels, am, B, L, "cpu").view(B, L)
+    sl, keep = labels[:, 1:], am[:, 1:] != 0
+    ref = torch.where(keep & (sl != -100), sl, -1)
+    assert torch.equal(t[:, :-1], ref) and (t[:, -1] == -1).all()
+
+
+def test_synthetic_batch_layout_4b():
+    from spatialvla_amd import presets
+    cfgd = presets.spatialvla_4b()
+    b = presets.synthetic_batch(cfgd, batch=2, seed=0)
+    assert b["input_ids"].shape == (2, 312)
+    assert (b["input_ids"][:, :256] == cfgd["image_token_index"]).all()
+    assert (b["token_type_ids"].sum(1) == 13).all()
+    assert cfgd["vocab_size"] == 265347 and cfgd["action_token_begin_idx"] == 257153
+    a0 = cfgd["action_token_begin_idx"]
+    acts = b["input_ids"][:, 299:311]
+    assert ((acts >= a0) & (acts < a0 + 8194)).all()
+
+
+def test_model_state_dict_keys_match_reference_weight_abi():
+    """State-dict keys are the weight ABI; compare with the reference's trainable set."""
+    from spatialvla_amd import SpatialVLAConfig
+    from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration
+    g = _load("tiny_train.safetensors")
+    m = SpatialVLAForConditionalGeneration(SpatialVLAConfig(**H.cfg_dict("tiny")))
+    mine = {k.replace("vision_tower.vision_model.", "vision_tower.") for k, _ in m.named_parameters()}
+    ref = {k[5:] for k in g if k.startswith("grad.")}
+    assert ref <= mine
+    extra = {k for k in mine - ref if not k.startswith("vision_zoe_model.")}
+    assert extra == {"language_model.model.embed_tokens.weight"}  # frozen in the reference
+
+
+def test_product_fails_loudly_without_gpu():
+    from spatialvla_amd import SpatialVLAConfig
+    from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration
+    from spatialvla_amd import presets
+    cfgd = H.cfg_dict("tiny")
+    m = SpatialVLAForConditionalGeneration(SpatialVLAConfig(**cfgd)).to(torch.bfloat16)
+    b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=1, seed=0), "cpu")
+    with pytest.raises(Exception):
+        m(**b)

@@ -1,0 +1,309 @@
+"""Per-kernel parity of libsvla against plain PyTorch fp32 references of the same op (GPU)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from harness import rel_l2
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _r(*shape, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * scale).to(BF)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 300, 136), (624, 577, 256), (9, 130, 72)])
+@pytest.mark.parametrize("layouts", ["nt", "nn", "tn"])
+def test_gemm_layouts(cuda, M, N, K, layouts):
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(0)
+    if layouts == "nt":      # x[M,K] @ W[N,K]^T
+        a, b = _r(M, K), _r(N, K)
+        ref = a.float() @ b.float().T
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_KC)
+    elif layouts == "nn":    # dy[M,K'] @ W[K',N]
+        a, b = _r(M, K), _r(K, N + (-N) % 8)[:, :N]
+        ref = a.float() @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_RC)
+    else:                    # dy^T @ x : A stored [K, M], B stored [K, N]
+        a, b = _r(K, M + (-M) % 8)[:, :M], _r(K, N + (-N) % 8)[:, :N]
+        ref = a.float().T @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_RC), Kn._operand([b], L.LAYOUT_RC)
+    c = torch.empty(M, N + (-N) % 8, dtype=BF, device=cuda)[:, :N]
+    Kn.gemm(M, N, K, A, B, [c], [0], c.stride(0), Kn._epi())
+    torch.cuda.synchronize()
+    assert rel_l2(c, ref) < 5e-3
+
+
+def test_gemm_epilogues(cuda):
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(1)
+    M, K, N = 300, 192, 264
+    x, w, bias, res = _r(M, K), _r(N, K, scale=0.1), _r(N, scale=0.5), _r(M, N)
+    acc = x.float() @ w.float().T
+    y = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], y, kind=L.EPI_BIAS, bias=bias, alpha=0.5)
+    assert rel_l2(y, (acc + bias.float()) * 0.5) < 5e-3
+    pre = torch.empty_like(y)
+    Kn.linear_fwd(x, [w], y, kind=L.EPI_BIAS_GELU, bias=bias, out1=pre)
+    assert rel_l2(pre, acc + bias.float()) < 5e-3
+    assert rel_l2(y, F.gelu(acc + bias.float(), approximate="tanh")) < 1e-2
+    Kn.linear_fwd(x, [w], y, kind=L.EPI_BIAS_RESID, bias=bias, in0=res)
+    assert rel_l2(y, acc + bias.float() + res.float()) < 5e-3
+    # accumulate
+    y0 = y.clone()
+    Kn.gemm(M, N, K, Kn._operand([x], L.LAYOUT_KC), Kn._operand([w], L.LAYOUT_KC), [y], [0], y.stride(0),
+            Kn._epi(L.EPI_STORE, accumulate=True))
+    assert rel_l2(y, y0.float() + acc) < 5e-3
+    # GELU_BWD: C = acc * gelu'(pre)
+    g = torch.empty_like(y)
+    Kn.gemm(M, N, K, Kn._operand([x], L.LAYOUT_KC), Kn._operand([w], L.LAYOUT_KC), [g], [0], g.stride(0),
+            Kn._epi(L.EPI_GELU_BWD, in0=pre))
+    p = pre.float().requires_grad_(True)
+    F.gelu(p, approximate="tanh").backward(acc)
+    assert rel_l2(g, p.grad) < 1e-2
+
+
+def test_gemm_segments_and_geglu(cuda):
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(2)
+    M, K = 333, 256
+    wq, wk, wv = _r(256, K, scale=0.1), _r(128, K, scale=0.1), _r(128, K, scale=0.1)
+    x = _r(M, K)
+    out = torch.empty(M, 512, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [wq, wk, wv], out)
+    ref = x.float() @ torch.cat([wq, wk, wv]).float().T
+    assert rel_l2(out, ref) < 5e-3
+    # dgrad over K segments and wgrad into C segments
+    dy = _r(M, 512)
+    dx = torch.empty(M, K, dtype=BF, device=cuda)
+    Kn.linear_dgrad(dy, [wq, wk, wv], dx)
+    assert rel_l2(dx, dy.float() @ torch.cat([wq, wk, wv]).float()) < 5e-3
+    gs = [torch.empty_like(w) for w in (wq, wk, wv)]
+    Kn.linear_wgrad(dy, x, gs)
+    assert rel_l2(torch.cat(gs), dy.float().T @ x.float()) < 5e-3
+    # GeGLU forward + backward epilogues
+    I = 192
+    wg, wu, wd = _r(I, K, scale=0.1), _r(I, K, scale=0.1), _r(K, I, scale=0.1)
+    h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    Kn.linear_geglu_fwd(x, wg, wu, h, g, u)
+    gr, ur = x.float() @ wg.float().T, x.float() @ wu.float().T
+    assert rel_l2(g, gr) < 5e-3 and rel_l2(u, ur) < 5e-3
+    assert rel_l2(h, F.gelu(gr, approximate="tanh") * ur) < 1e-2
+    dout = _r(M, K)
+    dgu = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+    Kn.linear_dgrad(dout, [wd], dgu[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=dgu[:, :I], out2=dgu[:, I:])
+    gg = g.float().requires_grad_(True)
+    uu = u.float().requires_grad_(True)
+    (F.gelu(gg, approximate="tanh") * uu).backward(dout.float() @ wd.float())
+    assert rel_l2(dgu[:, :I], gg.grad) < 2e-2 and rel_l2(dgu[:, I:], uu.grad) < 2e-2
+
+
+def test_gemm_softcap_ce(cuda):
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(3)
+    M, K, V = 100, 256, 1000
+    h, w = _r(M, K), _r(V, K, scale=0.2)
+    ldv = Kn.round_up(V, 64)
+    buf = torch.empty(M, ldv, dtype=BF, device=cuda)
+    ntn = Kn.ceil_div(V, 128)
+    stats = torch.empty(M, ntn, 3, dtype=torch.float32, device=cuda)
+    Kn.linear_fwd(h, [w], buf[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=stats, cap=30.0)
+    ref = 30.0 * torch.tanh((h.float() @ w.float().T) / 30.0)
+    assert rel_l2(buf[:, :V], ref) < 5e-3
+    tgt = torch.randint(0, V, (M,), device=cuda)
+    tgt[::3] = -1
+    lse, am = torch.empty(M, device=cuda), torch.empty(M, dtype=torch.int64, device=cuda)
+    lr, lo = torch.empty(M, device=cuda), torch.empty(2, device=cuda)
+    Kn.ce_finalize(V, ntn, stats, buf[:, :V], tgt, lse, am, lr, lo)
+    y = buf[:, :V].float()
+    assert torch.allclose(lse, torch.logsumexp(y, -1), atol=1e-3)
+    assert torch.equal(am, y.argmax(-1))
+    valid = tgt >= 0
+    ref_loss = F.cross_entropy(y[valid], tgt[valid])
+    assert abs(lo[0].item() - ref_loss.item()) < 1e-3 and lo[1].item() == valid.sum().item()
+    d = torch.empty(M, ldv, dtype=BF, device=cuda)
+    gscale = torch.tensor([1.0 / valid.sum().item()], device=cuda)
+    Kn.ce_bwd(V, buf[:, :V], lse, tgt, 30.0, gscale, d)
+    yy = y.clone().requires_grad_(True)
+    F.cross_entropy(yy[valid], tgt[valid]).backward()
+    ref_d = yy.grad * (1 - (y / 30.0) ** 2)
+    assert rel_l2(d[:, :V], ref_d) < 1e-2
+    assert d[:, V:].abs().sum().item() == 0
+
+
+# ------------------------------------------------------------------------------------------ norms
+def test_rmsnorm(cuda):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(4)
+    R, N = 77, 2304
+    x, w, res = _r(R, N), _r(N, scale=0.1), _r(R, N)
+    y = torch.empty_like(x)
+    rstd = torch.empty(R, device=cuda)
+    Kn.rmsnorm_fwd(x, w, 1e-6, y, rstd)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + wf)
+    assert rel_l2(y, ref) < 5e-3
+    dy = _r(R, N)
+    ref.backward(dy.float())
+    dx = torch.empty_like(x)
+    dw = torch.empty_like(w)
+    Kn.rmsnorm_bwd(x, w, rstd, dy, None, dx, dw)
+    assert rel_l2(dx, xf.grad) < 1e-2 and rel_l2(dw, wf.grad) < 1e-2
+    h = torch.empty_like(x)
+    Kn.add_rmsnorm_fwd(res, x, w, 1e-6, h, rstd)
+    assert rel_l2(h, res.float() + ref.detach()) < 5e-3
+    Kn.rmsnorm_bwd(x, w, rstd, dy, res, dx, None)
+    assert rel_l2(dx, xf.grad + res.float()) < 1e-2
+
+
+def test_layernorm_colsum(cuda):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(5)
+    R, N = 130, 1152
+    x, w, b = _r(R, N), _r(N, scale=0.1) + 1, _r(N, scale=0.1)
+    y = torch.empty_like(x)
+    mu, rs = torch.empty(R, device=cuda), torch.empty(R, device=cuda)
+    Kn.layernorm_fwd(x, w, b, 1e-6, y, mu, rs)
+    xf, wf, bf = (t.float().requires_grad_(True) for t in (x, w, b))
+    ref = F.layer_norm(xf, (N,), wf, bf, 1e-6)
+    assert rel_l2(y, ref) < 5e-3
+    dy = _r(R, N)
+    ref.backward(dy.float())
+    dx, dw, db = torch.empty_like(x), torch.empty_like(w), torch.empty_like(b)
+    Kn.layernorm_bwd(x, w, mu, rs, dy, None, dx, dw, db)
+    assert rel_l2(dx, xf.grad) < 1e-2 and rel_l2(dw, wf.grad) < 1e-2 and rel_l2(db, bf.grad) < 1e-2
+    cs = torch.empty(N, dtype=BF, device=cuda)
+    Kn.colsum_bf16(dy, cs)
+    assert rel_l2(cs, dy.float().sum(0)) < 5e-3
+
+
+# ------------------------------------------------------------------------------------------ attention
+def _ref_attn(q, k, v, scale, cap, kv_class, window, cos=None, sin=None):
+    """fp32 eager reference in [B, L, H, D] layout with per-key classes."""
+    B, L, Hq, D = q.shape
+    Hkv = k.shape[2]
+    q, k, v = (t.float().transpose(1, 2) for t in (q, k, v))
+    if cos is not None:
+        c, s = torch.cat([cos, cos], -1).float(), torch.cat([sin, sin], -1).float()
+        rh = lambda t: torch.cat((-t[..., D // 2:], t[..., :D // 2]), -1)  # noqa: E731
+        q = q * c + rh(q) * s
+        k = k * c + rh(k) * s
+    k = k.repeat_interleave(Hq // Hkv, 1)
+    v = v.repeat_interleave(Hq // Hkv, 1)
+    s_ = q @ k.transpose(-1, -2) * scale
+    if cap:
+        s_ = cap * torch.tanh(s_ / cap)
+    i = torch.arange(L, device=q.device)[:, None]
+    j = torch.arange(L, device=q.device)[None, :]
+    if kv_class is not None:
+        c = kv_class[:, None, None, :].long()
+        vis = (c == 0) | ((c == 1) & (j <= i))
+    else:
+        vis = torch.ones(1, 1, L, L, dtype=torch.bool, device=q.device)
+    if window:
+        vis = vis & ((i - j) < window)
+    s_ = torch.where(vis, s_, torch.tensor(-3.3895313892515355e38, device=q.device))
+    p = torch.softmax(s_, -1)
+    return (p @ v).transpose(1, 2)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,L,rope,cap", [(256, 2, 1, 140, True, 50.0), (256, 8, 4, 312, True, 50.0),
+                                                 (72, 2, 2, 256, False, 0.0), (72, 3, 3, 70, False, 0.0)])
+def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(6)
+    B = 2
+    qkv = _r(B * L, (Hq + 2 * Hkv) * D)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    scale = 1 / 16 if D == 256 else D ** -0.5
+    kv_class = None
+    cos = sin = None
+    if D == 256:
+        P = L - 13
+        kv_class = torch.zeros(B, L, dtype=torch.uint8, device=cuda)
+        kv_class[:, P:] = 1
+        kv_class[1, L - 3:] = 2
+        if rope:
+            inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+            f = (torch.arange(L, device=cuda).float() + 1)[:, None] * inv[None]
+            cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
+    a = Kn.attn_args(B, L, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap, kv_class, 0,
+                     cos, sin)
+    out = torch.empty(B * L, Hq * D, dtype=BF, device=cuda)
+    lse = torch.empty(B, Hq, L, device=cuda)
+    Kn.attn_fwd(a, out, lse)
+    qr = q.view(B, L, Hq, D).float().requires_grad_(True)
+    kr = k.view(B, L, Hkv, D).float().requires_grad_(True)
+    vr = v.view(B, L, Hkv, D).float().requires_grad_(True)
+    ref = _ref_attn(qr, kr, vr, scale, cap, kv_class, 0, cos, sin)
+    assert rel_l2(out.view(B, L, Hq, D), ref) < 1e-2
+    do = _r(B * L, Hq * D)
+    ref.backward(do.view(B, L, Hq, D).float())
+    dqkv = torch.empty_like(qkv)
+    ld = dqkv.stride(0)
+    Kn.attn_bwd(a, out, do, lse, dqkv[:, :Hq * D], ld, dqkv[:, Hq * D:(Hq + Hkv) * D], ld, dqkv[:, (Hq + Hkv) * D:], ld)
+    assert rel_l2(dqkv[:, :Hq * D].view(B, L, Hq, D), qr.grad) < 2e-2
+    assert rel_l2(dqkv[:, Hq * D:(Hq + Hkv) * D].view(B, L, Hkv, D), kr.grad) < 2e-2
+    assert rel_l2(dqkv[:, (Hq + Hkv) * D:].view(B, L, Hkv, D), vr.grad) < 2e-2
+
+
+# ------------------------------------------------------------------------------------------ glue
+def test_embed_merge(cuda):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(7)
+    V, H, na, a0 = 600, 256, 64, 513
+    emb, sp = _r(V, H), _r(na, H)
+    ids = torch.randint(0, 512, (2, 40), device=cuda)
+    ids[:, :10] = 512
+    ids[:, 30:36] = torch.randint(a0, a0 + na, (2, 6), device=cuda)
+    ids[1, 31] = ids[0, 30]
+    img = _r(20, H)
+    flat = ids.reshape(-1)
+    m = flat == 512
+    idx = torch.where(m, torch.cumsum(m.int(), 0) - 1, -1).int()
+    out = torch.empty(flat.numel(), H, dtype=BF, device=cuda)
+    Kn.embed_merge(flat, idx, emb, sp, a0, na, img, 16.0, out)
+    ref = emb[flat].float()
+    sel = (flat >= a0) & (flat < a0 + na)
+    ref[sel] = sp[flat[sel] - a0].float()
+    ref[m] = img.float()
+    assert torch.equal(out, (ref.to(BF) * 16.0).to(BF))
+    key = torch.where(sel, flat - a0, na)
+    rows = torch.argsort(key, stable=True).int()
+    cnt = torch.zeros(na + 1, dtype=torch.int32, device=cuda).scatter_add_(0, key, torch.ones_like(key, dtype=torch.int32))
+    offs = torch.zeros(na + 2, dtype=torch.int32, device=cuda)
+    offs[1:] = torch.cumsum(cnt, 0)
+    dout = _r(flat.numel(), H)
+    dsp, dimg = torch.empty_like(sp), torch.empty_like(img)
+    Kn.embed_merge_bwd(flat, idx, rows, offs[:na + 1].contiguous(), na, dout, 16.0, dsp, dimg)
+    ref_dsp = torch.zeros(na, H, device=cuda).index_add_(0, flat[sel] - a0, (dout[sel].float() * 16).to(BF).float())
+    assert rel_l2(dsp, ref_dsp) < 5e-3
+    assert rel_l2(dimg, dout[m].float() * 16) < 5e-3
+
+
+def test_adamw_and_norm(cuda):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(8)
+    n = 10007
+    p = torch.randn(n, device=cuda)
+    g = _r(n, scale=0.1)
+    master, m, v = p.clone(), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    pb = p.to(BF)
+    ss = torch.empty(1, device=cuda)
+    Kn.sumsq(g, ss, n_partial=64)
+    assert abs(ss.item() - g.float().pow(2).sum().item()) / g.float().pow(2).sum().item() < 1e-4
+    clip, nrm = torch.empty(1, device=cuda), torch.empty(1, device=cuda)
+    Kn.clip_scale(ss, 0.5, clip, nrm)
+    ref_p = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref_p], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    ref_p.grad = g.float() * clip
+    opt.step()
+    Kn.adamw(master, pb, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, 1, clip)
+    assert torch.allclose(master, ref_p.detach(), atol=1e-6, rtol=1e-5)
+    assert torch.equal(pb, master.to(BF))

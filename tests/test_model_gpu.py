@@ -1,0 +1,158 @@
+"""End-to-end parity of the HIP model against the reference (golden vectors) and the CPU oracle."""
+import json
+import os
+
+import pytest
+import torch
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    from safetensors.torch import load_file
+    return load_file(os.path.join(GOLD, name))
+
+
+def test_tiny_train_vs_reference_golden(cuda):
+    """Reference eager training step (oracle/gen_golden.py) vs the HIP model, same weights/inputs."""
+    g = _load("tiny_train.safetensors")
+    cfgd = H.cfg_dict("tiny")
+    model = H.build_hip_model(cfgd, "cuda:0")
+    batch = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
+    loss, logits, grads, am = H.run_hip(model, batch, depth=g["out.depth"])
+    gr = {k[5:]: v.float() for k, v in g.items() if k.startswith("grad.")}
+    res = H.compare(loss, logits, grads, am, g["out.loss"][0], g["out.logits"].float(), gr)
+    worst = sorted(res["grad_rel"].items(), key=lambda kv: -kv[1])[:5]
+    print(json.dumps({k: v for k, v in res.items() if k != "grad_rel"}, indent=1), worst)
+    assert not res["grads_missing"], res["grads_missing"]
+    assert abs(res["loss_hip"] - res["loss_ref"]) < 1e-2
+    assert res["logits_rel"] < H.LOGITS_TOL
+    assert res["grad_rel_max"] < H.GRAD_TOL, worst
+    assert res["argmax_agree_confident"] == 1.0
+
+
+def test_tiny_image_features_and_ego3d(cuda):
+    g = _load("tiny_train.safetensors")
+    cfgd = H.cfg_dict("tiny")
+    model = H.build_hip_model(cfgd, "cuda:0")
+    pv, k = g["in.pixel_values"].to(cuda), g["in.intrinsic"].to(cuda)
+    xyz = model.backproject_patch(k, g["out.depth"].to(cuda), 14, 2)
+    assert H.rel_l2(xyz, g["out.xyz"].float()) < 1e-5
+    model.predict_depth = lambda p: g["out.depth"].to(cuda)
+    with torch.no_grad():
+        f = model.get_image_features(pv, k)
+    assert H.rel_l2(f, g["out.image_features"].float()) < 1e-2
+
+
+def test_tiny_depth_estimator(cuda):
+    """The frozen 3p depth estimator on the GPU vs the reference's CPU output (stock torch ops)."""
+    g = _load("tiny_train.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    d = model.predict_depth(g["in.pixel_values"].to(cuda))
+    assert H.rel_l2(d, g["out.depth"].float()) < 2e-2
+
+
+def test_tiny_prefill_vs_reference_golden(cuda):
+    g = _load("tiny_train.safetensors")
+    gp = _load("tiny_prefill.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    model.predict_depth = lambda p: g["out.depth"].to(cuda)
+    b = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
+    with torch.no_grad():
+        out = model(input_ids=b["input_ids"], pixel_values=b["pixel_values"], intrinsic=b["intrinsic"],
+                    attention_mask=b["attention_mask"])
+    assert out.loss is None
+    assert H.rel_l2(out.logits, gp["out.logits"].float()) < H.LOGITS_TOL
+
+
+def test_tiny_ragged_vs_reference_golden(cuda):
+    """Right-padded ragged batch: padded keys visible in training, CE over valid rows."""
+    g = _load("tiny_ragged.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    b = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
+    loss, logits, grads, am = H.run_hip(model, b, depth=g["out.depth"])
+    assert abs(float(loss) - float(g["out.loss"][0])) < 1e-2
+    assert H.rel_l2(logits, g["out.logits"].float()) < H.LOGITS_TOL
+    for k, v in g.items():
+        if k.startswith("gradnorm."):
+            n = k[len("gradnorm."):]
+            assert abs(grads[n].norm().item() - v.item()) / max(v.item(), 1e-6) < 3e-2, n
+
+
+def test_tiny_vs_oracle_random_batch(cuda):
+    res = H.tiny_parity_run("cuda:0", batch=3, seed=21)
+    assert res["logits_rel"] < H.LOGITS_TOL
+    assert res["grad_rel_max"] < H.GRAD_TOL
+    assert res["argmax_agree_confident"] == 1.0
+
+
+def _layer4b_model(li, cuda):
+    from spatialvla_amd import SpatialVLAConfig
+    from spatialvla_amd import presets
+    from spatialvla_amd.detinit import deterministic_init_
+    from spatialvla_amd.modeling_gemma2 import Gemma2DecoderLayer
+    cfg = SpatialVLAConfig(**json.loads(json.dumps(presets.spatialvla_4b(use_vision_zoe=False))))
+    layer = Gemma2DecoderLayer(cfg.text_config, li).to(torch.bfloat16)
+    deterministic_init_(layer, seed=H.SEED, prefix=f"language_model.model.layers.{li}.")
+    return layer.to(cuda), cfg
+
+
+@pytest.mark.parametrize("li", [0, 1])
+def test_gemma2_layer_4b_vs_reference_golden(cuda, li):
+    """One Gemma2 decoder layer at SpatialVLA-4B widths (B=1, L=312, prefix 299) vs the reference."""
+    from spatialvla_amd.detinit import det_tensor
+    from spatialvla_amd.modeling_gemma2 import KVMask
+    g = _load("layer4b.safetensors")
+    layer, cfg = _layer4b_model(li, cuda)
+    L, P = 312, 299
+    h = g["gemma.in"].to(cuda).requires_grad_(True)
+    gout = det_tensor("gemma.gout", (1, L, 2304), H.SEED, scale=1.0).to(torch.bfloat16).to(cuda)
+    cls = torch.ones(1, L, dtype=torch.uint8, device=cuda)
+    cls[:, :P] = 0
+    rope = layer.self_attn.rotary_emb.tables((torch.arange(L, device=cuda) + 1)[None], torch.bfloat16)
+    y = layer(h, KVMask(cls), rope)
+    (y.float() * gout.float()).sum().backward()
+    if li == 1:
+        assert H.rel_l2(y, g["gemma1.out"].float()) < 1e-2
+        assert H.rel_l2(h.grad, g["gemma1.dx"].float()) < 3e-2
+    else:
+        assert H.rel_l2(y[0, ::13], g["gemma0.out_rows"].float()) < 1e-2
+        assert H.rel_l2(h.grad[0, ::13], g["gemma0.dx_rows"].float()) < 3e-2
+    for n, p in layer.named_parameters():
+        ref = g[f"gemma{li}.gradnorm.{n}"].item()
+        assert abs(p.grad.float().norm().item() - ref) / ref < 3e-2, n
+
+
+def test_siglip_layer_4b_vs_reference_golden(cuda):
+    from spatialvla_amd import SpatialVLAConfig, presets
+    from spatialvla_amd.detinit import det_tensor, deterministic_init_
+    from spatialvla_amd.modeling_siglip import SiglipEncoderLayer
+    g = _load("layer4b.safetensors")
+    cfg = SpatialVLAConfig(**json.loads(json.dumps(presets.spatialvla_4b(use_vision_zoe=False))))
+    layer = SiglipEncoderLayer(cfg.vision_config).to(torch.bfloat16)
+    deterministic_init_(layer, seed=H.SEED, prefix="vision_tower.vision_model.encoder.layers.0.")
+    layer = layer.to(cuda)
+    x = g["siglip.in"].to(cuda).reshape(256, 1152).requires_grad_(True)
+    go = det_tensor("siglip.gout", (1, 256, 1152), H.SEED, scale=1.0).to(torch.bfloat16).to(cuda)
+    y = layer(x, 1, 256)
+    (y.float() * go.reshape(256, 1152).float()).sum().backward()
+    assert H.rel_l2(y, g["siglip.out"].float().reshape(256, 1152)) < 1e-2
+    assert H.rel_l2(x.grad, g["siglip.dx"].float().reshape(256, 1152)) < 3e-2
+    for n, p in layer.named_parameters():
+        ref = g[f"siglip.gradnorm.{n}"].item()
+        assert abs(p.grad.float().norm().item() - ref) / ref < 3e-2, n
+
+
+def test_predict_action_decodes(cuda):
+    """Greedy decode runs through the HIP path and first token equals the prefill argmax."""
+    g = _load("tiny_train.safetensors")
+    gp = _load("tiny_prefill.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    model.predict_depth = lambda p: g["out.depth"].to(cuda)
+    ids = g["in.input_ids"][:, :-13]  # prompt only (prefix)
+    inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    out = model.predict_action(inputs, max_new_tokens=3, eos_token_id=-1)
+    assert out.shape == (2, 3)
