@@ -160,7 +160,7 @@ int svla_embed_merge(int64_t rows, int64_t H, const int64_t* ids, const int32_t*
 int svla_embed_merge_bwd(int64_t rows, int64_t H, const int64_t* ids, const int32_t* img_index,
                          const int32_t* spatial_sorted_rows, const int32_t* spatial_offsets, int64_t na,
                          const void* dout, float normalizer, void* dspatial, void* dimg, void* stream);
-/* Ego3D (modeling_spatialvla.py:195-223, :74-91): area-pool depth [B,1,Hd,Wd] to (hp*reso)^2, back-project
+/* Ego3D (modeling_spatialvla.py:195-223, :74-91): area-pool fp32 depth [B,1,Hd,Wd] to (hp*reso)^2, back-project
  * with inv(K) @ uv_h (uv_h passed in, bf16-quantised as the model buffer), permute per patch,
  * normalise ((xyz-center)/2 -> bf16), frequency-encode -> feat [B, hp*wp, ldf] bf16 (cols >= 12*(2F+1) zeroed). */
 int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* depth, const float* kinv, const float* uv_h,

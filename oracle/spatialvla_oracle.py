@@ -313,3 +313,26 @@ def param_shapes(cfg: dict) -> Dict[str, tuple]:
     s["language_model.model.norm.weight"] = (Ht,)
     s["language_model.lm_head.weight"] = (V, Ht)
     return s
+
+
+def build_params_random(cfg: dict, seed: int, dtype=BF16):
+    """Fast random parameters (torch CPU generator) for timing the oracle as the CPU baseline —
+    same shapes and scale rules as build_params, not bit-identical to it."""
+    g = torch.Generator().manual_seed(seed)
+    P = {}
+    for n, shp in param_shapes(cfg).items():
+        if len(shp) >= 2:
+            fan = 1
+            for d in shp[1:]:
+                fan *= d
+            t = (torch.randn(shp, generator=g, dtype=torch.float32) / math.sqrt(fan)).to(dtype)
+        elif n.endswith("weight") and ("layernorm" in n and n.startswith("language_model") or n.endswith("model.norm.weight")):
+            t = torch.zeros(shp, dtype=dtype)
+        elif n.endswith("weight"):
+            t = torch.ones(shp, dtype=dtype)
+        else:
+            t = torch.zeros(shp, dtype=dtype)
+        if n != "language_model.model.embed_tokens.weight":
+            t.requires_grad_(True)
+        P[n] = t
+    return P

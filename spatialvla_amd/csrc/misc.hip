@@ -72,7 +72,7 @@ __global__ void embed_spatial_bwd_kernel(int64_t H, const int32_t* __restrict__ 
 
 // ------------------------------------------------------------------ Ego3D
 // one block per (b, patch); thread layout: 12 coords x 17 features
-__global__ void ego3d_kernel(int B, int Hd, int Wd, const bf16_t* __restrict__ depth, const float* __restrict__ kinv,
+__global__ void ego3d_kernel(int B, int Hd, int Wd, const float* __restrict__ depth, const float* __restrict__ kinv,
                              const float* __restrict__ uvh, int patch, int reso, int n_freqs,
                              bf16_t* __restrict__ feat, int64_t ldf, float* __restrict__ xyz_out) {
   const int b = blockIdx.y, p = blockIdx.x;
@@ -85,11 +85,12 @@ __global__ void ego3d_kernel(int B, int Hd, int Wd, const bf16_t* __restrict__ d
   if ((int)threadIdx.x < npts) {
     const int sy = threadIdx.x / reso, sx = threadIdx.x % reso;
     const int gy = py * reso + sy, gx = px * reso + sx;
-    // F.interpolate(mode="area") == mean over the ry x rx window, result rounded to bf16
+    // F.interpolate(mode="area") == mean over the ry x rx window; ZoeDepth's metric head returns fp32
+    // depth, so the reference pools and back-projects in fp32 (no rounding here)
     float s = 0.f;
     for (int yy = 0; yy < ry; ++yy)
-      for (int xx = 0; xx < rx; ++xx) s += bf2f(depth[((int64_t)b * Hd + gy * ry + yy) * Wd + gx * rx + xx]);
-    const float d = round_bf(s / (float)(ry * rx));
+      for (int xx = 0; xx < rx; ++xx) s += depth[((int64_t)b * Hd + gy * ry + yy) * Wd + gx * rx + xx];
+    const float d = s / (float)(ry * rx);
     const int idx = gy * gw + gx;
     const float u = uvh[idx], v = uvh[gh * gw + idx], w1 = uvh[2 * gh * gw + idx];
     const float* K = kinv + b * 9;
@@ -386,7 +387,7 @@ extern "C" int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* 
   SVLA_CHECK_ARG(reso * reso * 3 <= 64 && n_freqs <= 16 && ldf >= reso * reso * 3 * (2 * n_freqs + 1),
                  "ego3d: reso/n_freqs/ldf");
   dim3 grid((Hd / patch) * (Wd / patch), B);
-  hipLaunchKernelGGL(ego3d_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, Hd, Wd, (const bf16_t*)depth, kinv,
+  hipLaunchKernelGGL(ego3d_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, Hd, Wd, (const float*)depth, kinv,
                      uv_h, patch, reso, n_freqs, (bf16_t*)feat, ldf, xyz_out);
   return svla::check_launch("ego3d");
 }

@@ -212,9 +212,13 @@ class Gemma2Model(nn.Module):
         kernel, reference :741-742)."""
         rope = self.layers[0].self_attn.rotary_emb.tables(position_ids, hidden_states.dtype)
         all_h = () if output_hidden_states else None
-        for layer in self.layers[: self.config.num_hidden_layers]:
+        hook = getattr(self, "_svla_layer_grad_hook", None)
+        for i, layer in enumerate(self.layers[: self.config.num_hidden_layers]):
             if output_hidden_states:
                 all_h += (hidden_states,)
+            if hook is not None and hidden_states.requires_grad:
+                # fires once d(layer input) is complete, i.e. after every weight grad of layers >= i
+                hidden_states.register_hook(lambda g, i=i: hook(i))
             hidden_states = layer(hidden_states, attention_mask, rope)
         hidden_states = self.norm(hidden_states)
         if output_hidden_states:

@@ -178,9 +178,10 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         B = depth.shape[0]
         np_ = (cfg.vision_config.image_size // cfg.vision_config.patch_size) ** 2
         nfeat = self.position_embedding_3d.freq_out_channels
-        feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=depth.dtype, device=depth.device)
+        dt = self.multi_modal_projector.linear.weight.dtype
+        feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=dt, device=depth.device)
         kinv = torch.linalg.inv(intrinsic.float()).contiguous()
-        K.ego3d_encode(depth.to(feat.dtype).contiguous(), kinv, self.uv_h.float().contiguous(),
+        K.ego3d_encode(depth.float().contiguous(), kinv, self.uv_h.float().contiguous(),
                        cfg.vision_config.patch_size, cfg.ego3d_patch_reso, cfg.n_freqs, feat)
         return feat
 
@@ -191,7 +192,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         nfeat = 3 * reso * reso * (2 * self.config.n_freqs + 1)
         feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=torch.bfloat16, device=depth.device)
         xyz = torch.empty(B, np_, 3 * reso * reso, dtype=torch.float32, device=depth.device)
-        K.ego3d_encode(depth.to(torch.bfloat16).contiguous(), torch.linalg.inv(K_.float()).contiguous(),
+        K.ego3d_encode(depth.float().contiguous(), torch.linalg.inv(K_.float()).contiguous(),
                        self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
         return xyz
 

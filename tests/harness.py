@@ -101,7 +101,16 @@ def run_oracle(P, zoe, cfgd, batch_cpu, depth=None):
 def compare(loss_h, logits_h, grads_h, argmax_h, loss_r, logits_r, grads_r):
     B, L, V = logits_r.shape
     res = {"loss_hip": float(loss_h), "loss_ref": float(loss_r), "logits_rel": rel_l2(logits_h, logits_r)}
-    rels = {n: rel_l2(grads_h[n], g) for n, g in grads_r.items() if n in grads_h}
+    rels = {}
+    for n, g in grads_r.items():
+        if n not in grads_h:
+            continue
+        if n.endswith("self_attn.k_proj.bias"):
+            # d loss / d k_bias is analytically 0 (softmax is invariant to a per-row shift q.b); both sides
+            # hold rounding noise only: require the same noise scale instead of a relative error
+            rels[n] = 0.0 if grads_h[n].norm() <= 3 * g.float().norm() + 1e-3 else float("inf")
+        else:
+            rels[n] = rel_l2(grads_h[n], g)
     missing = sorted(set(grads_r) - set(grads_h))
     res["grad_rel"] = rels
     res["grad_rel_max"] = max(rels.values()) if rels else 0.0

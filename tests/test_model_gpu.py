@@ -79,6 +79,9 @@ def test_tiny_ragged_vs_reference_golden(cuda):
     for k, v in g.items():
         if k.startswith("gradnorm."):
             n = k[len("gradnorm."):]
+            if n.endswith("self_attn.k_proj.bias"):  # analytically zero: compare noise scale only
+                assert grads[n].norm().item() <= 3 * v.item() + 1e-3, n
+                continue
             assert abs(grads[n].norm().item() - v.item()) / max(v.item(), 1e-6) < 3e-2, n
 
 
@@ -143,6 +146,9 @@ def test_siglip_layer_4b_vs_reference_golden(cuda):
     assert H.rel_l2(x.grad, g["siglip.dx"].float().reshape(256, 1152)) < 3e-2
     for n, p in layer.named_parameters():
         ref = g[f"siglip.gradnorm.{n}"].item()
+        if n.endswith("self_attn.k_proj.bias"):  # analytically zero (shift-invariant softmax): noise scale only
+            assert p.grad.float().norm().item() <= 3 * ref + 1e-3, n
+            continue
         assert abs(p.grad.float().norm().item() - ref) / ref < 3e-2, n
 
 
