@@ -53,6 +53,8 @@ typedef struct {
   int32_t layout;
   int32_t _pad;
   int64_t ld;
+  int64_t r_valid;   /* readable extent of the outer index (0 = M or N); beyond it the operand reads as 0 */
+  int64_t k_valid;   /* readable extent of the reduction index (0 = K); beyond it the operand reads as 0 */
 } svla_operand;
 
 enum {
@@ -81,7 +83,9 @@ typedef struct {
 
 /* C: up to 4 row segments (c_seg_start tile-aligned to 128) — lets dW of q/k/v (or gate/up)
  * land directly in separate gradient tensors.  c_nseg = 1 for a plain matrix.
- * Requirements: ld of every operand and of C a multiple of 8 elements; pointers 16-B aligned. */
+ * Requirements: ld of every operand and of C a multiple of 8 elements; pointers 16-B aligned; the
+ * reduction extent of a KC operand (k_valid, default K) a multiple of 8 (zero-pad: e.g. the lm_head
+ * dlogits rows are zero beyond V up to their padded ld). */
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                    const svla_epilogue* epi, void* stream);

@@ -27,7 +27,7 @@ EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EP
 
 class Operand(ctypes.Structure):
     _fields_ = [("ptr", c_vp * 4), ("seg_start", c_i64 * 5), ("nseg", c_i32), ("seg_dim", c_i32),
-                ("layout", c_i32), ("_pad", c_i32), ("ld", c_i64)]
+                ("layout", c_i32), ("_pad", c_i32), ("ld", c_i64), ("r_valid", c_i64), ("k_valid", c_i64)]
 
 
 class Epilogue(ctypes.Structure):

@@ -4,142 +4,144 @@
 // SpatialVLA hot path, forward and backward (see include/svla.h for the reference call sites).
 //
 // Design (CDNA4-first):
-//  * 128x128x64 block tile, 256 threads = 4 waves in a 2x2 grid, each wave a 64x64 sub-tile of
-//    4x4 v_mfma_f32_16x16x32_bf16 accumulators (64-lane operand maps, not 32-lane warp tiles).
-//  * Each operand may be KC (reduction dim contiguous: nn.Linear weights, activations) or RC
-//    (outer dim contiguous: activations read transposed for dW, weights read for dX). KC tiles
-//    are read with ds_read_b128 from an XOR-swizzled [128][64] LDS image; RC tiles are stored
-//    [64][128] (swizzled) and read with the gfx950 transpose read ds_read_b64_tr_b16, so no
-//    operand is ever transposed in HBM.
-//  * Register-staged double buffer: tile k+1 is loaded global->VGPR while tile k feeds the MFMAs,
-//    then written to the other LDS buffer; one barrier per K-tile.
-//  * Epilogue goes through LDS (fp32, padded rows) so every global store is a 16-B vector along N
-//    and every epilogue input (bias, residual, saved activations) is a 16-B vector load.
+//  * Block tiles BM x BN x 64 with 4 or 8 waves; each wave owns a WTM x WTN sub-tile of
+//    v_mfma_f32_16x16x32_bf16 accumulators (64-lane operand maps).  Three instantiations:
+//    256x256 (8 waves, 128x64 per wave), 256x128 (8 waves, 64x64), 128x128 (4 waves, 64x64); the
+//    host picks the largest that still gives >= 2 waves of blocks on the 256 CUs.  Large tiles halve
+//    the L2->LDS operand traffic per FLOP (a 128^2 tile needs ~39 TB/s of operand bandwidth at the
+//    MFMA peak, more than the L2 delivers).
+//  * Operands go global->LDS directly (buffer_load_dwordx4 ... lds, wave-uniform descriptors), out-of-
+//    range chunks are zero-filled by the descriptor range check.  Each operand is KC (reduction dim
+//    contiguous: Linear weights, activations) or RC (outer dim contiguous: activations read transposed
+//    for dW, weights read for dX); RC tiles are read with the gfx950 transpose read ds_read_b64_tr_b16,
+//    so no operand is ever transposed in HBM.  XOR swizzles live in the per-lane source address.
+//  * Two LDS stages, k-tiles k+1 and k+2 in flight behind a counted s_waitcnt vmcnt(N) and raw
+//    s_barrier (no vmcnt(0) inside the k-loop).
+//  * Epilogue through LDS in 64-row passes (fp32, padded rows): every global store is a 16-B vector
+//    along N, every epilogue input (bias, residual, saved activations) a 16-B vector load.
 //  * Block ids are remapped XCD-aware (consecutive tiles share an XCD L2) and grouped along M.
 #include "svla_common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64, NTH = 256;
-constexpr int TILE_BYTES = BM * BK * 2;                 // 16 KiB per operand per buffer
-constexpr int EPI_LD = 132;                             // fp32 row stride of the epilogue image
-constexpr int STAGE_BYTES = 4 * TILE_BYTES;             // A,B x 2 buffers
-constexpr int EPI_BYTES = BM * EPI_LD * 4;
-constexpr int LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+constexpr int BK = 64;
 constexpr int GROUP_M = 8;
+constexpr uint32_t OOB = 0x80000000u;  // voffset beyond num_records -> returns zeros
 
-struct SegSel {
-  const bf16_t* base;
-  int64_t rbase, kbase;  // indices to subtract
+template <int BM_, int BN_, int WGM_, int WGN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_;
+  static constexpr int NW = WGM * WGN, NTH = 64 * NW;
+  static constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  static constexpr int TM = WTM / 16, TN = WTN / 16;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int IA = BM / (8 * NW), IB = BN / (8 * NW);  // LDS-DMA instructions per wave per k-tile
+  static constexpr int EPI_ROWS = 64, EPI_LD = BN + 4;
+  static constexpr int EPI_BYTES = EPI_ROWS * EPI_LD * 4;
+  static constexpr int LDS = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  static_assert(IA >= 1 && IB >= 1, "tile too small for the wave count");
 };
+using CfgBig = Cfg<256, 256, 2, 4>;
+using CfgMid = Cfg<256, 128, 4, 2>;
+using CfgSmall = Cfg<128, 128, 2, 2>;
 
-__device__ __forceinline__ int find_seg(const svla_operand& op, int64_t idx) {
-  int s = 0;
-#pragma unroll
-  for (int i = 1; i < 4; ++i)
-    if (i < op.nseg && idx >= op.seg_start[i]) s = i;
-  return s;
-}
-
-__device__ __forceinline__ SegSel select(const svla_operand& op, int64_t r0, int64_t k0) {
-  SegSel s;
-  if (op.nseg <= 1 || op.seg_dim == SVLA_SEG_GEGLU) {
-    s.base = (const bf16_t*)op.ptr[0];
-    s.rbase = 0;
-    s.kbase = 0;
-  } else if (op.seg_dim == SVLA_SEG_OUTER) {
-    int i = find_seg(op, r0);
-    s.base = (const bf16_t*)op.ptr[i];
-    s.rbase = op.seg_start[i];
-    s.kbase = 0;
-  } else {
-    int i = find_seg(op, k0);
-    s.base = (const bf16_t*)op.ptr[i];
-    s.rbase = 0;
-    s.kbase = op.seg_start[i];
-  }
-  return s;
-}
-
-__device__ __forceinline__ u32x4 load8_guard(const bf16_t* p, int64_t n_valid) {
-  // n_valid = number of valid elements starting at p (<= 0: none)
-  if (n_valid >= 8) return *reinterpret_cast<const u32x4*>(p);
-  u32x4 v = {0u, 0u, 0u, 0u};
-  if (n_valid > 0) {
-    uint16_t tmp[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) tmp[j] = (j < n_valid) ? p[j] : (uint16_t)0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (uint32_t)tmp[2 * j] | ((uint32_t)tmp[2 * j + 1] << 16);
-  }
-  return v;
-}
-
-// swizzle of the RC image [64 k][16 chunks of 16 B]
+// RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
 
-// ---- global -> registers (4 x 16 B per thread per operand)
-template <int LAYOUT>
-__device__ __forceinline__ void load_tile(const svla_operand& op, int64_t R, int64_t K, int64_t r0, int64_t k0,
-                                          int t, u32x4 (&st)[4]) {
-  if (op.seg_dim == SVLA_SEG_GEGLU && op.nseg == 2) {
-    // B only, KC: rows 0..63 of the tile from ptr[0] (gate), 64..127 from ptr[1] (up)
-    const int64_t I = op.seg_start[1];
-    const int c = t & 7;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int lr = (t >> 3) + 32 * i;
-      int64_t n = (r0 >> 1) + (lr & 63);
-      const bf16_t* base = (const bf16_t*)op.ptr[lr >> 6];
-      int64_t kk = k0 + 8 * c;
-      st[i] = (n < I) ? load8_guard(base + n * op.ld + kk, K - kk) : u32x4{0u, 0u, 0u, 0u};
-    }
-    return;
-  }
-  SegSel s = select(op, r0, k0);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  // T20: make the descriptor provably wave-uniform (else hipcc wraps every load in a waterfall loop)
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pb = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)OOB, 0x00020000);
+}
+
+// segment pointer for outer tile start / k-tile start (scalar selects, no dynamic indexing)
+__device__ __forceinline__ const bf16_t* seg_ptr(const svla_operand& op, int64_t idx, int64_t& base_idx) {
+  const bf16_t* p = (const bf16_t*)op.ptr[0];
+  base_idx = 0;
+  if (op.nseg > 1 && idx >= op.seg_start[1]) { p = (const bf16_t*)op.ptr[1]; base_idx = op.seg_start[1]; }
+  if (op.nseg > 2 && idx >= op.seg_start[2]) { p = (const bf16_t*)op.ptr[2]; base_idx = op.seg_start[2]; }
+  if (op.nseg > 3 && idx >= op.seg_start[3]) { p = (const bf16_t*)op.ptr[3]; base_idx = op.seg_start[3]; }
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Operand staging.  A tile of TR outer rows x 64 k is TR*8 16-B chunks; wave-instruction j writes 1 KiB
+// lane-linearly:
+//   KC image [TR][64 k] (128-B rows): instruction j -> rows 8j..8j+7, lane l -> row 8j+(l>>3), LDS chunk
+//      p = l&7 holding global chunk p ^ (row&7)
+//   RC image [64 k][TR] (2*TR-B rows, CPR = TR/8 chunks): instruction j -> k-rows j*(64/CPR).., lane l ->
+//      k-row j*(64/CPR) + l/CPR, LDS chunk p = l%CPR holding global chunk p ^ rc_swz(k-row)
+// ---------------------------------------------------------------------------------------------
+template <int LAYOUT, int TR, int NI>
+struct OpState {
+  uint32_t voff[NI];  // per-lane byte offset of each DMA chunk; OOB for rows beyond the valid extent
+  int kq;             // KC: k offset (elements) of this lane's chunk; RC: k-row of instruction 0
+};
+
+template <int LAYOUT, int TR, int NI>
+__device__ __forceinline__ void op_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane,
+                                         OpState<LAYOUT, TR, NI>& st) {
+  const int64_t ldb = op.ld * 2;
   if (LAYOUT == SVLA_LAYOUT_KC) {
-    const int c = t & 7;
+    const int gc = (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3 for every instruction
+    st.kq = gc * 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + (t >> 3) + 32 * i;
-      int64_t kk = k0 + 8 * c;
-      st[i] = (r < R) ? load8_guard(s.base + (r - s.rbase) * op.ld + (kk - s.kbase), K - kk)
-                      : u32x4{0u, 0u, 0u, 0u};
+    for (int i = 0; i < NI; ++i) {
+      const int row = 8 * (w * NI + i) + (lane >> 3);
+      int64_t grow = r0 + row;
+      int rowoff = row;
+      if (op.seg_dim == SVLA_SEG_GEGLU) {  // gate rows 0..TR/2-1, up rows TR/2..TR-1 of the tile
+        grow = (r0 >> 1) + (row & (TR / 2 - 1));
+        rowoff = row & (TR / 2 - 1);
+      }
+      st.voff[i] = grow < rv ? (uint32_t)(rowoff * ldb + gc * 16) : OOB;
     }
   } else {
-    const int c = t & 15;
+    constexpr int CPR = TR / 8, RPI = 64 / CPR;
+    st.kq = RPI * w * NI + lane / CPR;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t k = k0 + (t >> 4) + 16 * i;
-      int64_t rr = r0 + 8 * c;
-      st[i] = (k < K) ? load8_guard(s.base + (k - s.kbase) * op.ld + (rr - s.rbase), R - rr)
-                      : u32x4{0u, 0u, 0u, 0u};
+    for (int i = 0; i < NI; ++i) {
+      const int kr = st.kq + RPI * i;
+      const int gc = (lane % CPR) ^ rc_swz(kr);
+      st.voff[i] = (r0 + gc * 8 < rv) ? (uint32_t)(kr * ldb + gc * 16) : OOB;
     }
   }
 }
 
-// ---- registers -> LDS image
-template <int LAYOUT>
-__device__ __forceinline__ void store_tile(char* lds, int t, const u32x4 (&st)[4]) {
-  if (LAYOUT == SVLA_LAYOUT_KC) {
-    const int c = t & 7;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int row = (t >> 3) + 32 * i;
-      *reinterpret_cast<u32x4*>(lds + row * 128 + ((c ^ (row & 7)) << 4)) = st[i];
-    }
+template <int LAYOUT, int TR, int NI>
+__device__ __forceinline__ void op_issue(const svla_operand& op, const OpState<LAYOUT, TR, NI>& st, int64_t r0,
+                                         int64_t k0, int64_t kv, char* lds, int w) {
+  const bf16_t* p;
+  const char* base;
+  if (LAYOUT == SVLA_LAYOUT_KC && op.seg_dim == SVLA_SEG_GEGLU) {
+    // the wave's rows [8*w*NI, 8*w*NI + 8*NI) lie in one half of the tile: gate or up
+    p = (const bf16_t*)(((8 * w * NI) >= TR / 2) ? op.ptr[1] : op.ptr[0]);
+    base = (const char*)(p + (r0 >> 1) * op.ld + k0);
   } else {
-    const int c = t & 15;
+    int64_t rb = 0, kb = 0;
+    if (op.seg_dim == SVLA_SEG_K) p = seg_ptr(op, k0, kb);
+    else p = seg_ptr(op, r0, rb);
+    base = (LAYOUT == SVLA_LAYOUT_KC) ? (const char*)(p + (r0 - rb) * op.ld + (k0 - kb))
+                                      : (const char*)(p + (k0 - kb) * op.ld + (r0 - rb));
+  }
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
+  constexpr int RPI = (LAYOUT == SVLA_LAYOUT_KC) ? 0 : 64 / (TR / 8);
+  const int64_t krem = kv - k0;  // valid k extent left in this k-tile
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int k = (t >> 4) + 16 * i;
-      *reinterpret_cast<u32x4*>(lds + k * 256 + ((c ^ rc_swz(k)) << 4)) = st[i];
-    }
+  for (int i = 0; i < NI; ++i) {
+    const bool ok = (LAYOUT == SVLA_LAYOUT_KC) ? (st.kq < krem) : (st.kq + RPI * i < krem);
+    const uint32_t voff = ok ? st.voff[i] : OOB;
+    LDS_AS void* dst = (LDS_AS void*)(lds + (w * NI + i) * 1024);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, voff, 0, 0, 0);
   }
 }
 
 // ---- LDS -> MFMA operand fragment (16 rows starting at rb, k-step ks of 32)
-template <int LAYOUT>
+template <int LAYOUT, int TR>
 __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int ks, int lane) {
   if (LAYOUT == SVLA_LAYOUT_KC) {
     int row = rb + (lane & 15);
@@ -150,8 +152,8 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int ks, int
     const int rc = rb + 4 * p;
     const int chunk = rc >> 3, off = (rc & 7) * 2;
     const int k1 = 32 * ks + 8 * g + q, k2 = k1 + 4;
-    const LDS_AS s16x4* a1 = (const LDS_AS s16x4*)(lds + k1 * 256 + ((chunk ^ rc_swz(k1)) << 4) + off);
-    const LDS_AS s16x4* a2 = (const LDS_AS s16x4*)(lds + k2 * 256 + ((chunk ^ rc_swz(k2)) << 4) + off);
+    const LDS_AS s16x4* a1 = (const LDS_AS s16x4*)(lds + k1 * (2 * TR) + ((chunk ^ rc_swz(k1)) << 4) + off);
+    const LDS_AS s16x4* a2 = (const LDS_AS s16x4*)(lds + k2 * (2 * TR) + ((chunk ^ rc_swz(k2)) << 4) + off);
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)a1);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)a2);
     s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -182,14 +184,88 @@ __device__ __forceinline__ void load8f(const bf16_t* p, float* v, int64_t n_vali
   }
 }
 
-template <int LA, int LB>
-__global__ __launch_bounds__(NTH, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
-                                                       svla_operand B, CDesc C, svla_epilogue E) {
+// epilogue for one row/8-column chunk (all kinds except GEGLU, SOFTCAP_CE handled by the caller)
+__device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16_t* cp, int64_t m, int64_t n,
+                                          int64_t nv, float* v) {
+  switch (kind) {
+    case SVLA_EPI_STORE: {
+      if (E.accumulate) {
+        float o[8];
+        load8f(cp, o, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = E.alpha * v[j] + o[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= E.alpha;
+      }
+      store8(cp, v, nv);
+    } break;
+    case SVLA_EPI_BIAS: {
+      float b[8];
+      load8f((const bf16_t*)E.bias + n, b, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + b[j]) * E.alpha;
+      store8(cp, v, nv);
+    } break;
+    case SVLA_EPI_BIAS_GELU: {
+      float b[8], pre[8];
+      load8f((const bf16_t*)E.bias + n, b, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pre[j] = round_bf(v[j] + b[j]);
+        v[j] = gelu_tanh(pre[j]);
+      }
+      store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
+      store8(cp, v, nv);
+    } break;
+    case SVLA_EPI_BIAS_RESID: {
+      float b[8], r[8];
+      if (E.bias) load8f((const bf16_t*)E.bias + n, b, nv);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+      load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + b[j]) + r[j];
+      store8(cp, v, nv);
+    } break;
+    case SVLA_EPI_GEGLU_BWD: {
+      float g[8], u[8], dg[8], du[8];
+      load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, g, nv);
+      load8f((const bf16_t*)E.in1 + m * E.ld_in1 + n, u, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dh = round_bf(v[j]);
+        float act = round_bf(gelu_tanh(g[j]));
+        float dact = round_bf(dh * u[j]);
+        du[j] = dh * act;
+        dg[j] = dact * gelu_tanh_grad(g[j]);
+      }
+      store8((bf16_t*)E.out1 + m * E.ld_out1 + n, dg, nv);
+      store8((bf16_t*)E.out2 + m * E.ld_out2 + n, du, nv);
+    } break;
+    case SVLA_EPI_GELU_BWD: {
+      float pre[8];
+      load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, pre, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) * gelu_tanh_grad(pre[j]);
+      store8(cp, v, nv);
+    } break;
+    default:
+      break;
+  }
+}
+
+template <typename C, int LA, int LB>
+__global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
+                                                          svla_operand B, CDesc Cd, svla_epilogue E) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  constexpr int BM = C::BM, BN = C::BN, NTH = C::NTH, TM = C::TM, TN = C::TN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
   const int total = tiles_m * tiles_n;
-  int pid = xcd_remap(blockIdx.x, total);
+  const int pid = xcd_remap(blockIdx.x, total);
   const int group = GROUP_M * tiles_n;
   const int first_m = (pid / group) * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -197,214 +273,162 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(int64_t M, int64_t N, int6
   const int tn = (pid % group) / gsz;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
-
-  const int wr = w >> 1, wc = w & 1;
-  f32x4 acc[4][4];
+  const int wr = w / C::WGN, wc = w % C::WGN;
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const int64_t rvA = A.r_valid > 0 ? A.r_valid : M;
+  const int64_t kvA = A.k_valid > 0 ? A.k_valid : K;
+  const int64_t rvB = B.r_valid > 0 ? B.r_valid : (B.seg_dim == SVLA_SEG_GEGLU ? B.seg_start[1] : N);
+  const int64_t kvB = B.k_valid > 0 ? B.k_valid : K;
+  OpState<LA, BM, C::IA> sa;
+  OpState<LB, BN, C::IB> sb;
+  op_setup<LA, BM, C::IA>(A, m0, rvA, w, lane, sa);
+  op_setup<LB, BN, C::IB>(B, n0, rvB, w, lane, sb);
+
+  constexpr int NLD = C::IA + C::IB;  // LDS-DMA instructions per lane per k-tile
   const int nk = (int)((K + BK - 1) / BK);
-  u32x4 sa[4], sb[4];
-  load_tile<LA>(A, M, K, m0, 0, t, sa);
-  load_tile<LB>(B, N, K, n0, 0, t, sb);
-  store_tile<LA>(smem, t, sa);
-  store_tile<LB>(smem + 2 * TILE_BYTES, t, sb);
-  __syncthreads();
-
+  op_issue<LA, BM, C::IA>(A, sa, m0, 0, kvA, smem, w);
+  op_issue<LB, BN, C::IB>(B, sb, n0, 0, kvB, smem + C::A_BYTES, w);
+  if (nk > 1) {
+    op_issue<LA, BM, C::IA>(A, sa, m0, BK, kvA, smem + C::STAGE, w);
+    op_issue<LB, BN, C::IB>(B, sb, n0, BK, kvB, smem + C::STAGE + C::A_BYTES, w);
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_tile<LA>(A, M, K, m0, (int64_t)(kt + 1) * BK, t, sa);
-      load_tile<LB>(B, N, K, n0, (int64_t)(kt + 1) * BK, t, sb);
-    }
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* la = smem + cur * C::STAGE;
+    const char* lb = la + C::A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<LA>(smem + cur * TILE_BYTES, 64 * wr + 16 * i, ks, lane);
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<LA, BM>(la, C::WTM * wr + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<LB>(smem + (2 + cur) * TILE_BYTES, 64 * wc + 16 * j, ks, lane);
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<LB, BN>(lb, C::WTN * wc + 16 * j, ks, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      store_tile<LA>(smem + (cur ^ 1) * TILE_BYTES, t, sa);
-      store_tile<LB>(smem + (2 + (cur ^ 1)) * TILE_BYTES, t, sb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) {
+      op_issue<LA, BM, C::IA>(A, sa, m0, (int64_t)(kt + 2) * BK, kvA, smem + cur * C::STAGE, w);
+      op_issue<LB, BN, C::IB>(B, sb, n0, (int64_t)(kt + 2) * BK, kvB, smem + cur * C::STAGE + C::A_BYTES, w);
     }
-    __syncthreads();
   }
 
-  // ---------------- epilogue: accumulators -> LDS fp32 image [128][EPI_LD]
+  // ---------------- epilogue: 64-row passes through an fp32 LDS image [64][BN+4]
   float* Ei = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = 64 * wc + 16 * j + (lane & 15);
-      const int rowb = 64 * wr + 16 * i + 4 * (lane >> 4);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ei[(rowb + r) * EPI_LD + col] = acc[i][j][r];
-    }
-  __syncthreads();
-
-  // output segment (tile aligned along M)
   int cs = 0;
 #pragma unroll
   for (int i = 1; i < 4; ++i)
-    if (i < C.n && m0 >= C.start[i]) cs = i;
-  bf16_t* cbase = C.ptr[cs];
-  const int64_t cm0 = C.start[cs];
+    if (i < Cd.n && m0 >= Cd.start[i]) cs = i;
+  bf16_t* cbase = Cd.ptr[cs];
+  const int64_t cm0 = Cd.start[cs];
   const int kind = E.kind;
-
-  if (kind == SVLA_EPI_GEGLU) {
-    const int64_t I = N >> 1;
-    const int64_t nout0 = n0 >> 1;
-    const int cc = t & 7;
+  constexpr int CPR = BN / 8;     // 16-B chunks per row
+  constexpr int RPP = NTH / CPR;  // rows per thread-pass
+  const int cc = t % CPR;
 #pragma unroll 1
-    for (int i = 0; i < 4; ++i) {
-      const int row = (t >> 3) + 32 * i;
-      const int64_t m = m0 + row;
-      const int64_t n = nout0 + 8 * cc;
-      if (m >= M || n >= I) continue;
-      float g[8], u[8], h[8];
-      const float* pg = Ei + row * EPI_LD + 8 * cc;
-      const float* pu = pg + 64;
+  for (int pass = 0; pass < BM / 64; ++pass) {
+    // waves whose accumulator rows fall in [64*pass, 64*pass+64) write them
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        g[j] = round_bf(pg[j]);
-        u[j] = round_bf(pu[j]);
-        h[j] = round_bf(gelu_tanh(g[j])) * u[j];
+    for (int i = 0; i < TM; ++i) {
+      const int rbase = C::WTM * wr + 16 * i;
+      if (rbase >= 64 * pass && rbase < 64 * pass + 64) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = C::WTN * wc + 16 * j + (lane & 15);
+          const int r = rbase - 64 * pass + 4 * (lane >> 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Ei[(r + q) * C::EPI_LD + col] = acc[i][j][q];
+        }
       }
-      store8(cbase + (m - cm0) * C.ld + n, h, I - n);
-      store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
-      store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u, I - n);
     }
-    return;
-  }
-
-  const int cc = t & 15;
-  const int ntn = tiles_n;
+    __syncthreads();
+    if (kind == SVLA_EPI_GEGLU) {
+      // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
+      constexpr int HC = CPR / 2;
+      const int64_t I = N >> 1;
+      for (int idx = t; idx < 64 * HC; idx += NTH) {
+        const int row = idx / HC, c2 = idx % HC;
+        const int64_t m = m0 + 64 * pass + row;
+        const int64_t n = (n0 >> 1) + 8 * c2;
+        if (m < M && n < I) {
+          float g[8], u[8], h[8];
+          const float* pg = Ei + row * C::EPI_LD + 8 * c2;
+          const float* pu = pg + BN / 2;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            g[j] = round_bf(pg[j]);
+            u[j] = round_bf(pu[j]);
+            h[j] = round_bf(gelu_tanh(g[j])) * u[j];
+          }
+          store8(cbase + (m - cm0) * Cd.ld + n, h, I - n);
+          store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
+          store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u, I - n);
+        }
+      }
+    } else {
 #pragma unroll 1
-  for (int i = 0; i < 8; ++i) {
-    const int row = (t >> 4) + 16 * i;
-    const int64_t m = m0 + row;
-    const int64_t n = n0 + 8 * cc;
-    const int64_t nv = N - n;
-    float v[8];
-    {
-      const float* pe = Ei + row * EPI_LD + 8 * cc;
-      f32x4 x0 = *reinterpret_cast<const f32x4*>(pe);
-      f32x4 x1 = *reinterpret_cast<const f32x4*>(pe + 4);
-      v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
-      v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
-    }
-    if (kind == SVLA_EPI_SOFTCAP_CE) {
-      // softcap, round to bf16, per-(row, tile) online-softmax partials over the valid columns
-      float mx = -INFINITY, se = 0.f;
-      int am = 0x7fffffff;
-      const float cap = E.cap, icap = 1.0f / E.cap;
+      for (int rr = t / CPR; rr < 64; rr += RPP) {
+        const int64_t m = m0 + 64 * pass + rr;
+        const int64_t n = n0 + 8 * cc;
+        const int64_t nv = N - n;
+        float v[8];
+        {
+          const float* pe = Ei + rr * C::EPI_LD + 8 * cc;
+          f32x4 x0 = *reinterpret_cast<const f32x4*>(pe);
+          f32x4 x1 = *reinterpret_cast<const f32x4*>(pe + 4);
+          v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
+          v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
+        }
+        if (kind == SVLA_EPI_SOFTCAP_CE) {
+          // softcap, round to bf16, per-(row, 128-column group) online-softmax partials (16 lanes share one)
+          float mx = -INFINITY, se = 0.f;
+          int am = 0x7fffffff;
+          const float cap = E.cap, icap = 1.0f / E.cap;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = round_bf(cap * tanhf(v[j] * icap));
-        if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf(cap * tanhf(round_bf(v[j]) * icap));
+            if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nv) se += __expf(v[j] - mx);
+          if (mx == -INFINITY) se = 0.f;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            float mx2 = __shfl_xor(mx, o, 64), se2 = __shfl_xor(se, o, 64);
+            int am2 = __shfl_xor(am, o, 64);
+            float mn = fmaxf(mx, mx2);
+            float s1 = (mx == -INFINITY) ? 0.f : se * __expf(mx - mn);
+            float s2 = (mx2 == -INFINITY) ? 0.f : se2 * __expf(mx2 - mn);
+            int a = (mx > mx2 || (mx == mx2 && am < am2)) ? am : am2;
+            mx = mn; se = s1 + s2; am = a;
+          }
+          if (m < M) {
+            if ((cc & 15) == 0) {
+              const int64_t ntn = (N + 127) / 128;
+              float* rs = E.row_stats + (m * ntn + (n0 + 8 * cc) / 128) * 3;
+              rs[0] = mx; rs[1] = se; rs[2] = __int_as_float(am);
+            }
+            if (nv > 0) store8(cbase + (m - cm0) * Cd.ld + n, v, nv);
+          }
+          continue;
+        }
+        if (m >= M || nv <= 0) continue;
+        epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < nv) se += __expf(v[j] - mx);
-      if (mx == -INFINITY) se = 0.f;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        float mx2 = __shfl_xor(mx, o, 64), se2 = __shfl_xor(se, o, 64);
-        int am2 = __shfl_xor(am, o, 64);
-        float mn = fmaxf(mx, mx2);
-        float s1 = (mx == -INFINITY) ? 0.f : se * __expf(mx - mn);
-        float s2 = (mx2 == -INFINITY) ? 0.f : se2 * __expf(mx2 - mn);
-        int a = (mx > mx2 || (mx == mx2 && am < am2)) ? am : am2;
-        mx = mn; se = s1 + s2; am = a;
-      }
-      if (m < M) {
-        if (cc == 0) {
-          float* rs = E.row_stats + (m * ntn + tn) * 3;
-          rs[0] = mx; rs[1] = se; rs[2] = __int_as_float(am);
-        }
-        if (nv > 0) store8(cbase + (m - cm0) * C.ld + n, v, nv);
-      }
-      continue;
     }
-    if (m >= M || nv <= 0) continue;
-    bf16_t* cp = cbase + (m - cm0) * C.ld + n;
-    switch (kind) {
-      case SVLA_EPI_STORE: {
-        if (E.accumulate) {
-          float o[8];
-          load8f(cp, o, nv);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = E.alpha * v[j] + o[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= E.alpha;
-        }
-        store8(cp, v, nv);
-      } break;
-      case SVLA_EPI_BIAS: {
-        float b[8];
-        load8f((const bf16_t*)E.bias + n, b, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + b[j]) * E.alpha;
-        store8(cp, v, nv);
-      } break;
-      case SVLA_EPI_BIAS_GELU: {
-        float b[8], pre[8];
-        load8f((const bf16_t*)E.bias + n, b, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pre[j] = round_bf(v[j] + b[j]);
-          v[j] = gelu_tanh(pre[j]);
-        }
-        store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
-        store8(cp, v, nv);
-      } break;
-      case SVLA_EPI_BIAS_RESID: {
-        float b[8], r[8];
-        if (E.bias) load8f((const bf16_t*)E.bias + n, b, nv);
-        else
-#pragma unroll
-          for (int j = 0; j < 8; ++j) b[j] = 0.f;
-        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j] + b[j]) + r[j];
-        store8(cp, v, nv);
-      } break;
-      case SVLA_EPI_GEGLU_BWD: {
-        float g[8], u[8], dg[8], du[8];
-        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, g, nv);
-        load8f((const bf16_t*)E.in1 + m * E.ld_in1 + n, u, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float dh = round_bf(v[j]);
-          float act = round_bf(gelu_tanh(g[j]));
-          float dact = round_bf(dh * u[j]);
-          du[j] = dh * act;
-          dg[j] = dact * gelu_tanh_grad(g[j]);
-        }
-        store8((bf16_t*)E.out1 + m * E.ld_out1 + n, dg, nv);
-        store8((bf16_t*)E.out2 + m * E.ld_out2 + n, du, nv);
-      } break;
-      case SVLA_EPI_GELU_BWD: {
-        float pre[8];
-        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, pre, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = round_bf(v[j]) * gelu_tanh_grad(pre[j]);
-        store8(cp, v, nv);
-      } break;
-      default:
-        break;
-    }
+    __syncthreads();
   }
 }
 
@@ -417,9 +441,28 @@ void set_lds_once(int bytes) {
   }
 }
 
+template <typename C>
+int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
+           const svla_epilogue& E, hipStream_t s) {
+  const int64_t tiles = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
+  dim3 grid((unsigned)tiles), block(C::NTH);
+  const int la = A.layout, lb = B.layout;
+#define SVLA_LAUNCH(LA_, LB_)                                                                      \
+  {                                                                                                \
+    set_lds_once<gemm_kernel<C, LA_, LB_>>(C::LDS);                                                \
+    hipLaunchKernelGGL((gemm_kernel<C, LA_, LB_>), grid, block, C::LDS, s, M, N, K, A, B, Cd, E);  \
+  }
+  if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH(0, 0)
+  else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH(0, 1)
+  else if (la == SVLA_LAYOUT_RC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH(1, 0)
+  else SVLA_LAUNCH(1, 1)
+#undef SVLA_LAUNCH
+  return svla::check_launch("gemm");
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K, int64_t tileR) {
+int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K) {
   SVLA_CHECK_ARG(op != nullptr, "gemm: operand %s is NULL", name);
   SVLA_CHECK_ARG(op->layout == SVLA_LAYOUT_KC || op->layout == SVLA_LAYOUT_RC, "gemm: %s bad layout", name);
   SVLA_CHECK_ARG(op->nseg >= 1 && op->nseg <= 4, "gemm: %s nseg=%d", name, op->nseg);
@@ -434,13 +477,20 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
     SVLA_CHECK_ARG(op->seg_start[1] * 2 == R && op->seg_start[1] % 64 == 0,
                    "gemm: GEGLU rows per weight must be N/2 and a multiple of 64");
   } else if (op->nseg > 1) {
-    int64_t tile = op->seg_dim == SVLA_SEG_OUTER ? tileR : BK;
+    const int64_t tile = op->seg_dim == SVLA_SEG_OUTER ? 128 : BK;
     SVLA_CHECK_ARG(op->seg_start[0] == 0, "gemm: %s seg_start[0] must be 0", name);
     for (int i = 1; i < op->nseg; ++i)
       SVLA_CHECK_ARG(op->seg_start[i] % tile == 0 && op->seg_start[i] > op->seg_start[i - 1],
-                     "gemm: %s segment %d start %lld not tile aligned", name, i, (long long)op->seg_start[i]);
+                     "gemm: %s segment %d start %lld not tile aligned (%lld)", name, i, (long long)op->seg_start[i],
+                     (long long)tile);
   }
-  (void)K;
+  const int64_t kv = op->k_valid > 0 ? op->k_valid : K;
+  // KC: a 16-B chunk straddling the reduction extent would multiply garbage into every output -> the
+  // extent must be a multiple of 8 (zero-pad).  RC: a straddling chunk only feeds outputs beyond R,
+  // which are never stored (the row of a [K][ld] matrix is readable up to ld >= round8(R)).
+  if (op->layout == SVLA_LAYOUT_KC)
+    SVLA_CHECK_ARG(kv % 8 == 0, "gemm: %s (KC) reduction extent %lld must be a multiple of 8 (zero-pad)", name,
+                   (long long)kv);
   return 0;
 }
 
@@ -452,8 +502,8 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   SVLA_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
                  (long long)K);
   SVLA_CHECK_ARG(epi != nullptr, "gemm: epilogue is NULL");
-  if (int rc = check_operand(A, "A", M, K, BM)) return rc;
-  if (int rc = check_operand(B, "B", N, K, BN)) return rc;
+  if (int rc = check_operand(A, "A", M, K)) return rc;
+  if (int rc = check_operand(B, "B", N, K)) return rc;
   SVLA_CHECK_ARG(A->seg_dim != SVLA_SEG_GEGLU, "gemm: GEGLU segmentation is for B only");
   SVLA_CHECK_ARG((epi->kind == SVLA_EPI_GEGLU) == (B->seg_dim == SVLA_SEG_GEGLU && B->nseg == 2),
                  "gemm: EPI_GEGLU requires B with SVLA_SEG_GEGLU and vice versa");
@@ -469,7 +519,7 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
     C.ptr[i] = (bf16_t*)c_ptr[i];
     C.start[i] = c_seg_start ? c_seg_start[i] : 0;
     SVLA_CHECK_ARG(!needs_c || (C.ptr[i] && aligned16(C.ptr[i])), "gemm: C ptr[%d] null or misaligned", i);
-    if (i > 0) SVLA_CHECK_ARG(C.start[i] % BM == 0, "gemm: C segment start must be a multiple of 128");
+    if (i > 0) SVLA_CHECK_ARG(C.start[i] % 128 == 0, "gemm: C segment start must be a multiple of 128");
   }
   switch (epi->kind) {
     case SVLA_EPI_STORE: break;
@@ -490,22 +540,22 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
     default: SVLA_CHECK_ARG(false, "gemm: unknown epilogue %d", epi->kind);
   }
   if (epi->accumulate) SVLA_CHECK_ARG(epi->kind == SVLA_EPI_STORE, "gemm: accumulate only with EPI_STORE");
-  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  SVLA_CHECK_ARG(tiles < (1ll << 31), "gemm: too many tiles");
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((unsigned)tiles), block(NTH);
-  const int la = A->layout, lb = B->layout;
-  if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC)
-  { set_lds_once<gemm_kernel<0, 0>>(LDS_BYTES);
-    hipLaunchKernelGGL((gemm_kernel<0, 0>), grid, block, LDS_BYTES, s, M, N, K, *A, *B, C, *epi); }
-  else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC)
-  { set_lds_once<gemm_kernel<0, 1>>(LDS_BYTES);
-    hipLaunchKernelGGL((gemm_kernel<0, 1>), grid, block, LDS_BYTES, s, M, N, K, *A, *B, C, *epi); }
-  else if (la == SVLA_LAYOUT_RC && lb == SVLA_LAYOUT_KC)
-  { set_lds_once<gemm_kernel<1, 0>>(LDS_BYTES);
-    hipLaunchKernelGGL((gemm_kernel<1, 0>), grid, block, LDS_BYTES, s, M, N, K, *A, *B, C, *epi); }
-  else
-  { set_lds_once<gemm_kernel<1, 1>>(LDS_BYTES);
-    hipLaunchKernelGGL((gemm_kernel<1, 1>), grid, block, LDS_BYTES, s, M, N, K, *A, *B, C, *epi); }
-  return svla::check_launch("gemm");
+  // tile choice: the largest tile that still gives >= ~2 waves of blocks on the 256 CUs (1 block/CU);
+  // segment boundaries (outer segments, output segments, GeGLU halves) must not split a tile
+  auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  auto seg_ok = [&](int bm, int bn) {
+    if (B->seg_dim == SVLA_SEG_GEGLU && (B->seg_start[1] % (bn / 2)) != 0) return false;
+    bool ok = true;
+    if (B->nseg > 1 && B->seg_dim == SVLA_SEG_OUTER)
+      for (int i = 1; i < B->nseg; ++i) ok = ok && (B->seg_start[i] % bn == 0);
+    if (A->nseg > 1 && A->seg_dim == SVLA_SEG_OUTER)
+      for (int i = 1; i < A->nseg; ++i) ok = ok && (A->seg_start[i] % bm == 0);
+    for (int i = 1; i < c_nseg; ++i) ok = ok && (C.start[i] % bm == 0);
+    return ok;
+  };
+  if (tiles(256, 256) >= 512 && seg_ok(256, 256)) return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
+  if (tiles(256, 128) >= 256 && seg_ok(256, 128)) return launch<CfgMid>(M, N, K, *A, *B, C, *epi, s);
+  SVLA_CHECK_ARG(seg_ok(128, 128), "gemm: segment starts must be multiples of 128");
+  return launch<CfgSmall>(M, N, K, *A, *B, C, *epi, s);
 }

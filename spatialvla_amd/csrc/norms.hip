@@ -253,40 +253,38 @@ __global__ __launch_bounds__(NTH) void ln_bwd_kernel(int64_t rows, int64_t N, co
 }
 
 // ------------------------------------------------------------------ column reductions
-__global__ void colsum_f32_kernel(int64_t P, int64_t N, const float* __restrict__ in, bf16_t* __restrict__ out,
-                                  int acc) {
-  int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int64_t p = 0; p < P; ++p) s += in[p * N + n];
-  if (acc) s += bf2f(out[n]);
-  out[n] = f2bf(s);
-}
+// Deterministic column sums: a block owns 64 columns; its 256 threads are 4 row-groups of 64 lanes
+// (coalesced 256-B row segments), each summing a strided subset of its row range; the 4 partials are
+// combined in a fixed order through LDS.  grid.y splits the rows into independent partial rows.
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 
-// stage 1: 64 row-chunks, each thread a column pair of 8 consecutive columns
-__global__ void colsum_bf16_stage1(int64_t M, int64_t N, const bf16_t* __restrict__ x, int64_t ldx,
-                                   float* __restrict__ ws) {
-  const int64_t nch = (N + 7) >> 3;
-  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int part = blockIdx.y;  // 0..63
-  if (ch >= nch) return;
-  const int64_t rows_per = (M + 63) / 64;
-  const int64_t r0 = part * rows_per, r1 = min(M, r0 + rows_per);
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t n0 = ch * 8;
-  const bool full = n0 + 8 <= N;
-  for (int64_t r = r0; r < r1; ++r) {
-    const bf16_t* p = x + r * ldx + n0;
-    if (full) {
-      float f[8];
-      unpack8(*reinterpret_cast<const u32x4*>(p), f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += f[j];
+template <typename T, bool FINAL>
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t P, int64_t N, const T* __restrict__ in, int64_t ld,
+                                                     float* __restrict__ part, bf16_t* __restrict__ out, int acc) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t per = (P + gridDim.y - 1) / gridDim.y;
+  const int64_t p0 = (int64_t)blockIdx.y * per, p1 = min(P, p0 + per);
+  float s = 0.f;
+  if (n < N)
+    for (int64_t p = p0 + sg; p < p1; p += 4) s += ldf<T>(in + p * ld + n);
+  red[sg][cl] = s;
+  __syncthreads();
+  if (sg == 0 && n < N) {
+    float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    if (FINAL) {
+      if (acc) t += bf2f(out[n]);
+      out[n] = f2bf(t);
     } else {
-      for (int j = 0; j < 8 && n0 + j < N; ++j) s[j] += bf2f(p[j]);
+      part[(int64_t)blockIdx.y * N + n] = t;
     }
   }
-  for (int j = 0; j < 8 && n0 + j < N; ++j) ws[part * N + n0 + j] = s[j];
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -348,17 +346,17 @@ extern "C" int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const 
 extern "C" int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate,
                                void* stream) {
   SVLA_CHECK_ARG(P > 0 && N > 0 && in && out_bf16, "colsum_f32: bad args");
-  hipLaunchKernelGGL(colsum_f32_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream, P,
-                     N, in, (bf16_t*)out_bf16, accumulate);
+  hipLaunchKernelGGL((colsum_kernel<float, true>), dim3((unsigned)((N + 63) / 64), 1), dim3(256), 0,
+                     (hipStream_t)stream, P, N, in, N, (float*)nullptr, (bf16_t*)out_bf16, accumulate);
   return svla::check_launch("colsum_f32");
 }
 
 extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16,
                                 int32_t accumulate, float* workspace, void* stream) {
-  SVLA_CHECK_ARG(M > 0 && N > 0 && x && out_bf16 && workspace && ldx % 8 == 0 && al16(x), "colsum_bf16: bad args");
-  const int64_t nch = (N + 7) / 8;
-  hipLaunchKernelGGL(colsum_bf16_stage1, dim3((unsigned)((nch + 255) / 256), 64), dim3(256), 0,
-                     (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace);
+  SVLA_CHECK_ARG(M > 0 && N > 0 && x && out_bf16 && workspace && ldx >= N, "colsum_bf16: bad args");
+  const unsigned parts = (unsigned)((M + 63) / 64 < 64 ? (M + 63) / 64 : 64);
+  hipLaunchKernelGGL((colsum_kernel<bf16_t, false>), dim3((unsigned)((N + 63) / 64), parts), dim3(256), 0,
+                     (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace, (bf16_t*)nullptr, 0);
   if (int rc = svla::check_launch("colsum_bf16")) return rc;
-  return svla_colsum_f32(64, N, workspace, out_bf16, accumulate, stream);
+  return svla_colsum_f32(parts, N, workspace, out_bf16, accumulate, stream);
 }

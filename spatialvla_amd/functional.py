@@ -531,10 +531,10 @@ class LMHeadCEFn(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[0]:
             dh = torch.empty_like(h)
-            # K dimension = V: B operand = W [V, H] read RC with rows up to V (tail masked), A = dlog (zero-padded)
-            A = K._operand([dlog[:, :V]], L.LAYOUT_KC)
-            Bop = K._operand([w], L.LAYOUT_RC)
-            K.gemm(M, w.shape[1], V, A, Bop, [dh], [0], dh.stride(0), K._epi(L.EPI_STORE))
+            # reduction over the padded vocab: dlog is zero in [V, ldv); W rows beyond V read as 0 (k_valid=V)
+            A = K._operand([dlog], L.LAYOUT_KC, k_valid=ldv)
+            Bop = K._operand([w], L.LAYOUT_RC, k_valid=V)
+            K.gemm(M, w.shape[1], ldv, A, Bop, [dh], [0], dh.stride(0), K._epi(L.EPI_STORE))
         dw, acc, rw = _grad_dest(w, ctx.needs_input_grad[1])
         if dw is not None:
             K.linear_wgrad(dlog[:, :V], h, [dw], accumulate=acc)

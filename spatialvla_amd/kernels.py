@@ -38,8 +38,11 @@ def _ld(t: torch.Tensor) -> int:
 
 
 # ---------------------------------------------------------------------------------------- GEMM
-def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUTER, starts=None) -> L.Operand:
+def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUTER, starts=None, r_valid: int = 0,
+             k_valid: int = 0) -> L.Operand:
     op = L.Operand()
+    op.r_valid = int(r_valid)
+    op.k_valid = int(k_valid)
     ld = _ld(mats[0])
     for i, m in enumerate(mats):
         _chk_bf16(m, "gemm operand")

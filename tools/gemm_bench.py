@@ -1,0 +1,56 @@
+"""Microbenchmark of svla_gemm_bf16 on the SpatialVLA-4B GEMM shapes (B=32, M=9984), with torch.matmul
+(hipBLASLt) on the same operands as a yardstick.  Prints one line per shape: TFLOP/s and % of 2.5 PF."""
+import sys, os, time, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from spatialvla_amd import kernels as K, _lib as L
+
+BF = torch.bfloat16
+M = 9984
+SHAPES = [  # name, M, N, K, layouts
+    ("qkv fwd", M, 4096, 2304, "nt"), ("o fwd", M, 2304, 2048, "nt"), ("gate/up fwd", M, 18432, 2304, "nt"),
+    ("down fwd", M, 2304, 9216, "nt"), ("down dgrad", M, 9216, 2304, "nn"), ("gate/up dgrad", M, 2304, 18432, "nn"),
+    ("gate/up wgrad", 18432, 2304, M, "tn"), ("down wgrad", 2304, 9216, M, "tn"),
+    ("lm_head fwd", M, 265408, 2304, "nt"), ("siglip fc1 fwd", 8192, 4304, 1152, "nt"),
+]
+
+
+def run(name, m, n, k, lay, reps=10):
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(0)
+    if lay == "nt":
+        a = torch.randn(m, k, device=dev, generator=g).to(BF); b = torch.randn(n, k, device=dev, generator=g).to(BF)
+        A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_KC)
+        ref = lambda: a @ b.T
+    elif lay == "nn":
+        a = torch.randn(m, k, device=dev, generator=g).to(BF); b = torch.randn(k, n, device=dev, generator=g).to(BF)
+        A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_RC)
+        ref = lambda: a @ b
+    else:
+        a = torch.randn(k, m, device=dev, generator=g).to(BF); b = torch.randn(k, n, device=dev, generator=g).to(BF)
+        A, B = K._operand([a], L.LAYOUT_RC), K._operand([b], L.LAYOUT_RC)
+        ref = lambda: a.T @ b
+    c = torch.empty(m, n, dtype=BF, device=dev)
+    f = lambda: K.gemm(m, n, k, A, B, [c], [0], n, K._epi())
+    for fn in (f, ref):
+        for _ in range(2): fn()
+    torch.cuda.synchronize()
+    out = {}
+    for tag, fn in (("svla", f), ("torch", ref)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps): fn()
+        e1.record(); e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[tag] = (ms, 2.0 * m * n * k / ms / 1e9)
+    err = ((c.float() - ref().float()).norm() / ref().float().norm()).item()
+    print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} svla {out['svla'][0]:8.3f} ms {out['svla'][1]:7.1f} TF "
+          f"({out['svla'][1]/25:.1f}%)  torch {out['torch'][0]:8.3f} ms {out['torch'][1]:7.1f} TF  relerr {err:.1e}",
+          flush=True)
+
+
+if __name__ == "__main__":
+    sel = sys.argv[1:]
+    for s in SHAPES:
+        if not sel or any(x in s[0] for x in sel):
+            run(*s)
