@@ -12,7 +12,7 @@ import threading
 import torch  # noqa: F401  (must precede the dlopen below, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsvla.so")
+LIB_PATH = os.environ.get("SVLA_LIB") or os.path.join(_HERE, "libsvla.so")  # SVLA_LIB: diagnostic builds
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32

@@ -542,6 +542,40 @@ class LMHeadCEFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------ attention plug-in
+def kv_class_from_additive_mask(mask: Optional[torch.Tensor], B: int, Lq: int, Lk: int, device) -> torch.Tensor:
+    """Per-key classes (0 visible to all queries, 1 visible to queries i >= j, 2 never visible) equivalent to
+    the reference's additive [B,1,Lq,Lk] mask (modeling_spatialvla.py:258-306).  Raises ValueError when the
+    mask is not of that form (the kernel never materialises an L x L mask)."""
+    if mask is None:
+        return torch.zeros(B, Lk, dtype=torch.uint8, device=device)
+    if Lq != Lk:
+        raise ValueError(f"svla attention: query length {Lq} != key length {Lk} (KV cache not supported)")
+    vis = mask[:, 0, :, :Lk] == 0                                   # [B, Lq, Lk]
+    all_vis = vis.all(dim=1)
+    none_vis = ~vis.any(dim=1)
+    cls = torch.where(all_vis, 0, torch.where(none_vis, 2, 1)).to(torch.uint8)
+    i = torch.arange(Lq, device=device)
+    causal = i[:, None] >= i[None, :]
+    rebuilt = torch.where(cls[:, None, :] == 0, True, torch.where(cls[:, None, :] == 2, False, causal[None]))
+    if not bool((rebuilt == vis).all()):
+        raise ValueError("svla attention: mask is not a per-key prefix-LM/causal/padding mask")
+    return cls.contiguous()
+
+
+def gemma2_attention_forward(module, query, key, value, mask, **_kwargs):
+    """Drop-in entry for the reference's plugin table GEMMA2_ATTENTION_FUNCTION (modeling_gemma2.py:317-322,
+    called at :401-403 as fn(self, q, k, v, attention_mask, output_attentions=...)).  Same arguments and
+    return as eager_attention_forward (:169-195): q [B,Hq,L,D], k/v [B,Hkv,L,D] after RoPE, additive mask
+    [B,1,L,L] or None -> (out [B,L,Hq,D] contiguous, None).  Scale = module.scaling, softcap =
+    module.attn_logit_softcapping; probabilities are rounded to bf16 before PV as in the reference (Q3)."""
+    if _kwargs.get("output_attentions"):
+        raise NotImplementedError("svla attention does not materialise attention weights")
+    B, _, Lq, _ = query.shape
+    cls = kv_class_from_additive_mask(mask, B, Lq, key.shape[2], query.device)
+    softcap = getattr(module, "attn_logit_softcapping", None) or 0.0
+    return hip_attention(query, key, value, module.scaling, softcap, cls, 0), None
+
+
 def hip_attention(q, k, v, scale, softcap=0.0, kv_class=None, window=0):
     """Reference plug-in signature adapter (GEMMA2_ATTENTION_FUNCTION, modeling_gemma2.py:317-322):
     q [B, Hq, L, D], k/v [B, Hkv, L, D] (post-RoPE) -> [B, L, Hq, D].  Differentiable."""

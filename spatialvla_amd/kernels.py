@@ -118,6 +118,11 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
          _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap))
 
 
+# Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch
+# record a pair of HIP events on the stream it is launched on (the current torch stream).
+launch_timer: dict = {}
+
+
 def linear_geglu_fwd(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor, h: torch.Tensor, g: torch.Tensor,
                      u: torch.Tensor):
     """h = gelu_tanh(x Wg^T) * (x Wu^T); g, u saved (Gemma2MLP, modeling_gemma2.py:91-92)."""
@@ -126,7 +131,14 @@ def linear_geglu_fwd(x: torch.Tensor, w_gate: torch.Tensor, w_up: torch.Tensor, 
     _req(I % 64 == 0 and w_up.shape[0] == I, "geglu: intermediate size must be a multiple of 64")
     A = _operand([x], L.LAYOUT_KC)
     B = _operand([w_gate, w_up], L.LAYOUT_KC, L.SEG_GEGLU, [0, I])
+    rec = launch_timer.get("geglu")
+    if rec is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
     gemm(M, 2 * I, K, A, B, [h], [0], _ld(h), _epi(L.EPI_GEGLU, out1=g, out2=u))
+    if rec is not None:
+        e1.record(torch.cuda.current_stream())
+        rec.append((e0, e1, M, 2 * I, K))
 
 
 def linear_dgrad(dy: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, kind=L.EPI_STORE, in0=None,

@@ -137,6 +137,31 @@ def test_kvmask_matches_reference_additive_mask(training, ragged):
     assert torch.equal(visible, visible_ref)
 
 
+@pytest.mark.parametrize("training,ragged", [(True, False), (True, True), (False, True)])
+def test_plugin_mask_classes_from_additive_mask(training, ragged):
+    """The GEMMA2_ATTENTION_FUNCTION adapter recovers per-key classes from the reference's dense mask."""
+    import spatialvla_oracle as O
+    from spatialvla_amd import presets
+    from spatialvla_amd.functional import kv_class_from_additive_mask
+    from spatialvla_amd.modeling_gemma2 import KVMask
+    cfgd = H.cfg_dict("tiny")
+    b = presets.synthetic_batch(cfgd, batch=3, seed=7, ragged=ragged)
+    am, tt = torch.from_numpy(b["attention_mask"]), torch.from_numpy(b["token_type_ids"])
+    B, L = am.shape
+    dense = O.prefix_mask(am, tt, training, L, torch.bfloat16)
+    got = kv_class_from_additive_mask(dense, B, L, L, "cpu")
+    vis = dense[:, 0] == 0
+    i = torch.arange(L)
+    rebuilt = (got[:, None, :] == 0) | ((got[:, None, :] == 1) & (i[None, :] <= i[:, None]))
+    assert torch.equal(rebuilt, vis)
+    if not ragged:
+        assert torch.equal(got, KVMask.build(am, tt, training, B, L, "cpu").kv_class)
+    bad = dense.clone()
+    bad[0, 0, 3, 1] = torch.finfo(torch.bfloat16).min   # one masked cell in an otherwise visible column
+    with pytest.raises(ValueError):
+        kv_class_from_additive_mask(bad, B, L, L, "cpu")
+
+
 def test_ce_targets_match_reference_shift():
     from spatialvla_amd import presets
     from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration as M

@@ -253,6 +253,36 @@ def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
     assert rel_l2(dqkv[:, (Hq + Hkv) * D:].view(B, L, Hkv, D), vr.grad) < 2e-2
 
 
+def test_gemma2_attention_plugin_signature(cuda):
+    """functional.gemma2_attention_forward as the reference's GEMMA2_ATTENTION_FUNCTION entry: same call
+    (module, q, k, v, additive mask) and output layout as eager_attention_forward (modeling_gemma2.py:169-195)."""
+    import types
+    from spatialvla_amd.functional import gemma2_attention_forward
+    torch.manual_seed(8)
+    B, Hq, Hkv, L, D = 2, 8, 4, 130, 256
+    q = _r(B * Hq * L, D).view(B, Hq, L, D).detach().requires_grad_(True)
+    k = _r(B * Hkv * L, D).view(B, Hkv, L, D).detach().requires_grad_(True)
+    v = _r(B * Hkv * L, D).view(B, Hkv, L, D).detach().requires_grad_(True)
+    P = L - 13
+    i = torch.arange(L, device=cuda)
+    vis = (i[None, :] <= i[:, None]) | (i[None, :] < P)
+    mask = torch.where(vis, 0.0, torch.finfo(BF).min).to(BF)[None, None].expand(B, 1, L, L).contiguous()
+    mod = types.SimpleNamespace(scaling=1 / 16, attn_logit_softcapping=50.0, num_key_value_groups=2)
+    out, w = gemma2_attention_forward(mod, q, k, v, mask, output_attentions=False)
+    assert w is None and out.shape == (B, L, Hq, D) and out.is_contiguous()
+    kv_class = torch.zeros(B, L, dtype=torch.uint8, device=cuda)
+    kv_class[:, P:] = 1
+    qr, kr, vr = (t.detach().transpose(1, 2).float().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qr, kr, vr, 1 / 16, 50.0, kv_class, 0, None, None)
+    assert rel_l2(out, ref) < 1e-2
+    do = _r(B * L, Hq * D).view(B, L, Hq, D)
+    out.backward(do)
+    ref.backward(do.float())
+    assert rel_l2(q.grad.transpose(1, 2), qr.grad) < 2e-2
+    assert rel_l2(k.grad.transpose(1, 2), kr.grad) < 2e-2
+    assert rel_l2(v.grad.transpose(1, 2), vr.grad) < 2e-2
+
+
 # ------------------------------------------------------------------------------------------ glue
 def test_embed_merge(cuda):
     from spatialvla_amd import kernels as Kn
