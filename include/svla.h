@@ -146,7 +146,8 @@ int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, co
                        const float* rstd, const void* dy, const void* dres, void* dx, float* dwb_partial,
                        int64_t* n_partial, void* stream);
 /* out[n] = bf16(sum_p in[p, n]) (+ existing out if accumulate): reduces partial sums. */
-int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate, void* stream);
+int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate, float* workspace,
+                    void* stream);
 /* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients). workspace >= 64*N fp32 */
 int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16, int32_t accumulate,
                      float* workspace, void* stream);

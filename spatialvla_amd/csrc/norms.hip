@@ -344,10 +344,19 @@ extern "C" int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const 
 }
 
 extern "C" int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate,
-                               void* stream) {
+                               float* workspace, void* stream) {
   SVLA_CHECK_ARG(P > 0 && N > 0 && in && out_bf16, "colsum_f32: bad args");
-  hipLaunchKernelGGL((colsum_kernel<float, true>), dim3((unsigned)((N + 63) / 64), 1), dim3(256), 0,
-                     (hipStream_t)stream, P, N, in, N, (float*)nullptr, (bf16_t*)out_bf16, accumulate);
+  hipStream_t s = (hipStream_t)stream;
+  if (workspace && P > 64) {  // two fixed-order passes: P rows -> 64 partial rows -> out
+    const unsigned parts = 64;
+    hipLaunchKernelGGL((colsum_kernel<float, false>), dim3((unsigned)((N + 63) / 64), parts), dim3(256), 0, s, P, N,
+                       in, N, workspace, (bf16_t*)nullptr, 0);
+    if (int rc = svla::check_launch("colsum_f32")) return rc;
+    in = workspace;
+    P = parts;
+  }
+  hipLaunchKernelGGL((colsum_kernel<float, true>), dim3((unsigned)((N + 63) / 64), 1), dim3(256), 0, s, P, N, in, N,
+                     (float*)nullptr, (bf16_t*)out_bf16, accumulate);
   return svla::check_launch("colsum_f32");
 }
 
@@ -358,5 +367,5 @@ extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx
   hipLaunchKernelGGL((colsum_kernel<bf16_t, false>), dim3((unsigned)((N + 63) / 64), parts), dim3(256), 0,
                      (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace, (bf16_t*)nullptr, 0);
   if (int rc = svla::check_launch("colsum_bf16")) return rc;
-  return svla_colsum_f32(parts, N, workspace, out_bf16, accumulate, stream);
+  return svla_colsum_f32(parts, N, workspace, out_bf16, accumulate, nullptr, stream);
 }

@@ -96,6 +96,21 @@ def _starts(sizes):
     return out, acc
 
 
+def _merge_rows(mats: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Row blocks [N_i, K] that sit back to back in one allocation (the engine's flat parameter buffer) as a
+    single [sum N_i, K] view; otherwise unchanged."""
+    if len(mats) < 2:
+        return mats
+    K = mats[0].shape[1]
+    nxt = mats[0].data_ptr()
+    for m in mats:
+        if m.dim() != 2 or m.shape[1] != K or m.stride() != (K, 1) or m.data_ptr() != nxt:
+            return mats
+        nxt += m.numel() * m.element_size()
+    m0 = mats[0]
+    return [torch.as_strided(m0, (sum(m.shape[0] for m in mats), K), (K, 1))]
+
+
 def _aligned(sizes, mult):
     st, _ = _starts(sizes)
     return all(s % mult == 0 for s in st)
@@ -108,6 +123,8 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
     sizes = [w.shape[0] for w in weights]
     for w in weights:
         _req(w.shape[1] == K, f"linear: weight K {w.shape[1]} != {K}")
+    weights = _merge_rows(weights)
+    sizes = [w.shape[0] for w in weights]
     if len(weights) > 1 and not _aligned(sizes, 128):
         weights = [torch.cat(weights, 0)]
         sizes = [weights[0].shape[0]]
@@ -148,6 +165,8 @@ def linear_dgrad(dy: torch.Tensor, weights: List[torch.Tensor], out: torch.Tenso
     K = weights[0].shape[1]
     sizes = [w.shape[0] for w in weights]
     _req(sum(sizes) == N, "dgrad: weight rows must sum to dy columns")
+    weights = _merge_rows(weights)
+    sizes = [w.shape[0] for w in weights]
     if len(weights) > 1 and not _aligned(sizes, 64):
         weights = [torch.cat(weights, 0)]
         sizes = [N]
@@ -166,6 +185,8 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, outs: List[torch.Tensor], ac
     _req(sum(sizes) == N, "wgrad: out rows must sum to dy columns")
     for o in outs:
         _req(o.shape[1] == K and o.is_contiguous(), "wgrad: outputs must be contiguous [N_i, K]")
+    outs = _merge_rows(outs)
+    sizes = [o.shape[0] for o in outs]
     if len(outs) > 1 and not _aligned(sizes, 128):
         tmp = torch.empty(N, K, dtype=BF16, device=dy.device)
         linear_wgrad(dy, x, [tmp], accumulate=False)
@@ -209,8 +230,7 @@ def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False):
                                      _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart), _stream()),
             "rmsnorm_bwd")
     if dw_out is not None:
-        L.check(L.lib().svla_colsum_f32(npart.value, N, part.data_ptr(), dw_out.data_ptr(), int(dw_accumulate),
-                                        _stream()), "colsum_f32")
+        colsum_f32(part[:npart.value], dw_out, dw_accumulate)
 
 
 def layernorm_fwd(x, w, b, eps, y, mean, rstd):
@@ -229,13 +249,17 @@ def layernorm_bwd(x, w, mean, rstd, dy, dres, dx, dw_out, db_out, accumulate=Fal
                                        _stream()), "layernorm_bwd")
     # partial layout [nb][2][N]: reduce dw (stride 2N) and db separately via contiguous copies
     if dw_out is not None:
-        pw = part[:, 0].contiguous()
-        L.check(L.lib().svla_colsum_f32(nb, N, pw.data_ptr(), dw_out.data_ptr(), int(accumulate), _stream()),
-                "colsum_f32")
+        colsum_f32(part[:, 0].contiguous(), dw_out, accumulate)
     if db_out is not None:
-        pb = part[:, 1].contiguous()
-        L.check(L.lib().svla_colsum_f32(nb, N, pb.data_ptr(), db_out.data_ptr(), int(accumulate), _stream()),
-                "colsum_f32")
+        colsum_f32(part[:, 1].contiguous(), db_out, accumulate)
+
+
+def colsum_f32(part, out, accumulate=False):
+    """out[n] = bf16(sum_p part[p, n]) (+ out), two fixed-order passes when P > 64."""
+    P, N = part.shape
+    ws = torch.empty(64, N, dtype=torch.float32, device=part.device) if P > 64 else None
+    L.check(L.lib().svla_colsum_f32(P, N, part.data_ptr(), out.data_ptr(), int(accumulate), _ptr(ws), _stream()),
+            "colsum_f32")
 
 
 def colsum_bf16(x, out, accumulate=False):
