@@ -103,8 +103,10 @@ def _merge_rows(mats: List[torch.Tensor]) -> List[torch.Tensor]:
         return mats
     K = mats[0].shape[1]
     nxt = mats[0].data_ptr()
+    st = mats[0].untyped_storage().data_ptr()
     for m in mats:
-        if m.dim() != 2 or m.shape[1] != K or m.stride() != (K, 1) or m.data_ptr() != nxt:
+        if (m.dim() != 2 or m.shape[1] != K or m.stride() != (K, 1) or m.data_ptr() != nxt
+                or m.untyped_storage().data_ptr() != st):
             return mats
         nxt += m.numel() * m.element_size()
     m0 = mats[0]

@@ -52,8 +52,15 @@ def run(name, m, n, k, lay, reps=10):
 def stamps(m, n, k, lay="nt"):
     """Diagnostic build 12 (SVLA_GEMM_DIAG bit 3): per-wave s_memtime at every barrier of block 0."""
     dev = "cuda"
-    a = torch.randn(m, k, device=dev).to(BF); b = torch.randn(n, k, device=dev).to(BF)
-    A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_KC)
+    if lay == "nt":
+        a = torch.randn(m, k, device=dev).to(BF); b = torch.randn(n, k, device=dev).to(BF)
+        A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_KC)
+    elif lay == "nn":
+        a = torch.randn(m, k, device=dev).to(BF); b = torch.randn(k, n, device=dev).to(BF)
+        A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_RC)
+    else:
+        a = torch.randn(k, m, device=dev).to(BF); b = torch.randn(k, n, device=dev).to(BF)
+        A, B = K._operand([a], L.LAYOUT_RC), K._operand([b], L.LAYOUT_RC)
     c = torch.zeros(m, n, dtype=BF, device=dev)
     for _ in range(3):
         K.gemm(m, n, k, A, B, [c], [0], n, K._epi())
@@ -61,13 +68,15 @@ def stamps(m, n, k, lay="nt"):
     nst = (k + 31) // 32
     raw = c.view(-1).view(torch.int64)[: 8 * (2 * nst + 4)].cpu().view(8, 2 * nst + 4)[:, : 2 * nst + 1]
     d = (raw[:, 1:] - raw[:, :-1]).float()
-    print(f"stamps M={m} N={n} K={k}: phase-a mean {d[:, 0::2].mean():.0f}  phase-b mean {d[:, 1::2].mean():.0f} "
+    print(f"stamps {lay} M={m} N={n} K={k}: phase-a mean {d[:, 0::2].mean():.0f}  phase-b mean {d[:, 1::2].mean():.0f} "
           f"(s_memtime ticks); first stage {d[:, :2].tolist()[0]}, per-wave mean {d.mean(1).tolist()}")
 
 
 if __name__ == "__main__":
     if os.environ.get("SVLA_STAMPS"):
         stamps(9984, 18432, 2304)
+        stamps(9984, 9216, 2304, "nn")
+        stamps(18432, 2304, 9984, "tn")
         sys.exit(0)
     sel = sys.argv[1:]
     for s in SHAPES:
