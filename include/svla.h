@@ -89,6 +89,9 @@ typedef struct {
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                    const svla_epilogue* epi, void* stream);
+/* Tuning knob (not a reference interface): main-loop variant for the 256x256 tile.
+ * 0 = 8-phase ping-pong schedule (default), 1 = two-barrier schedule.  Returns 0. */
+int svla_gemm_set_variant(int variant);
 
 /* ------------------------------------------------------------------------------------------
  * Attention.  Reference: eager_attention_forward (model/modeling_gemma2.py:169-195) selected via

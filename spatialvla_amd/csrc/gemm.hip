@@ -256,6 +256,107 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
   }
 }
 
+// ---------------- epilogue: 64-row passes through an fp32 LDS image [64][BN+4]; write_pass(pass, Ei) stores
+// the accumulators of rows [64*pass, 64*pass+64) into the image
+template <int BM, int BN, int NTH, typename WritePass>
+__device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, int64_t n0, const CDesc& Cd,
+                                              const svla_epilogue& E, char* smem, int t, WritePass write_pass) {
+  constexpr int EPI_LD = BN + 4;
+  float* Ei = reinterpret_cast<float*>(smem);
+  int cs = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < Cd.n && m0 >= Cd.start[i]) cs = i;
+  bf16_t* cbase = Cd.ptr[cs];
+  const int64_t cm0 = Cd.start[cs];
+  const int kind = E.kind;
+  constexpr int CPR = BN / 8;     // 16-B chunks per row
+  constexpr int RPP = NTH / CPR;  // rows per thread-pass
+  const int cc = t % CPR;
+#pragma unroll 1
+  for (int pass = 0; pass < BM / 64; ++pass) {
+    write_pass(pass, Ei);
+    __syncthreads();
+    if (kind == SVLA_EPI_GEGLU) {
+      // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
+      constexpr int HC = CPR / 2;
+      const int64_t I = N >> 1;
+      for (int idx = t; idx < 64 * HC; idx += NTH) {
+        const int row = idx / HC, c2 = idx % HC;
+        const int64_t m = m0 + 64 * pass + row;
+        const int64_t n = (n0 >> 1) + 8 * c2;
+        if (m < M && n < I) {
+          float g[8], u[8], h[8];
+          const float* pg = Ei + row * EPI_LD + 8 * c2;
+          const float* pu = pg + BN / 2;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            g[j] = round_bf(pg[j]);
+            u[j] = round_bf(pu[j]);
+            h[j] = round_bf(gelu_tanh(g[j])) * u[j];
+          }
+          store8(cbase + (m - cm0) * Cd.ld + n, h, I - n);
+          store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
+          store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u, I - n);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int rr = t / CPR; rr < 64; rr += RPP) {
+        const int64_t m = m0 + 64 * pass + rr;
+        const int64_t n = n0 + 8 * cc;
+        const int64_t nv = N - n;
+        float v[8];
+        {
+          const float* pe = Ei + rr * EPI_LD + 8 * cc;
+          f32x4 x0 = *reinterpret_cast<const f32x4*>(pe);
+          f32x4 x1 = *reinterpret_cast<const f32x4*>(pe + 4);
+          v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
+          v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
+        }
+        if (kind == SVLA_EPI_SOFTCAP_CE) {
+          // softcap, round to bf16, per-(row, 128-column group) online-softmax partials (16 lanes share one)
+          float mx = -INFINITY, se = 0.f;
+          int am = 0x7fffffff;
+          const float cap = E.cap, icap = 1.0f / E.cap;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf(cap * tanhf(round_bf(v[j]) * icap));
+            if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nv) se += __expf(v[j] - mx);
+          if (mx == -INFINITY) se = 0.f;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            float mx2 = __shfl_xor(mx, o, 64), se2 = __shfl_xor(se, o, 64);
+            int am2 = __shfl_xor(am, o, 64);
+            float mn = fmaxf(mx, mx2);
+            float s1 = (mx == -INFINITY) ? 0.f : se * __expf(mx - mn);
+            float s2 = (mx2 == -INFINITY) ? 0.f : se2 * __expf(mx2 - mn);
+            int a = (mx > mx2 || (mx == mx2 && am < am2)) ? am : am2;
+            mx = mn; se = s1 + s2; am = a;
+          }
+          if (m < M) {
+            if ((cc & 15) == 0 && n < N) {  // a 128-column group that starts beyond N has no stats slot
+              const int64_t ntn = (N + 127) / 128;
+              float* rs = E.row_stats + (m * ntn + (n0 + 8 * cc) / 128) * 3;
+              rs[0] = mx; rs[1] = se; rs[2] = __int_as_float(am);
+            }
+            if (nv > 0) store8(cbase + (m - cm0) * Cd.ld + n, v, nv);
+          }
+          continue;
+        }
+        if (m >= M || nv <= 0) continue;
+        epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+
 template <typename C, int LA, int LB>
 __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
                                                           svla_operand B, CDesc Cd, svla_epilogue E) {
@@ -324,20 +425,7 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
     }
   }
 
-  // ---------------- epilogue: 64-row passes through an fp32 LDS image [64][BN+4]
-  float* Ei = reinterpret_cast<float*>(smem);
-  int cs = 0;
-#pragma unroll
-  for (int i = 1; i < 4; ++i)
-    if (i < Cd.n && m0 >= Cd.start[i]) cs = i;
-  bf16_t* cbase = Cd.ptr[cs];
-  const int64_t cm0 = Cd.start[cs];
-  const int kind = E.kind;
-  constexpr int CPR = BN / 8;     // 16-B chunks per row
-  constexpr int RPP = NTH / CPR;  // rows per thread-pass
-  const int cc = t % CPR;
-#pragma unroll 1
-  for (int pass = 0; pass < BM / 64; ++pass) {
+  tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
     // waves whose accumulator rows fall in [64*pass, 64*pass+64) write them
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -348,88 +436,311 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
           const int col = C::WTN * wc + 16 * j + (lane & 15);
           const int r = rbase - 64 * pass + 4 * (lane >> 4);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) Ei[(r + q) * C::EPI_LD + col] = acc[i][j][q];
+          for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = acc[i][j][q];
         }
       }
     }
-    __syncthreads();
-    if (kind == SVLA_EPI_GEGLU) {
-      // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
-      constexpr int HC = CPR / 2;
-      const int64_t I = N >> 1;
-      for (int idx = t; idx < 64 * HC; idx += NTH) {
-        const int row = idx / HC, c2 = idx % HC;
-        const int64_t m = m0 + 64 * pass + row;
-        const int64_t n = (n0 >> 1) + 8 * c2;
-        if (m < M && n < I) {
-          float g[8], u[8], h[8];
-          const float* pg = Ei + row * C::EPI_LD + 8 * c2;
-          const float* pu = pg + BN / 2;
+  });
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, 8-phase ping-pong main loop (the structure that keeps the MFMA pipe fed at 1 block/CU).
+//
+//  * 8 waves = two groups of 4 (G0 = waves 0-3, G1 = waves 4-7; partners on a SIMD are w and w+4).  G1 runs
+//    one s_barrier behind G0, so on every SIMD one wave is in its MFMA section while its partner issues
+//    LDS reads and LDS-DMA: the matrix pipe never waits for a fragment read.
+//  * The tile is four 128-row half-tiles per K-step of 64: A_h0, A_h1 (rows 0-127, 128-255) and B_h0, B_h1.
+//    Wave (wr = w>>2, wc = w&3) owns rows {64wr..64wr+63} of each A half and columns {32wc..32wc+31} of each
+//    B half: four 64x32 quadrants, one per phase, 16 MFMAs each.
+//  * Phases of K-tile t (buffer t&1):  p1 read A_h0+B_h0 -> (0,0);  p2 read B_h1 -> (0,1);
+//    p3 read A_h1 -> (1,1);  p4 -> (1,0).  Every phase: [LDS-DMA one half-tile] reads, lgkmcnt(0), barrier,
+//    MFMAs, barrier.  A half-tile is restaged one or more phases after its last read (A_h0 of t+2 in p2,
+//    B_h0 in p3, B_h1 in p4, A_h1 of t+1 in p1), so two LDS buffers suffice; the only vmcnt wait is in p4
+//    (vmcnt(6): the three half-tiles of t+2 stay in flight across the barriers).
+// ---------------------------------------------------------------------------------------------
+namespace p8 {
+constexpr int BM = 256, BN = 256, HALF = 128, NTH = 512;
+constexpr int HB = HALF * BK * 2;  // bytes per half-tile image (16 KiB)
+constexpr int STAGE = 4 * HB;      // A_h0 | A_h1 | B_h0 | B_h1
+constexpr int LDS = 2 * STAGE;     // 128 KiB (the 66.5 KiB epilogue image reuses it)
+static_assert(64 * (BN + 4) * 4 <= LDS, "epilogue image must fit");
+}  // namespace p8
+
+template <int LAYOUT>
+struct HalfOp {
+  uint32_t voff[2][2];  // [half][instruction]: per-lane byte offset of the DMA chunk, OOB beyond the valid rows
+  int kq;               // KC: k offset of this lane's chunk; RC: k-row of instruction 0
+};
+
+// instruction (w, i) of a half-tile: KC rows 8(2w+i)..+7; RC k-rows 4(2w+i)..+3 (see OpState for the images)
+template <int LAYOUT>
+__device__ __forceinline__ void half_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane,
+                                           HalfOp<LAYOUT>& st) {
+  const int64_t ldb = op.ld * 2;
+  if (LAYOUT == SVLA_LAYOUT_KC) {
+    const int gc = (lane & 7) ^ (lane >> 3);
+    st.kq = gc * 8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            g[j] = round_bf(pg[j]);
-            u[j] = round_bf(pu[j]);
-            h[j] = round_bf(gelu_tanh(g[j])) * u[j];
-          }
-          store8(cbase + (m - cm0) * Cd.ld + n, h, I - n);
-          store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
-          store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u, I - n);
-        }
-      }
-    } else {
-#pragma unroll 1
-      for (int rr = t / CPR; rr < 64; rr += RPP) {
-        const int64_t m = m0 + 64 * pass + rr;
-        const int64_t n = n0 + 8 * cc;
-        const int64_t nv = N - n;
-        float v[8];
-        {
-          const float* pe = Ei + rr * C::EPI_LD + 8 * cc;
-          f32x4 x0 = *reinterpret_cast<const f32x4*>(pe);
-          f32x4 x1 = *reinterpret_cast<const f32x4*>(pe + 4);
-          v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3];
-          v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
-        }
-        if (kind == SVLA_EPI_SOFTCAP_CE) {
-          // softcap, round to bf16, per-(row, 128-column group) online-softmax partials (16 lanes share one)
-          float mx = -INFINITY, se = 0.f;
-          int am = 0x7fffffff;
-          const float cap = E.cap, icap = 1.0f / E.cap;
+    for (int i = 0; i < 2; ++i) {
+      const int row = 8 * (2 * w + i) + (lane >> 3);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf(cap * tanhf(round_bf(v[j]) * icap));
-            if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (j < nv) se += __expf(v[j] - mx);
-          if (mx == -INFINITY) se = 0.f;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            float mx2 = __shfl_xor(mx, o, 64), se2 = __shfl_xor(se, o, 64);
-            int am2 = __shfl_xor(am, o, 64);
-            float mn = fmaxf(mx, mx2);
-            float s1 = (mx == -INFINITY) ? 0.f : se * __expf(mx - mn);
-            float s2 = (mx2 == -INFINITY) ? 0.f : se2 * __expf(mx2 - mn);
-            int a = (mx > mx2 || (mx == mx2 && am < am2)) ? am : am2;
-            mx = mn; se = s1 + s2; am = a;
-          }
-          if (m < M) {
-            if ((cc & 15) == 0) {
-              const int64_t ntn = (N + 127) / 128;
-              float* rs = E.row_stats + (m * ntn + (n0 + 8 * cc) / 128) * 3;
-              rs[0] = mx; rs[1] = se; rs[2] = __int_as_float(am);
-            }
-            if (nv > 0) store8(cbase + (m - cm0) * Cd.ld + n, v, nv);
-          }
-          continue;
-        }
-        if (m >= M || nv <= 0) continue;
-        epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
+      for (int h = 0; h < 2; ++h) {
+        // GeGLU: half 0 = gate rows n0/2.., half 1 = up rows n0/2.. (same row index, different tensor)
+        const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + row : r0 + p8::HALF * h + row;
+        st.voff[h][i] = grow < rv ? (uint32_t)(row * ldb + gc * 16) : OOB;
       }
     }
-    __syncthreads();
+  } else {
+    st.kq = 8 * w + lane / 16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kr = st.kq + 4 * i;
+      const int gc = (lane % 16) ^ rc_swz(kr);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        st.voff[h][i] = (r0 + p8::HALF * h + gc * 8 < rv) ? (uint32_t)(kr * ldb + gc * 16) : OOB;
+    }
   }
+}
+
+// base address of half H of an operand at k = 0 (segment resolved once per tile: the 8-phase kernel is only
+// dispatched when no operand is segmented along k)
+template <int LAYOUT>
+__device__ __forceinline__ const char* half_base(const svla_operand& op, int64_t r0, int H) {
+  if (LAYOUT == SVLA_LAYOUT_KC && op.seg_dim == SVLA_SEG_GEGLU)
+    return (const char*)((const bf16_t*)op.ptr[H] + (r0 >> 1) * op.ld);
+  const int64_t rh = r0 + p8::HALF * H;
+  int64_t rb = 0;
+  const bf16_t* p = seg_ptr(op, rh, rb);
+  return (const char*)(p + (rh - rb) * (LAYOUT == SVLA_LAYOUT_KC ? op.ld : 1));
+}
+
+template <int LAYOUT, int H>
+__device__ __forceinline__ void half_issue(const char* base, int64_t kstride, const HalfOp<LAYOUT>& st, int64_t k0,
+                                           int64_t kv, char* lds, int w) {
+  __amdgpu_buffer_rsrc_t rs = make_rsrc(base + k0 * kstride);
+  const int64_t krem = kv - k0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool ok = (LAYOUT == SVLA_LAYOUT_KC) ? (st.kq < krem) : (st.kq + 4 * i < krem);
+    const uint32_t voff = ok ? st.voff[H][i] : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(lds + (2 * w + i) * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+// MFMA operand fragment of a 128-row half-tile image.  RC fragments are read with inline-asm
+// ds_read_b64_tr_b16: through the builtin, hipcc treats the transpose read as aliasing every LDS-DMA in flight
+// and drains vmcnt(0) before it, which would serialise the ping-pong pipeline.  The pair is only combined into
+// the MFMA operand after the phase's lgkmcnt(0) + barrier (any register copy happens after the data landed).
+template <int LAYOUT>
+struct Frag;
+template <>
+struct Frag<SVLA_LAYOUT_KC> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const char* lds, int rb, int ks, int lane) {
+    v = read_frag<SVLA_LAYOUT_KC, p8::HALF>(lds, rb, ks, lane);
+  }
+  __device__ __forceinline__ bf16x8 get() const { return v; }
+};
+template <>
+struct Frag<SVLA_LAYOUT_RC> {
+  u32x2 lo, hi;
+  __device__ __forceinline__ void load(const char* lds, int rb, int ks, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int rc = rb + 4 * p;
+    const int chunk = rc >> 3, off = (rc & 7) * 2;
+    const int k1 = 32 * ks + 8 * g + q;  // k-row k1 + 4 has the same swizzle: offset 4 rows = 1 KiB
+    const uint32_t a = (uint32_t)(uintptr_t)(const LDS_AS char*)(lds + k1 * (2 * p8::HALF) +
+                                                                  ((chunk ^ rc_swz(k1)) << 4) + off);
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:1024"
+                 : "=&v"(lo), "=v"(hi)
+                 : "v"(a));
+  }
+  __device__ __forceinline__ bf16x8 get() const {
+    const u32x4 r = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+};
+
+#define P8_BARRIER()                      \
+  __builtin_amdgcn_sched_barrier(0);      \
+  __builtin_amdgcn_s_barrier();           \
+  __builtin_amdgcn_sched_barrier(0)
+#define P8_LGKM0()                                         \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
+  __builtin_amdgcn_sched_barrier(0)
+
+template <int LA, int LB>
+__global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
+                                                        svla_operand B, CDesc Cd, svla_epilogue E) {
+  using namespace p8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+  const int total = tiles_m * tiles_n;
+  const int pid = xcd_remap(blockIdx.x, total);
+  const int group = GROUP_M * tiles_n;
+  const int first_m = (pid / group) * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (pid % group) % gsz;
+  const int tn = (pid % group) / gsz;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  f32x4 acc[2][4][2][2];  // [A half][16-row frag][B half][16-col frag]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][i][b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t rvA = A.r_valid > 0 ? A.r_valid : M;
+  const int64_t kvA = A.k_valid > 0 ? A.k_valid : K;
+  const int64_t rvB = B.r_valid > 0 ? B.r_valid : (B.seg_dim == SVLA_SEG_GEGLU ? B.seg_start[1] : N);
+  const int64_t kvB = B.k_valid > 0 ? B.k_valid : K;
+  HalfOp<LA> sa;
+  HalfOp<LB> sb;
+  half_setup<LA>(A, m0, rvA, w, lane, sa);
+  half_setup<LB>(B, n0, rvB, w, lane, sb);
+  const int nk = (int)((K + BK - 1) / BK);
+  const char* const a0p = half_base<LA>(A, m0, 0);
+  const char* const a1p = half_base<LA>(A, m0, 1);
+  const char* const b0p = half_base<LB>(B, n0, 0);
+  const char* const b1p = half_base<LB>(B, n0, 1);
+  const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
+
+  // prologue: K-tile 0 whole, K-tile 1 except A_h1 (issued in phase 1 of K-tile 0)
+  half_issue<LA, 0>(a0p, ksa, sa, 0, kvA, smem, w);
+  half_issue<LA, 1>(a1p, ksa, sa, 0, kvA, smem + HB, w);
+  half_issue<LB, 0>(b0p, ksb, sb, 0, kvB, smem + 2 * HB, w);
+  half_issue<LB, 1>(b1p, ksb, sb, 0, kvB, smem + 3 * HB, w);
+  if (nk > 1) {
+    half_issue<LA, 0>(a0p, ksa, sa, BK, kvA, smem + STAGE, w);
+    half_issue<LB, 0>(b0p, ksb, sb, BK, kvB, smem + STAGE + 2 * HB, w);
+    half_issue<LB, 1>(b1p, ksb, sb, BK, kvB, smem + STAGE + 3 * HB, w);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  P8_BARRIER();
+  if (wr) { P8_BARRIER(); }  // G1 runs one barrier behind G0
+
+  const int ra = 64 * wr, cb = 32 * wc;
+#pragma unroll 1
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
+    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
+    const int64_t k1 = (int64_t)(kt + 1) * BK, k2 = (int64_t)(kt + 2) * BK;
+    Frag<LA> a0[2][4], a1[2][4];
+    Frag<LB> b0[2][2], b1[2][2];
+
+    // ---- phase 1: (A_h0, B_h0)
+    if (more1) half_issue<LA, 1>(a1p, ksa, sa, k1, kvA, nxt + HB, w);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[ks][j].load(cur + 2 * HB, cb + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a0[ks][i].load(cur, ra + 16 * i, ks, lane);
+    }
+    P8_LGKM0();
+    P8_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b0[ks][j].get(), acc[0][i][0][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    P8_BARRIER();
+
+    // ---- phase 2: (A_h0, B_h1)
+    if (more2) half_issue<LA, 0>(a0p, ksa, sa, k2, kvA, cur, w);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[ks][j].load(cur + 3 * HB, cb + 16 * j, ks, lane);
+    P8_LGKM0();
+    P8_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b1[ks][j].get(), acc[0][i][1][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    P8_BARRIER();
+
+    // ---- phase 3: (A_h1, B_h1)
+    if (more2) half_issue<LB, 0>(b0p, ksb, sb, k2, kvB, cur + 2 * HB, w);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a1[ks][i].load(cur + HB, ra + 16 * i, ks, lane);
+    P8_LGKM0();
+    P8_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b1[ks][j].get(), acc[1][i][1][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    P8_BARRIER();
+
+    // ---- phase 4: (A_h1, B_h0); K-tile t+1 must have landed before the next phase 1 reads it
+    if (more2) {
+      half_issue<LB, 1>(b1p, ksb, sb, k2, kvB, cur + 3 * HB, w);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    P8_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b0[ks][j].get(), acc[1][i][0][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    P8_BARRIER();
+  }
+  if (!wr) { P8_BARRIER(); }  // re-align the groups
+  __syncthreads();
+
+  tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+    // pass p holds rows [64p, 64p+64) = A half (p>>1), group (p&1)
+    if ((pass & 1) == wr) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        if ((pass >> 1) != a) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int col = HALF * b + cb + 16 * j + (lane & 15);
+              const int r = 16 * i + 4 * (lane >> 4);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = acc[a][i][b][j][q];
+            }
+      }
+    }
+  });
 }
 
 template <auto KERN>
@@ -458,6 +769,24 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   else SVLA_LAUNCH(1, 1)
 #undef SVLA_LAUNCH
   return svla::check_launch("gemm");
+}
+
+int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
+            const svla_epilogue& E, hipStream_t s) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  dim3 grid((unsigned)tiles), block(p8::NTH);
+  const int la = A.layout, lb = B.layout;
+#define SVLA_LAUNCH8(LA_, LB_)                                                                         \
+  {                                                                                                    \
+    set_lds_once<gemm8_kernel<LA_, LB_>>(p8::LDS);                                                     \
+    hipLaunchKernelGGL((gemm8_kernel<LA_, LB_>), grid, block, p8::LDS, s, M, N, K, A, B, Cd, E);        \
+  }
+  if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH8(0, 0)
+  else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH8(0, 1)
+  else if (la == SVLA_LAYOUT_RC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH8(1, 0)
+  else SVLA_LAUNCH8(1, 1)
+#undef SVLA_LAUNCH8
+  return svla::check_launch("gemm8");
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -494,7 +823,14 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
   return 0;
 }
 
+int g_variant = 0;  // 0: 8-phase 256x256 kernel, 1: 2-barrier 256x256 kernel (A/B tuning knob)
+
 }  // namespace
+
+extern "C" int svla_gemm_set_variant(int v) {
+  g_variant = v;
+  return 0;
+}
 
 extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                               void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
@@ -554,7 +890,11 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
     for (int i = 1; i < c_nseg; ++i) ok = ok && (C.start[i] % bm == 0);
     return ok;
   };
-  if (tiles(256, 256) >= 512 && seg_ok(256, 256)) return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
+  if (tiles(256, 256) >= 512 && seg_ok(256, 256)) {
+    const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
+    if (g_variant == 0 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
+    return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
+  }
   if (tiles(256, 128) >= 256 && seg_ok(256, 128)) return launch<CfgMid>(M, N, K, *A, *B, C, *epi, s);
   SVLA_CHECK_ARG(seg_ok(128, 128), "gemm: segment starts must be multiples of 128");
   return launch<CfgSmall>(M, N, K, *A, *B, C, *epi, s);

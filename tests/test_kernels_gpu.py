@@ -39,6 +39,121 @@ def test_gemm_layouts(cuda, M, N, K, layouts):
     assert rel_l2(c, ref) < 5e-3
 
 
+def _both_variants(fn):
+    """Run fn() with the 8-phase (0) and the 2-barrier (1) 256x256 main loop; returns both results."""
+    from spatialvla_amd import _lib as L
+    outs = []
+    try:
+        for v in (1, 0):
+            L.lib().svla_gemm_set_variant(v)
+            outs.append(fn())
+            torch.cuda.synchronize()
+    finally:
+        L.lib().svla_gemm_set_variant(0)
+    return outs
+
+
+@pytest.mark.parametrize("M,N,K", [(2000, 16500, 200), (2304, 14336, 1000), (4100, 8200, 64)])
+@pytest.mark.parametrize("layouts", ["nt", "nn", "tn"])
+def test_gemm_big_tile(cuda, M, N, K, layouts):
+    """Shapes that take the 256x256 tile (>= 512 tiles): ragged M/N/K edges, all operand layouts.  Both main
+    loops accumulate every output in the same k order, so they must agree bitwise."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(5)
+    if layouts == "nt":
+        a, b = _r(M, K), _r(N, K)
+        ref = a.float() @ b.float().T
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_KC)
+    elif layouts == "nn":
+        a, b = _r(M, K), _r(K, N + (-N) % 8)[:, :N]
+        ref = a.float() @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_RC)
+    else:
+        a, b = _r(K, M + (-M) % 8)[:, :M], _r(K, N + (-N) % 8)[:, :N]
+        ref = a.float().T @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_RC), Kn._operand([b], L.LAYOUT_RC)
+
+    def run():
+        c = torch.full((M, N + (-N) % 8), 7.0, dtype=BF, device=cuda)
+        Kn.gemm(M, N, K, A, B, [c[:, :N]], [0], c.stride(0), Kn._epi())
+        return c
+
+    c1, c0 = _both_variants(run)
+    assert torch.equal(c0, c1)
+    assert rel_l2(c0[:, :N], ref) < 5e-3
+    assert bool((c0[:, N:] == 7.0).all())  # nothing written beyond N
+
+
+def test_gemm_big_tile_epilogues(cuda):
+    """GeGLU, GeGLU-backward, bias+residual, softcap-CE and dW C-segments on the 256x256 tile, bitwise vs the
+    2-barrier main loop."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(6)
+    M, K, I = 4200, 320, 8192
+    x, wg, wu = _r(M, K), _r(I, K, scale=0.1), _r(I, K, scale=0.1)
+
+    def geglu():
+        h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+        Kn.linear_geglu_fwd(x, wg, wu, h, g, u)
+        return h, g, u
+
+    (h1, g1, u1), (h0, g0, u0) = _both_variants(geglu)
+    assert torch.equal(h0, h1) and torch.equal(g0, g1) and torch.equal(u0, u1)
+    gr, ur = x.float() @ wg.float().T, x.float() @ wu.float().T
+    assert rel_l2(g0, gr) < 5e-3 and rel_l2(u0, ur) < 5e-3
+    assert rel_l2(h0, F.gelu(gr, approximate="tanh") * ur) < 1e-2
+
+    wd = _r(K, I, scale=0.1)
+    dout = _r(M, K)
+
+    def geglu_bwd():  # dgrad of down_proj with the GeGLU-backward epilogue: N = I, K' = K
+        dgu = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+        Kn.linear_dgrad(dout, [wd], dgu[:, :I], kind=L.EPI_GEGLU_BWD, in0=g0, in1=u0, out1=dgu[:, :I],
+                        out2=dgu[:, I:])
+        return dgu
+
+    d1, d0 = _both_variants(geglu_bwd)
+    assert torch.equal(d0, d1)
+
+    bias, res = _r(I, scale=0.5), _r(M, I)
+
+    def bias_resid():
+        y = torch.empty(M, I, dtype=BF, device=cuda)
+        Kn.linear_fwd(x, [wg], y, kind=L.EPI_BIAS_RESID, bias=bias, in0=res)
+        return y
+
+    y1, y0 = _both_variants(bias_resid)
+    assert torch.equal(y0, y1)
+    assert rel_l2(y0, gr + bias.float() + res.float()) < 5e-3
+
+    V = 30011
+    wv = _r(V, K, scale=0.2)
+    ldv = Kn.round_up(V, 64)
+    ntn = Kn.ceil_div(V, 128)
+
+    def softcap():
+        buf = torch.empty(M, ldv, dtype=BF, device=cuda)
+        stats = torch.empty(M, ntn, 3, dtype=torch.float32, device=cuda)
+        Kn.linear_fwd(x, [wv], buf[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=stats, cap=30.0)
+        return buf[:, :V], stats
+
+    (b1, s1), (b0, s0) = _both_variants(softcap)
+    assert torch.equal(b0, b1) and torch.equal(s0, s1)
+
+    # wgrad into 3 gradient tensors (C row segments) with accumulate
+    dy, x2 = _r(M, 2 * I), _r(M, 2304)
+    gs0 = [torch.zeros(s, 2304, dtype=BF, device=cuda) for s in (8192, 4096, 4096)]
+
+    def wgrad():
+        gs = [t.clone() for t in gs0]
+        Kn.linear_wgrad(dy, x2, gs)
+        return torch.cat(gs)
+
+    w1, w0 = _both_variants(wgrad)
+    assert torch.equal(w0, w1)
+    assert rel_l2(w0, dy.float().T @ x2.float()) < 5e-3
+
+
 def test_gemm_epilogues(cuda):
     from spatialvla_amd import kernels as Kn, _lib as L
     torch.manual_seed(1)

@@ -35,18 +35,25 @@ def run(name, m, n, k, lay, reps=10):
     for fn in (f, ref):
         for _ in range(2): fn()
     torch.cuda.synchronize()
-    out = {}
-    for tag, fn in (("svla", f), ("torch", ref)):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps): fn()
-        e1.record(); e1.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        out[tag] = (ms, 2.0 * m * n * k / ms / 1e9)
+    variants = [int(v) for v in os.environ.get("SVLA_VARIANTS", "0").split(",")]
+    arms = [(f"v{v}", v, f) for v in variants] + [("torch", None, ref)]
+    best = {}
+    for rnd in range(3):  # interleaved rounds in one process; report the best of 3 per arm
+        for tag, v, fn in arms:
+            if v is not None:
+                L.lib().svla_gemm_set_variant(v)
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps): fn()
+            e1.record(); e1.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            best[tag] = min(best.get(tag, 1e30), ms)
+    L.lib().svla_gemm_set_variant(variants[0])
+    f(); torch.cuda.synchronize()
     err = ((c.float() - ref().float()).norm() / ref().float().norm()).item()
-    print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} svla {out['svla'][0]:8.3f} ms {out['svla'][1]:7.1f} TF "
-          f"({out['svla'][1]/25:.1f}%)  torch {out['torch'][0]:8.3f} ms {out['torch'][1]:7.1f} TF  relerr {err:.1e}",
-          flush=True)
+    cols = "  ".join(f"{t} {best[t]:7.3f} ms {2.0 * m * n * k / best[t] / 1e9:7.1f} TF" for t, _, _ in arms)
+    print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} {cols}  relerr {err:.1e}", flush=True)
 
 
 def stamps(m, n, k, lay="nt"):
