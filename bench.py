@@ -87,7 +87,7 @@ def dominant_kernel_roofline(records):
     flops = 2.0 * M * N * K                          # algorithmic: M x (2I) x H multiply-adds
     ach = flops / (avg * 1e-3) / 1e12
     bytes_alg = 2.0 * (M * K + N * K + 3 * M * (N // 2))   # x, Wg, Wu read; h, g, u written (bf16)
-    return {"kernel": "svla gemm_kernel<256x256,KC,KC> EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
+    return {"kernel": "svla gemm8_kernel<KC,KC> (256x256 8-phase) EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(avg, 4),
             "launches_timed": len(ms), "algorithmic_flops_per_launch": flops,

@@ -90,8 +90,14 @@ int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                    const svla_epilogue* epi, void* stream);
 /* Tuning knob (not a reference interface): main-loop variant for the 256x256 tile.
- * 0 = 8-phase ping-pong schedule (default), 1 = two-barrier schedule.  Returns 0. */
+ * 0 = 8-phase ping-pong + stream-K (default), 1 = two-barrier schedule, 2 = 8-phase without
+ * stream-K.  Returns 0. */
 int svla_gemm_set_variant(int variant);
+/* Stream-K workspace of the 256x256 GEMM (caller-owned, zero-filled once before first use, 256-B aligned,
+ * at least svla_gemm_workspace_bytes() for the current device).  Without one (ws = NULL) every output tile
+ * runs whole.  GEMMs that use it must be ordered on one stream.  Returns 0 or SVLA_ERR_ARG. */
+size_t svla_gemm_workspace_bytes(void);
+int svla_gemm_set_workspace(void* ws, size_t bytes);
 
 /* ------------------------------------------------------------------------------------------
  * Attention.  Reference: eager_attention_forward (model/modeling_gemma2.py:169-195) selected via

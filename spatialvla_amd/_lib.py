@@ -51,6 +51,8 @@ SIGNATURES = {
                                ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64,
                                ctypes.POINTER(Epilogue), c_vp]),
     "svla_gemm_set_variant": (c_i32, [c_i32]),
+    "svla_gemm_workspace_bytes": (ctypes.c_size_t, []),
+    "svla_gemm_set_workspace": (c_i32, [c_vp, ctypes.c_size_t]),
     "svla_attn_fwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_vp]),
     "svla_attn_bwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, c_vp]),

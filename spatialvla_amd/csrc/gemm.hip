@@ -570,177 +570,315 @@ struct Frag<SVLA_LAYOUT_RC> {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
   __builtin_amdgcn_sched_barrier(0)
 
+// Stream-K schedule of the 8-phase kernel.  Output tiles [0, dp_tiles) run whole, round-robin over the grid;
+// the k-iterations of tiles [dp_tiles, tiles) are split evenly over the grid (block L owns iterations
+// [L*I/G, (L+1)*I/G)).  A block that ends with a partial tile writes its fp32 accumulators to a slab; the last
+// block to arrive at a tile (arrival counter, write-through slabs) sums the slabs in k order and runs
+// the epilogue — no block ever waits for another.
+struct SKArgs {
+  int dp_tiles;
+  int nk;
+  int grid;
+  int _pad;
+  int64_t sk_iters;  // (tiles - dp_tiles) * nk, >= grid when nonzero
+  float* slabs;      // [2 * grid][32 f32x4 x 512 threads]
+  int* counters;     // [tiles - dp_tiles] (< 2 * grid), zero between launches
+};
+
+#define P8_FOR_ACC(BODY)                         \
+  _Pragma("unroll") for (int a_ = 0; a_ < 2; ++a_)   \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)   \
+  _Pragma("unroll") for (int b_ = 0; b_ < 2; ++b_)   \
+  _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_) { \
+    const int r_ = ((a_ * 4 + i_) * 2 + b_) * 2 + j_; \
+    (void)r_;                                    \
+    BODY;                                        \
+  }
+
 template <int LA, int LB>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
-                                                        svla_operand B, CDesc Cd, svla_epilogue E) {
+                                                        svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
   using namespace p8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int t_in = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(t_in >> 6);
   const int wr = w >> 2, wc = w & 3;
-  const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
-  const int total = tiles_m * tiles_n;
-  const int pid = xcd_remap(blockIdx.x, total);
-  const int group = GROUP_M * tiles_n;
-  const int first_m = (pid / group) * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (pid % group) % gsz;
-  const int tn = (pid % group) / gsz;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-
-  f32x4 acc[2][4][2][2];  // [A half][16-row frag][B half][16-col frag]
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][i][b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
+  const int tiles_n = (int)((N + BN - 1) / BN), tiles_m = (int)((M + BM - 1) / BM);
+  const int L = xcd_remap(blockIdx.x, sk.grid);  // consecutive L share an XCD (and its L2)
+  const int nk = sk.nk;
   const int64_t rvA = A.r_valid > 0 ? A.r_valid : M;
   const int64_t kvA = A.k_valid > 0 ? A.k_valid : K;
   const int64_t rvB = B.r_valid > 0 ? B.r_valid : (B.seg_dim == SVLA_SEG_GEGLU ? B.seg_start[1] : N);
   const int64_t kvB = B.k_valid > 0 ? B.k_valid : K;
-  HalfOp<LA> sa;
-  HalfOp<LB> sb;
-  half_setup<LA>(A, m0, rvA, w, lane, sa);
-  half_setup<LB>(B, n0, rvB, w, lane, sb);
-  const int nk = (int)((K + BK - 1) / BK);
-  const char* const a0p = half_base<LA>(A, m0, 0);
-  const char* const a1p = half_base<LA>(A, m0, 1);
-  const char* const b0p = half_base<LB>(B, n0, 0);
-  const char* const b1p = half_base<LB>(B, n0, 1);
   const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
-
-  // prologue: K-tile 0 whole, K-tile 1 except A_h1 (issued in phase 1 of K-tile 0)
-  half_issue<LA, 0>(a0p, ksa, sa, 0, kvA, smem, w);
-  half_issue<LA, 1>(a1p, ksa, sa, 0, kvA, smem + HB, w);
-  half_issue<LB, 0>(b0p, ksb, sb, 0, kvB, smem + 2 * HB, w);
-  half_issue<LB, 1>(b1p, ksb, sb, 0, kvB, smem + 3 * HB, w);
-  if (nk > 1) {
-    half_issue<LA, 0>(a0p, ksa, sa, BK, kvA, smem + STAGE, w);
-    half_issue<LB, 0>(b0p, ksb, sb, BK, kvB, smem + STAGE + 2 * HB, w);
-    half_issue<LB, 1>(b1p, ksb, sb, BK, kvB, smem + STAGE + 3 * HB, w);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  P8_BARRIER();
-  if (wr) { P8_BARRIER(); }  // G1 runs one barrier behind G0
-
   const int ra = 64 * wr, cb = 32 * wc;
-#pragma unroll 1
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    char* nxt = smem + ((kt & 1) ^ 1) * STAGE;
-    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
-    const int64_t k1 = (int64_t)(kt + 1) * BK, k2 = (int64_t)(kt + 2) * BK;
-    Frag<LA> a0[2][4], a1[2][4];
-    Frag<LB> b0[2][2], b1[2][2];
+  f32x4 acc[2][4][2][2];  // [A half][16-row frag][B half][16-col frag]
 
-    // ---- phase 1: (A_h0, B_h0)
-    if (more1) half_issue<LA, 1>(a1p, ksa, sa, k1, kvA, nxt + HB, w);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b0[ks][j].load(cur + 2 * HB, cb + 16 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a0[ks][i].load(cur, ra + 16 * i, ks, lane);
-    }
-    P8_LGKM0();
-    P8_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b0[ks][j].get(), acc[0][i][0][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    P8_BARRIER();
+  auto coords = [&](int tile, int64_t& m0, int64_t& n0) {
+    const int group = GROUP_M * tiles_n;
+    const int first_m = (tile / group) * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    m0 = (int64_t)(first_m + (tile % group) % gsz) * BM;
+    n0 = (int64_t)((tile % group) / gsz) * BN;
+  };
 
-    // ---- phase 2: (A_h0, B_h1)
-    if (more2) half_issue<LA, 0>(a0p, ksa, sa, k2, kvA, cur, w);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b1[ks][j].load(cur + 3 * HB, cb + 16 * j, ks, lane);
-    P8_LGKM0();
-    P8_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b1[ks][j].get(), acc[0][i][1][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    P8_BARRIER();
-
-    // ---- phase 3: (A_h1, B_h1)
-    if (more2) half_issue<LB, 0>(b0p, ksb, sb, k2, kvB, cur + 2 * HB, w);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a1[ks][i].load(cur + HB, ra + 16 * i, ks, lane);
-    P8_LGKM0();
-    P8_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b1[ks][j].get(), acc[1][i][1][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    P8_BARRIER();
-
-    // ---- phase 4: (A_h1, B_h0); K-tile t+1 must have landed before the next phase 1 reads it
-    if (more2) {
-      half_issue<LB, 1>(b1p, ksb, sb, k2, kvB, cur + 3 * HB, w);
+  // acc = sum over k-tiles [kb, ke) of the (m0, n0) tile
+  auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
+    P8_FOR_ACC(acc[a_][i_][b_][j_] = (f32x4{0.f, 0.f, 0.f, 0.f}));
+    HalfOp<LA> sa;
+    HalfOp<LB> sb;
+    half_setup<LA>(A, m0, rvA, w, lane, sa);
+    half_setup<LB>(B, n0, rvB, w, lane, sb);
+    const char* const a0p = half_base<LA>(A, m0, 0);
+    const char* const a1p = half_base<LA>(A, m0, 1);
+    const char* const b0p = half_base<LB>(B, n0, 0);
+    const char* const b1p = half_base<LB>(B, n0, 1);
+    const int64_t kb0 = (int64_t)kb * BK;
+    // prologue: k-tile kb whole, k-tile kb+1 except A_h1 (issued in phase 1 of k-tile kb)
+    half_issue<LA, 0>(a0p, ksa, sa, kb0, kvA, smem, w);
+    half_issue<LA, 1>(a1p, ksa, sa, kb0, kvA, smem + HB, w);
+    half_issue<LB, 0>(b0p, ksb, sb, kb0, kvB, smem + 2 * HB, w);
+    half_issue<LB, 1>(b1p, ksb, sb, kb0, kvB, smem + 3 * HB, w);
+    if (kb + 1 < ke) {
+      half_issue<LA, 0>(a0p, ksa, sa, kb0 + BK, kvA, smem + STAGE, w);
+      half_issue<LB, 0>(b0p, ksb, sb, kb0 + BK, kvB, smem + STAGE + 2 * HB, w);
+      half_issue<LB, 1>(b1p, ksb, sb, kb0 + BK, kvB, smem + STAGE + 3 * HB, w);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     P8_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b0[ks][j].get(), acc[1][i][0][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    P8_BARRIER();
-  }
-  if (!wr) { P8_BARRIER(); }  // re-align the groups
-  __syncthreads();
+    if (wr) { P8_BARRIER(); }  // G1 runs one barrier behind G0
 
-  tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
-    // pass p holds rows [64p, 64p+64) = A half (p>>1), group (p&1)
-    if ((pass & 1) == wr) {
+#pragma unroll 1
+    for (int kt = kb; kt < ke; ++kt) {
+      char* cur = smem + ((kt - kb) & 1) * STAGE;
+      char* nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
+      const bool more1 = kt + 1 < ke, more2 = kt + 2 < ke;
+      const int64_t k1 = (int64_t)(kt + 1) * BK, k2 = (int64_t)(kt + 2) * BK;
+      Frag<LA> a0[2][4], a1[2][4];
+      Frag<LB> b0[2][2], b1[2][2];
+
+      // ---- phase 1: (A_h0, B_h0)
+      if (more1) half_issue<LA, 1>(a1p, ksa, sa, k1, kvA, nxt + HB, w);
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        if ((pass >> 1) != a) continue;
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b0[ks][j].load(cur + 2 * HB, cb + 16 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[ks][i].load(cur, ra + 16 * i, ks, lane);
+      }
+      P8_LGKM0();
+      P8_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
+          for (int j = 0; j < 2; ++j)
+            acc[0][i][0][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b0[ks][j].get(), acc[0][i][0][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      P8_BARRIER();
+
+      // ---- phase 2: (A_h0, B_h1)
+      if (more2) half_issue<LA, 0>(a0p, ksa, sa, k2, kvA, cur, w);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const int col = HALF * b + cb + 16 * j + (lane & 15);
-              const int r = 16 * i + 4 * (lane >> 4);
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-              for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = acc[a][i][b][j][q];
-            }
+        for (int j = 0; j < 2; ++j) b1[ks][j].load(cur + 3 * HB, cb + 16 * j, ks, lane);
+      P8_LGKM0();
+      P8_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[0][i][1][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[ks][i].get(), b1[ks][j].get(), acc[0][i][1][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      P8_BARRIER();
+
+      // ---- phase 3: (A_h1, B_h1)
+      if (more2) half_issue<LB, 0>(b0p, ksb, sb, k2, kvB, cur + 2 * HB, w);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a1[ks][i].load(cur + HB, ra + 16 * i, ks, lane);
+      P8_LGKM0();
+      P8_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[1][i][1][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b1[ks][j].get(), acc[1][i][1][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      P8_BARRIER();
+
+      // ---- phase 4: (A_h1, B_h0); k-tile kt+1 must have landed before the next phase 1 reads it
+      if (more2) {
+        half_issue<LB, 1>(b1p, ksb, sb, k2, kvB, cur + 3 * HB, w);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      P8_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[1][i][0][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks][i].get(), b0[ks][j].get(), acc[1][i][0][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      P8_BARRIER();
+    }
+    if (!wr) { P8_BARRIER(); }  // re-align the groups
+    __syncthreads();
+  };
+
+  auto epilogue = [&](int64_t m0, int64_t n0, const int t) {
+    const int lane = t & 63;
+    tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+      // pass p holds rows [64p, 64p+64) = A half (p>>1), group (p&1)
+      if ((pass & 1) == wr) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if ((pass >> 1) != a) continue;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const int col = HALF * b + cb + 16 * j + (lane & 15);
+                const int r = 16 * i + 4 * (lane >> 4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = acc[a][i][b][j][q];
+              }
+        }
+      }
+    });
+  };
+
+  // one work unit per iteration: whole tiles L, L+G, .. < dp_tiles, then this block's stream-K segments
+  const int64_t I = sk.sk_iters, G = sk.grid;
+  const int64_t it1 = ((int64_t)L + 1) * I / G;
+  int* sflag = reinterpret_cast<int*>(smem);
+  int dp_tile = L;
+  int64_t it = (int64_t)L * I / G;
+#pragma unroll 1
+  while (true) {
+    int tile, kb, ke, st = 0;
+    if (dp_tile < sk.dp_tiles) {
+      tile = dp_tile;
+      dp_tile += sk.grid;
+      kb = 0;
+      ke = nk;
+    } else {
+      if (it >= it1) break;
+      st = (int)(it / nk);
+      kb = (int)(it - (int64_t)st * nk);
+      ke = (int)min((int64_t)nk, kb + (it1 - it));
+      it += ke - kb;
+      tile = sk.dp_tiles + st;
+    }
+    // an opaque copy of the thread id per work unit: keeps hipcc from hoisting the epilogue's per-thread
+    // address arithmetic out of the unit loop, where it would stay live across the main loop and spill
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t_in));
+    int64_t m0, n0;
+    coords(tile, m0, n0);
+    mainloop(m0, n0, kb, ke, t & 63);
+    if (kb != 0 || ke != nk) {
+      // ---- partial tile: segments are owned by blocks Lh..Ll (start(L) = floor(L*I/G) is strictly increasing)
+      const int64_t T0 = (int64_t)st * nk, T1 = T0 + nk;
+      const int Lh = (int)(((T0 + 1) * G + I - 1) / I - 1);
+      const int Ll = (int)min(G - 1, (T1 * G + I - 1) / I - 1);
+      const int nseg = Ll - Lh + 1, j = L - Lh;
+      auto slab = [&](int seg) {  // the head segment is its block's last segment (slot 1), the others their first
+        return make_rsrc(reinterpret_cast<const f32x4*>(sk.slabs) +
+                         (int64_t)(2 * (Lh + seg) + (seg == 0 ? 1 : 0)) * (32 * NTH));
+      };
+      // Hand-off form (cdna_hip_programming.md G16 R1, MI355X_MICROARCH.md visibility table row 1): slabs are
+      // stored and loaded sc1 (write-through / L1-bypass), every storing wave drains vmcnt before the barrier,
+      // one lane adds to the tile's counter; the block whose add returns nseg-1 reduces.  No agent-scope fence:
+      // a release would write back the XCD L2's dirty output lines (tens of us), an acquire is replaced by the
+      // sc1 loads.
+      int* cnt = sk.counters + st;
+      bool last = false;
+      if (j == 0) {  // the head usually finishes last: if every other segment is in, skip the slab round trip
+        if (t == 0) {
+          const int c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sflag[0] = (c == nseg - 1);
+          if (c == nseg - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        last = sflag[0] != 0;
+        __syncthreads();
+      }
+      if (!last) {
+        const __amdgpu_buffer_rsrc_t rs = slab(j);
+        uint32_t vo = t * 16;
+        P8_FOR_ACC({
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a_][i_][b_][j_]), rs, vo, 0, 16);
+          vo += NTH * 16;
+          asm volatile("" : "+v"(vo));
+        });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+          const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sflag[0] = (old == nseg - 1);
+          if (old == nseg - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        last = sflag[0] != 0;
+        __syncthreads();
+      }
+      if (!last) continue;  // another block finishes this tile
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: loads stay below
+      // reducer: sum the segments in k order.  Every segment but a polled head is in its slab (this block's own
+      // included), so the order ((s0 + s1) + s2) + .. is the same whichever block reduces.  The offset is
+      // stepped opaquely: precomputed per-accumulator addresses would take VGPRs beside the 128 of acc.
+      for (int sg = (j != 0) ? 0 : 1; sg < nseg; ++sg) {
+        const __amdgpu_buffer_rsrc_t rs = slab(sg);
+        const bool first = sg == 0;
+        uint32_t vo = t * 16;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {  // 16 accumulators (256 B per lane) in flight per step
+          f32x4 x[4][2][2];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                x[i][b][jj] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, ((i * 2 + b) * 2 + jj) * NTH * 16, 16));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int jj = 0; jj < 2; ++jj)
+                acc[a][i][b][jj] = first ? x[i][b][jj] : acc[a][i][b][jj] + x[i][b][jj];
+          vo += 16 * NTH * 16;
+          asm volatile("" : "+v"(vo));
+        }
       }
     }
-  });
+    epilogue(m0, n0, t);
+  }
 }
 
 template <auto KERN>
@@ -771,15 +909,62 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   return svla::check_launch("gemm");
 }
 
+// main-loop variant of the 256x256 tile (A/B tuning knob): 0 = 8-phase + stream-K, 1 = 2-barrier kernel,
+// 2 = 8-phase without stream-K
+int g_variant = 0;
+
+struct SKWorkspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+SKWorkspace g_ws;
+
+int num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
+
+// 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
+size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }
+
 int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
             const svla_epilogue& E, hipStream_t s) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  dim3 grid((unsigned)tiles), block(p8::NTH);
+  SKArgs sk;
+  memset(&sk, 0, sizeof(sk));
+  sk.nk = (int)((K + BK - 1) / BK);
+  sk.dp_tiles = (int)tiles;
+  sk.grid = (int)tiles;
+  // stream-K over the tiles of the last, partial wave of the grid (persistent grid = one block per CU)
+  const int G = num_cus();
+  const int64_t rem = tiles % G;
+  int64_t sk_tiles = tiles < G ? tiles : rem;
+  // fewer than 8 k-tiles per block would split a tile over too many slabs: fold one more full wave into SK
+  if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
+  if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;  // last wave nearly full: nothing to balance
+  const size_t need = sk_workspace_bytes(G);
+  if (g_variant == 0 && g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
+      sk_tiles * sk.nk >= 8 * G) {
+    sk.dp_tiles = (int)(tiles - sk_tiles);
+    sk.grid = G;
+    sk.sk_iters = sk_tiles * sk.nk;
+    sk.slabs = reinterpret_cast<float*>(g_ws.ptr);
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(g_ws.ptr) + (size_t)2 * G * 32 * p8::NTH * 16);
+  }
+  dim3 grid((unsigned)sk.grid), block(p8::NTH);
   const int la = A.layout, lb = B.layout;
 #define SVLA_LAUNCH8(LA_, LB_)                                                                         \
   {                                                                                                    \
     set_lds_once<gemm8_kernel<LA_, LB_>>(p8::LDS);                                                     \
-    hipLaunchKernelGGL((gemm8_kernel<LA_, LB_>), grid, block, p8::LDS, s, M, N, K, A, B, Cd, E);        \
+    hipLaunchKernelGGL((gemm8_kernel<LA_, LB_>), grid, block, p8::LDS, s, M, N, K, A, B, Cd, E, sk);    \
   }
   if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH8(0, 0)
   else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH8(0, 1)
@@ -823,12 +1008,19 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
   return 0;
 }
 
-int g_variant = 0;  // 0: 8-phase 256x256 kernel, 1: 2-barrier 256x256 kernel (A/B tuning knob)
-
 }  // namespace
 
 extern "C" int svla_gemm_set_variant(int v) {
   g_variant = v;
+  return 0;
+}
+
+extern "C" size_t svla_gemm_workspace_bytes(void) { return sk_workspace_bytes(num_cus()); }
+
+extern "C" int svla_gemm_set_workspace(void* ws, size_t bytes) {
+  SVLA_CHECK_ARG(ws == nullptr || ((uintptr_t)ws & 255) == 0, "gemm workspace must be 256-B aligned");
+  g_ws.ptr = ws;
+  g_ws.bytes = ws ? bytes : 0;
   return 0;
 }
 
@@ -890,11 +1082,13 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
     for (int i = 1; i < c_nseg; ++i) ok = ok && (C.start[i] % bm == 0);
     return ok;
   };
-  if (tiles(256, 256) >= 512 && seg_ok(256, 256)) {
-    const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
-    if (g_variant == 0 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
-    return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
-  }
+  const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
+  const int64_t nk = (K + BK - 1) / BK;
+  const bool sk_ok = g_variant == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  if (g_variant != 1 && !kseg && seg_ok(256, 256) &&
+      (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
+    return launch8(M, N, K, *A, *B, C, *epi, s);
+  if (tiles(256, 256) >= 512 && seg_ok(256, 256)) return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   if (tiles(256, 128) >= 256 && seg_ok(256, 128)) return launch<CfgMid>(M, N, K, *A, *B, C, *epi, s);
   SVLA_CHECK_ARG(seg_ok(128, 128), "gemm: segment starts must be multiples of 128");
   return launch<CfgSmall>(M, N, K, *A, *B, C, *epi, s);

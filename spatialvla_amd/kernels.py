@@ -78,8 +78,23 @@ def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=
     return e
 
 
+_gemm_ws: dict = {}
+
+
+def _ensure_gemm_workspace():
+    """Register the stream-K workspace of the 256x256 GEMM once per process (zero-filled, caller-owned)."""
+    dev = torch.cuda.current_device()
+    if dev not in _gemm_ws:
+        n = int(L.lib().svla_gemm_workspace_bytes())
+        buf = torch.zeros(n, dtype=torch.uint8, device=f"cuda:{dev}")
+        L.check(L.lib().svla_gemm_set_workspace(buf.data_ptr(), n), "svla_gemm_set_workspace")
+        _gemm_ws[dev] = buf
+
+
 def gemm(M: int, N: int, K: int, A: L.Operand, B: L.Operand, c_mats: Sequence[Optional[torch.Tensor]],
          c_starts: Sequence[int], ldc: int, epi: L.Epilogue):
+    if not _gemm_ws:
+        _ensure_gemm_workspace()
     n = len(c_mats)
     cp = (ctypes.c_void_p * 4)(*([_ptr(c) for c in c_mats] + [None] * (4 - n)))
     cs = (ctypes.c_int64 * 5)(*([int(s) for s in c_starts] + [0] * (5 - n)))

@@ -98,7 +98,7 @@ def test_header_symbols_exported_by_library():
     """libsvla.so loads (no GPU needed) and exports every entry point declared in include/svla.h."""
     from spatialvla_amd import _lib
     hdr = open(os.path.join(REPO, "include", "svla.h")).read()
-    names = set(re.findall(r"^\s*(?:const char\*|int)\s+(svla_\w+)\s*\(", hdr, re.M))
+    names = set(re.findall(r"^\s*(?:const char\*|int|size_t)\s+(svla_\w+)\s*\(", hdr, re.M))
     assert len(names) >= 20
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for n in names:

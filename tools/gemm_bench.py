@@ -12,6 +12,10 @@ SHAPES = [  # name, M, N, K, layouts
     ("down fwd", M, 2304, 9216, "nt"), ("down dgrad", M, 9216, 2304, "nn"), ("gate/up dgrad", M, 2304, 18432, "nn"),
     ("gate/up wgrad", 18432, 2304, M, "tn"), ("down wgrad", 2304, 9216, M, "tn"),
     ("lm_head fwd", M, 265408, 2304, "nt"), ("siglip fc1 fwd", 8192, 4304, 1152, "nt"),
+    ("siglip qkv fwd", 8192, 3456, 1152, "nt"), ("siglip o fwd", 8192, 1152, 1152, "nt"),
+    ("siglip fc2 fwd", 8192, 1152, 4304, "nt"), ("siglip fc2 dgrad", 8192, 4304, 1152, "nn"),
+    ("siglip fc1 wgrad", 4304, 1152, 8192, "tn"), ("siglip o wgrad", 1152, 1152, 8192, "tn"),
+    ("qkv wgrad", 4096, 2304, M, "tn"), ("o dgrad", M, 2048, 2304, "nn"),
 ]
 
 

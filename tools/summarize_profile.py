@@ -36,7 +36,7 @@ def _key(n):
 
 
 def _is_dom(r):
-    return "gemm_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) == DOM_GRID
+    return re.search(r"gemm8?_kernel", r["Kernel_Name"]) is not None and int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) == DOM_GRID
 
 
 def trace(d, out):
