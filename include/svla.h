@@ -65,7 +65,11 @@ enum {
   SVLA_EPI_GEGLU = 4,      /* B uses SVLA_SEG_GEGLU; g->out1, u->out2, C = gelu_tanh(g)*u     */
   SVLA_EPI_GEGLU_BWD = 5,  /* acc = dH; in0=g, in1=u: out1 = dH*u*gelu'(g), out2 = dH*gelu(g) */
   SVLA_EPI_GELU_BWD = 6,   /* acc = dAct; in0 = pre-activation: C = dAct*gelu'(pre)           */
-  SVLA_EPI_SOFTCAP_CE = 7  /* C = cap*tanh(acc/cap); row_stats[m, tile_n] = {max,sumexp,argmax} */
+  SVLA_EPI_SOFTCAP_CE = 7, /* C = cap*tanh(acc/cap); row_stats[m, tile_n] = {max,sumexp,argmax} */
+  SVLA_EPI_ROPE = 8        /* C = bf16(acc), then Gemma2 rotate_half RoPE on columns < rope_cols (heads of
+                              rope_D, position m % rope_L, tables [rope_L][rope_D/2]) with the reference's bf16
+                              rounding: bf16(bf16(x*cos) + bf16(rotate_half(x)*sin))
+                              (model/modeling_gemma2.py:123-154) — q/k leave the QKV GEMM rotated */
 };
 
 typedef struct {
@@ -79,6 +83,12 @@ typedef struct {
   void* out1; int64_t ld_out1;
   void* out2; int64_t ld_out2;
   float* row_stats;          /* [M][ceil(N/128)][3] fp32 (SOFTCAP_CE) */
+  const void* rope_cos;      /* ROPE: bf16 [rope_L][rope_D/2] tables, row stride rope_ld */
+  const void* rope_sin;
+  int64_t rope_ld;
+  int64_t rope_cols;         /* columns [0, rope_cols) are rotated (q and k heads), the rest (v) plain */
+  int32_t rope_L;            /* sequence length: row m is position m % rope_L */
+  int32_t rope_D;            /* head dim; the GEMM tile width must be a multiple of it */
 } svla_epilogue;
 
 /* C: up to 4 row segments (c_seg_start tile-aligned to 128) — lets dW of q/k/v (or gate/up)
@@ -110,9 +120,11 @@ int svla_gemm_set_workspace(void* ws, size_t bytes);
  * Masked scores take the bf16 minimum (-3.3895e38) exactly as the reference's additive mask.
  * q/k/v are read in place from projection outputs: element (b, t, h, d) at
  *   base + (b*L + t)*ld + h*D + d.
- * rope_cos/rope_sin (optional, [L][D/2] bf16, row stride rope_ld) apply Gemma2 rotate_half RoPE
- * to q and k on load (forward) and its transpose to dq/dk (backward).
- * head_dim D in {256, 72}.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
+ * q and k arrive already rotated (Gemma2 RoPE is applied in the QKV GEMM epilogue, SVLA_EPI_ROPE).
+ * rope_cos/rope_sin ([L][D/2] bf16, row stride rope_ld) are for svla_attn_bwd only: with them dq/dk are
+ * returned w.r.t. the pre-rotation q/k (the transpose of rotate_half RoPE applied to the gradients);
+ * svla_attn_fwd rejects them.
+ * head_dim D in {256, 72}; L <= 8192.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
  * ---------------------------------------------------------------------------------------- */
 typedef struct {
   int32_t B, L, Hq, Hkv, D;
@@ -123,7 +135,7 @@ typedef struct {
   const void* k; int64_t ldk;
   const void* v; int64_t ldv;
   const uint8_t* kv_class;   /* [B, L] or NULL (= all visible) */
-  const void* rope_cos;      /* [L][D/2] bf16 or NULL */
+  const void* rope_cos;      /* [L][D/2] bf16 or NULL (backward only) */
   const void* rope_sin;
   int64_t rope_ld;
 } svla_attn_args;

@@ -22,7 +22,7 @@ c_vp = ctypes.c_void_p
 # enums mirrored from include/svla.h
 LAYOUT_KC, LAYOUT_RC = 0, 1
 SEG_OUTER, SEG_K, SEG_GEGLU = 0, 1, 2
-EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EPI_GELU_BWD, EPI_SOFTCAP_CE = range(8)
+EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EPI_GELU_BWD, EPI_SOFTCAP_CE, EPI_ROPE = range(9)
 
 
 class Operand(ctypes.Structure):
@@ -33,7 +33,9 @@ class Operand(ctypes.Structure):
 class Epilogue(ctypes.Structure):
     _fields_ = [("kind", c_i32), ("accumulate", c_i32), ("alpha", c_f32), ("cap", c_f32), ("bias", c_vp),
                 ("in0", c_vp), ("ld_in0", c_i64), ("in1", c_vp), ("ld_in1", c_i64), ("out1", c_vp),
-                ("ld_out1", c_i64), ("out2", c_vp), ("ld_out2", c_i64), ("row_stats", c_vp)]
+                ("ld_out1", c_i64), ("out2", c_vp), ("ld_out2", c_i64), ("row_stats", c_vp),
+                ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64), ("rope_cols", c_i64), ("rope_L", c_i32),
+                ("rope_D", c_i32)]
 
 
 class AttnArgs(ctypes.Structure):

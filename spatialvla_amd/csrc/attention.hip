@@ -59,18 +59,6 @@ __device__ __forceinline__ bf16x8 pack_frag(const float* v) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
-// rotate a pair of 8-element chunks (d, d+128) by RoPE: lo' = lo*c - hi*s, hi' = hi*c + lo*s
-__device__ __forceinline__ void rope_pair(float* lo, float* hi, const bf16_t* cs, const bf16_t* sn) {
-  float c[8], s[8];
-  unpack8(*reinterpret_cast<const u32x4*>(cs), c);
-  unpack8(*reinterpret_cast<const u32x4*>(sn), s);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float a = lo[j], b = hi[j];
-    lo[j] = a * c[j] - b * s[j];
-    hi[j] = b * c[j] + a * s[j];
-  }
-}
 // transpose of rope_pair (gradient): dlo = dlo'*c + dhi'*s, dhi = dhi'*c - dlo'*s
 __device__ __forceinline__ void rope_pair_t(float& lo, float& hi, float c, float s) {
   float a = lo, b = hi;
@@ -78,76 +66,89 @@ __device__ __forceinline__ void rope_pair_t(float& lo, float& hi, float c, float
   hi = b * c - a * s;
 }
 
-// Stage a [64 rows][D] tile (row r -> global row row0+r of a (b,·,h) head slice) into LDS, zero
-// padding columns >= D and rows >= L.  With ROPE (D==256), chunk pairs (c, c+16) are rotated.
-template <int D, bool ROPE>
-__device__ __forceinline__ void stage_tile(char* lds, const bf16_t* base, int64_t ld, int row0, int L,
-                                           const svla_attn_args& a, int t) {
-  constexpr int RS = Cfg<D>::RS;
-  if constexpr (ROPE) {
-    static_assert(D == 256, "rope needs D=256");
-    for (int idx = t; idx < 64 * 16; idx += 256) {
-      const int r = idx >> 4, ch = idx & 15;
-      const int row = row0 + r;
-      u32x4 lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
-      if (row < L) {
-        const bf16_t* p = base + (int64_t)row * ld + ch * 8;
-        float fl[8], fh[8];
-        unpack8(*reinterpret_cast<const u32x4*>(p), fl);
-        unpack8(*reinterpret_cast<const u32x4*>(p + 128), fh);
-        const bf16_t* cs = (const bf16_t*)a.rope_cos + (int64_t)row * a.rope_ld + ch * 8;
-        const bf16_t* sn = (const bf16_t*)a.rope_sin + (int64_t)row * a.rope_ld + ch * 8;
-        rope_pair(fl, fh, cs, sn);
-        lo = pack8(fl);
-        hi = pack8(fh);
-      }
-      *reinterpret_cast<u32x4*>(lds + toff<RS>(r, ch)) = lo;
-      *reinterpret_cast<u32x4*>(lds + toff<RS>(r, ch + 16)) = hi;
-    }
-  } else {
-    constexpr int NCH = RS / 8;
-    for (int idx = t; idx < 64 * NCH; idx += 256) {
-      const int r = idx / NCH, ch = idx % NCH;
-      const int row = row0 + r;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (row < L && ch * 8 < D) v = *reinterpret_cast<const u32x4*>(base + (int64_t)row * ld + ch * 8);
-      *reinterpret_cast<u32x4*>(lds + toff<RS>(r, ch)) = v;
-    }
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA staging of a [ROWS][RS] tile (rows row0.. of a (b, ·, head) slice, D valid columns) into the
+// swizzled image toff<RS>: wave-instruction j writes 1 KiB lane-linearly (RPI = 512/RS rows); lane l lands at
+// row j*RPI + l/CPR, image chunk p = l%CPR, which holds global chunk p ^ 2*(row&7).  Rows >= nrows and
+// columns >= D read as zero (descriptor range check).
+template <int RS, int ROWS, int NW>
+__device__ __forceinline__ void glds_tile(char* lds, const bf16_t* base, int64_t ld, int nrows, int D, int w,
+                                          int lane) {
+  constexpr int CPR = RS / 8, RPI = 1024 / (2 * RS), NI = ROWS * RS * 2 / 1024;
+  static_assert(NI % NW == 0, "tile instructions must split evenly over the waves");
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
+#pragma unroll
+  for (int i = 0; i < NI / NW; ++i) {
+    const int j = w + NW * i;
+    const int r = j * RPI + lane / CPR;
+    const int ch = (lane % CPR) ^ ((r & 7) << 1);
+    const uint32_t voff = (r < nrows && ch * 8 < D) ? (uint32_t)(r * ld * 2 + ch * 16) : SVLA_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(lds + j * 1024), 16, voff, 0, 0, 0);
   }
 }
 
-// Per-lane register fragments of one row (the lane's query/key) for all k-steps over d:
-// frag[ks][j] = X[row][32ks + 8g + j]; rotated by RoPE in registers when ROPE.
-template <int D, bool ROPE>
+// transposed fragment via inline-asm ds_read_b64_tr_b16 (through the builtin, hipcc drains every LDS-DMA in
+// flight before it, which would serialise the prefetch); same element map as frag_tr.  Issue a batch with
+// load(), then tr_wait(), then get(): the pair is assembled only after the data landed.
+struct TrFrag {
+  u32x2 lo, hi;
+  template <int RS>
+  __device__ __forceinline__ void load(const char* lds, int rb, int c0, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int col = c0 + 4 * p;
+    const int r1 = rb + 4 * g + q;  // r1 + 16 has the same swizzle ((r & 7) unchanged)
+    const uint32_t a1 = (uint32_t)(uintptr_t)(const LDS_AS char*)(lds + toff<RS>(r1, col >> 3) + (col & 7) * 2);
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+                 : "=&v"(lo), "=v"(hi)
+                 : "v"(a1), "i"(16 * RS * 2));
+  }
+  __device__ __forceinline__ bf16x8 get() const {
+    const u32x4 r = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+};
+__device__ __forceinline__ void tr_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// acc[dt] += A(dt) * B over NDT d-tiles, A read transposed from LDS in batches of 8 (32 VGPRs in flight);
+// AT_A: the LDS operand is the MFMA A operand (else B)
+template <int RS, int NDT, bool AT_A>
+__device__ __forceinline__ void mfma_tr_sweep(f32x4 (&acc)[NDT], const char* lds, int rb, bf16x8 other, int lane) {
+#pragma unroll
+  for (int d0 = 0; d0 < NDT; d0 += 8) {
+    constexpr int CH = NDT < 8 ? NDT : 8;
+    TrFrag f[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (d0 + i < NDT) f[i].template load<RS>(lds, rb, 16 * (d0 + i), lane);
+    tr_wait();
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (d0 + i < NDT) {
+        if (AT_A) acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[i].get(), other, acc[d0 + i], 0, 0, 0);
+        else acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(other, f[i].get(), acc[d0 + i], 0, 0, 0);
+      }
+  }
+}
+
+// Per-lane register fragments of one row (the lane's query): f[ks] = X[row][32ks + 8g + j]
+template <int D>
 __device__ __forceinline__ void load_row_frags(bf16x8 (&f)[Cfg<D>::DP / 32], const bf16_t* rowp, bool valid,
-                                               const svla_attn_args& a, int row, int lane) {
+                                               int lane) {
   constexpr int NKS = Cfg<D>::DP / 32;
   const int g = lane >> 4;
-  float v[NKS][8];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     const int d = 32 * ks + 8 * g;
-    if (valid && d < D) unpack8(*reinterpret_cast<const u32x4*>(rowp + d), v[ks]);
-    else
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[ks][j] = 0.f;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (valid && d < D) v = *reinterpret_cast<const u32x4*>(rowp + d);
+    f[ks] = __builtin_bit_cast(bf16x8, v);
   }
-  if constexpr (ROPE) {
-    if (valid) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int d = 32 * ks + 8 * g;
-        rope_pair(v[ks], v[ks + 4], (const bf16_t*)a.rope_cos + (int64_t)row * a.rope_ld + d,
-                  (const bf16_t*)a.rope_sin + (int64_t)row * a.rope_ld + d);
-      }
-    }
-  }
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) f[ks] = pack_frag(v[ks]);
 }
 
-__device__ __forceinline__ bool visible(const uint8_t* cls, int kj, int qi, int window) {
-  const int c = cls ? cls[kj] : 0;
+__device__ __forceinline__ bool visible(int c, int kj, int qi, int window) {
   bool v = (c == 0) || (c == 1 && kj <= qi);
   if (window > 0 && qi - kj >= window) v = false;
   return v;
@@ -155,31 +156,45 @@ __device__ __forceinline__ bool visible(const uint8_t* cls, int kj, int qi, int 
 
 __device__ __forceinline__ float softcap_f(float z, float cap) { return cap > 0.f ? cap * tanhf(z / cap) : z; }
 
-// ================================================================== forward
-template <int D, bool ROPE>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out, int64_t ldo,
-                                                          float* __restrict__ lse) {
-  constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
-  constexpr int NKS = DP / 32, NDT = DV / 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsK = smem;
-  char* ldsV = smem + 64 * RS * 2;
-  uint8_t* lcls = (uint8_t*)(smem + 2 * 64 * RS * 2);
+// key classes of the whole sequence -> LDS (plain loads, before any LDS-DMA is in flight)
+__device__ __forceinline__ void load_classes(uint8_t* lcls, const uint8_t* cls, int L, int t, int nth) {
+  for (int i = t; i < L; i += nth) lcls[i] = cls ? cls[i] : 0;
+}
 
-  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+template <int D>
+constexpr int tile_bytes(int rows) { return rows * Cfg<D>::RS * 2; }
+
+// ================================================================== forward
+// Block = (query tile of 64, NH query heads sharing one kv head, batch); 4 waves per head, 16 queries per wave.
+// K/V tiles stream through two LDS stages by LDS-DMA: tile kt+1 lands while tile kt is consumed.
+template <int D, int NH>
+__global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
+                                                               int64_t ldo, float* __restrict__ lse) {
+  constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
+  constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH;
+  constexpr int TB = tile_bytes<D>(64), STAGE = 2 * TB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
+
+  const int b = blockIdx.z, qt = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int h = blockIdx.y * NH + (w >> 2), wq = w & 3;
   const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int L = a.L;
-  const int qi = qt * 64 + 16 * w + c;
+  const int qi = qt * 64 + 16 * wq + c;
   const bool qvalid = qi < L;
 
   const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
-  const uint8_t* cls = a.kv_class ? a.kv_class + (int64_t)b * L : nullptr;
 
+  load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 64 * NW);
   bf16x8 qf[NKS];
-  load_row_frags<D, ROPE>(qf, qbase + (int64_t)qi * a.ldq, qvalid, a, qi, lane);
+  load_row_frags<D>(qf, qbase + (int64_t)qi * a.ldq, qvalid, lane);
+  const int nkt = (L + 63) / 64;
+  glds_tile<RS, 64, NW>(smem, kbase, a.ldk, L, D, w, lane);
+  glds_tile<RS, 64, NW>(smem + TB, vbase, a.ldv, L, D, w, lane);
 
   f32x4 acc[NDT];
 #pragma unroll
@@ -187,14 +202,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(svla_attn_args a, bf16
   float m = -INFINITY, l = 0.f;
   const float LOG2E = 1.4426950408889634f;
 
-  const int nkt = (L + 63) / 64;
   for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
-    stage_tile<D, ROPE>(ldsK, kbase, a.ldk, kt * 64, L, a, t);
-    stage_tile<D, false>(ldsV, vbase, a.ldv, kt * 64, L, a, t);
-    if (t < 64) lcls[t] = (cls && kt * 64 + t < L) ? cls[kt * 64 + t] : 0;
-    __syncthreads();
-
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile kt landed for every wave; every wave is done with the stage refilled below
+    const char* ldsK = smem + (kt & 1) * STAGE;
+    const char* ldsV = ldsK + TB;
+    if (kt + 1 < nkt) {
+      char* nx = smem + ((kt + 1) & 1) * STAGE;
+      const int r0 = (kt + 1) * 64;
+      glds_tile<RS, 64, NW>(nx, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
+      glds_tile<RS, 64, NW>(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
+    }
     f32x4 s[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -209,10 +227,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(svla_attn_args a, bf16
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int kl = 16 * nt + 4 * g + j, kj = kt * 64 + kl;
+        const int kj = kt * 64 + 16 * nt + 4 * g + j;
         float v = softcap_f(s[nt][j] * a.scale, a.softcap);
         if (kj >= L) v = -INFINITY;
-        else if (!visible(a.kv_class ? lcls : nullptr, kl, qi - kt * 64, a.sliding_window)) v = MASKVAL;
+        else if (!visible(lcls[kj], kj, qi, a.sliding_window)) v = MASKVAL;
         x[nt][j] = v;
         mt = fmaxf(mt, v);
       }
@@ -238,9 +256,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(svla_attn_args a, bf16
       float pv[8] = {p[2 * ks][0], p[2 * ks][1], p[2 * ks][2], p[2 * ks][3],
                      p[2 * ks + 1][0], p[2 * ks + 1][1], p[2 * ks + 1][2], p[2 * ks + 1][3]};
       const bf16x8 pb = pack_frag(pv);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<RS>(ldsV, 32 * ks, 16 * dt, lane), pb, acc[dt], 0, 0, 0);
+      mfma_tr_sweep<RS, NDT, true>(acc, ldsV, 32 * ks, pb, lane);
     }
   }
   l += __shfl_xor(l, 16, 64);
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(svla_attn_args a, bf16
   constexpr int CPR = D / 8;  // 16-B chunks per output row
   for (int idx = lane; idx < 16 * CPR; idx += 64) {
     const int r = idx / CPR, ch = idx % CPR;
-    const int q = qt * 64 + 16 * w + r;
+    const int q = qt * 64 + 16 * wq + r;
     if (q < L)
       *reinterpret_cast<u32x4*>(out + ((int64_t)b * L + q) * ldo + (int64_t)h * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(img + r * DV + ch * 8);
@@ -290,7 +306,31 @@ __global__ void attn_delta_kernel(int B, int L, int H, int D, const bf16_t* __re
   if (lane == 0) delta[((int64_t)b * H + h) * L + q] = s;
 }
 
+// transpose of rotate_half RoPE on a [rows x 16dt+c] accumulator layout (lo half dt < 8, hi half dt + 8)
+template <int NDT>
+__device__ __forceinline__ void rope_t_acc(f32x4 (&acc)[NDT], const svla_attn_args& a, int row0, int L, int g,
+                                           int c) {
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = row0 + 4 * g + j;
+      if (row < L) {
+        const int d = 16 * dt + c;
+        const float cs = bf2f(((const bf16_t*)a.rope_cos)[(int64_t)row * a.rope_ld + d]);
+        const float sn = bf2f(((const bf16_t*)a.rope_sin)[(int64_t)row * a.rope_ld + d]);
+        float lo = acc[dt][j], hi = acc[dt + 8][j];
+        rope_pair_t(lo, hi, cs, sn);
+        acc[dt][j] = lo;
+        acc[dt + 8][j] = hi;
+      }
+    }
+}
+
 // ================================================================== backward: dK, dV
+// Block = (key tile of 64, kv head, batch), 4 waves x 16 keys.  K/V stay in LDS; the query heads of the group
+// and their 32-row Q / dO tiles stream through two LDS stages by LDS-DMA.  lse / delta of the group's heads
+// and the key classes are preloaded to LDS.
 template <int D, bool ROPE>
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
                                                               int64_t lddo, const float* __restrict__ lse,
@@ -298,114 +338,99 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
                                                               int64_t lddk, bf16_t* __restrict__ dv, int64_t lddv) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
   constexpr int NKS = DP / 32, NDT = DV / 16;
-  constexpr int TB = 64 * RS * 2;
+  constexpr int TB = tile_bytes<D>(64), QB = tile_bytes<D>(32), QSTAGE = 2 * QB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsK = smem;
   char* ldsV = smem + TB;
-  char* ldsQ = smem + 2 * TB;
-  char* ldsO = smem + 3 * TB;
-  float* llse = (float*)(smem + 4 * TB);
-  float* ldel = llse + 64;
-  uint8_t* lcls = (uint8_t*)(ldel + 64);
+  char* qst = smem + 2 * TB;  // 2 stages of {Q [32][RS], dO [32][RS]}
+  const int L = a.L;
+  const int grp = a.Hq / a.Hkv;
+  float* llse = (float*)(qst + 2 * QSTAGE);  // [grp][L]
+  float* ldel = llse + grp * L;
+  uint8_t* lcls = (uint8_t*)(ldel + grp * L);
 
   const int b = blockIdx.z, hk = blockIdx.y, kt = blockIdx.x;
-  const int grp = a.Hq / a.Hkv;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, g = lane >> 4, c = lane & 15;
-  const int L = a.L;
+  const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
-  const uint8_t* cls = a.kv_class ? a.kv_class + (int64_t)b * L : nullptr;
 
-  stage_tile<D, ROPE>(ldsK, kbase, a.ldk, kt * 64, L, a, t);
-  stage_tile<D, false>(ldsV, vbase, a.ldv, kt * 64, L, a, t);
-  if (t < 64) lcls[t] = (cls && kt * 64 + t < L) ? cls[kt * 64 + t] : 0;
+  load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 256);
+  for (int i = t; i < grp * L; i += 256) {
+    const int hh = i / L, q = i % L;
+    const int64_t o = ((int64_t)b * a.Hq + hk * grp + hh) * L + q;
+    llse[i] = lse[o];
+    ldel[i] = delta[o];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int r0 = kt * 64;
+  glds_tile<RS, 64, 4>(ldsK, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
+  glds_tile<RS, 64, 4>(ldsV, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
+
+  const int nqt = (L + 31) / 32, nsteps = grp * nqt;
+  auto issue_q = [&](int step, char* dst) {
+    const int hh = step / nqt, q0 = (step % nqt) * 32;
+    const int h = hk * grp + hh;
+    const bf16_t* qb = (const bf16_t*)a.q + ((int64_t)b * L + q0) * a.ldq + (int64_t)h * D;
+    const bf16_t* ob = dout + ((int64_t)b * L + q0) * lddo + (int64_t)h * D;
+    glds_tile<RS, 32, 4>(dst, qb, a.ldq, L - q0, D, w, lane);
+    glds_tile<RS, 32, 4>(dst + QB, ob, lddo, L - q0, D, w, lane);
+  };
+  issue_q(0, qst);
 
   const int kl = 16 * w + c;  // this lane's key (local)
-  const int kj = kt * 64 + kl;
+  const int kj = r0 + kl;
   f32x4 adk[NDT], adv[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) adk[i] = adv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float LOG2E = 1.4426950408889634f;
-  const int nqt = (L + 63) / 64;
 
-  for (int hh = 0; hh < grp; ++hh) {
-    const int h = hk * grp + hh;
-    const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
-    const bf16_t* obase = dout + (int64_t)b * L * lddo + (int64_t)h * D;
-    for (int qt = 0; qt < nqt; ++qt) {
-      __syncthreads();
-      stage_tile<D, ROPE>(ldsQ, qbase, a.ldq, qt * 64, L, a, t);
-      stage_tile<D, false>(ldsO, obase, lddo, qt * 64, L, a, t);
-      if (t < 64) {
-        const int q = qt * 64 + t;
-        llse[t] = q < L ? lse[((int64_t)b * a.Hq + h) * L + q] : 0.f;
-        ldel[t] = q < L ? delta[((int64_t)b * a.Hq + h) * L + q] : 0.f;
-      }
-      __syncthreads();
-      f32x4 s[4], dp[4];
+  for (int step = 0; step < nsteps; ++step) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const char* ldsQ = qst + (step & 1) * QSTAGE;
+    const char* ldsO = ldsQ + QB;
+    if (step + 1 < nsteps) issue_q(step + 1, qst + ((step + 1) & 1) * QSTAGE);
+    const int hh = step / nqt, q0 = (step % nqt) * 32;
+    const float* sl = llse + hh * L;
+    const float* sd = ldel + hh * L;
+    f32x4 s[2], dp[2];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        s[mt] = dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 2; ++mt) {
+      s[mt] = dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsQ, 16 * mt, ks, lane),
-                                                          frag_row<RS>(ldsK, 16 * w, ks, lane), s[mt], 0, 0, 0);
-          dp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsO, 16 * mt, ks, lane),
-                                                           frag_row<RS>(ldsV, 16 * w, ks, lane), dp[mt], 0, 0, 0);
-        }
-      }
-      // element (mt, j): query ql = 16mt + 4g + j, key = lane col (kl)
-      float pz[4][4], zz[4][4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ql = 16 * mt + 4 * g + j, qi = qt * 64 + ql;
-          float p = 0.f, z = 0.f;
-          if (qi < L && kj < L) {
-            const float sc = softcap_f(s[mt][j] * a.scale, a.softcap);
-            const float xv = visible(a.kv_class ? lcls : nullptr, kl, qi - kt * 64, a.sliding_window) ? sc : MASKVAL;
-            p = exp2f((xv - llse[ql]) * LOG2E);
-            const float ds = p * (dp[mt][j] - ldel[ql]);
-            const float dcap = a.softcap > 0.f ? (1.0f - (sc / a.softcap) * (sc / a.softcap)) : 1.0f;
-            z = ds * dcap * a.scale;
-          }
-          pz[mt][j] = p;
-          zz[mt][j] = z;
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float pv[8] = {pz[2 * ks][0], pz[2 * ks][1], pz[2 * ks][2], pz[2 * ks][3],
-                       pz[2 * ks + 1][0], pz[2 * ks + 1][1], pz[2 * ks + 1][2], pz[2 * ks + 1][3]};
-        float zv[8] = {zz[2 * ks][0], zz[2 * ks][1], zz[2 * ks][2], zz[2 * ks][3],
-                       zz[2 * ks + 1][0], zz[2 * ks + 1][1], zz[2 * ks + 1][2], zz[2 * ks + 1][3]};
-        const bf16x8 pa = pack_frag(pv), za = pack_frag(zv);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          adv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_tr<RS>(ldsO, 32 * ks, 16 * dt, lane), adv[dt], 0, 0, 0);
-          adk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za, frag_tr<RS>(ldsQ, 32 * ks, 16 * dt, lane), adk[dt], 0, 0, 0);
-        }
+      for (int ks = 0; ks < NKS; ++ks) {
+        s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsQ, 16 * mt, ks, lane),
+                                                        frag_row<RS>(ldsK, 16 * w, ks, lane), s[mt], 0, 0, 0);
+        dp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsO, 16 * mt, ks, lane),
+                                                         frag_row<RS>(ldsV, 16 * w, ks, lane), dp[mt], 0, 0, 0);
       }
     }
-  }
-  // accumulators: C[key = 16w + 4g + j][d = 16dt + c]
-  if constexpr (ROPE) {
+    // element (mt, j): query q0 + 16mt + 4g + j, key = lane col (kl)
+    float pv[8], zv[8];
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int key = kt * 64 + 16 * w + 4 * g + j;
-        if (key < L) {
-          const int d = 16 * dt + c;
-          const float cs = bf2f(((const bf16_t*)a.rope_cos)[(int64_t)key * a.rope_ld + d]);
-          const float sn = bf2f(((const bf16_t*)a.rope_sin)[(int64_t)key * a.rope_ld + d]);
-          float lo = adk[dt][j], hi = adk[dt + 8][j];
-          rope_pair_t(lo, hi, cs, sn);
-          adk[dt][j] = lo;
-          adk[dt + 8][j] = hi;
+        const int qi = q0 + 16 * mt + 4 * g + j;
+        float p = 0.f, z = 0.f;
+        if (qi < L && kj < L) {
+          const float sc = softcap_f(s[mt][j] * a.scale, a.softcap);
+          const float xv = visible(lcls[kj], kj, qi, a.sliding_window) ? sc : MASKVAL;
+          p = exp2f((xv - sl[qi]) * LOG2E);
+          const float ds = p * (dp[mt][j] - sd[qi]);
+          const float dcap = a.softcap > 0.f ? (1.0f - (sc / a.softcap) * (sc / a.softcap)) : 1.0f;
+          z = ds * dcap * a.scale;
         }
+        pv[4 * mt + j] = p;
+        zv[4 * mt + j] = z;
       }
+    const bf16x8 pa = pack_frag(pv), za = pack_frag(zv);
+    mfma_tr_sweep<RS, NDT, false>(adv, ldsO, 0, pa, lane);
+    mfma_tr_sweep<RS, NDT, false>(adk, ldsQ, 0, za, lane);
   }
+  // accumulators: C[key = 16w + 4g + j][d = 16dt + c]
+  if constexpr (ROPE) rope_t_acc<NDT>(adk, a, r0 + 16 * w, L, g, c);
   __syncthreads();
   // stage both results as bf16 [64][DV] images, then 16-B row stores
   bf16_t* imgK = (bf16_t*)smem;
@@ -422,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
   constexpr int CPR = D / 8;
   for (int idx = t; idx < 64 * CPR; idx += 256) {
     const int r = idx / CPR, ch = idx % CPR;
-    const int key = kt * 64 + r;
+    const int key = r0 + r;
     if (key < L) {
       *reinterpret_cast<u32x4*>(dk + ((int64_t)b * L + key) * lddk + (int64_t)hk * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(imgK + r * DV + ch * 8);
@@ -433,48 +458,58 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
 }
 
 // ================================================================== backward: dQ
-template <int D, bool ROPE>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
-                                                             int64_t lddo, const float* __restrict__ lse,
-                                                             const float* __restrict__ delta, bf16_t* __restrict__ dq,
-                                                             int64_t lddq) {
+// Block = (query tile of 64, NH query heads sharing one kv head, batch), like the forward: K/V tiles stream
+// through two LDS stages by LDS-DMA.
+template <int D, int NH, bool ROPE>
+__global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
+                                                                  int64_t lddo, const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  bf16_t* __restrict__ dq, int64_t lddq) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
-  constexpr int NKS = DP / 32, NDT = DV / 16;
-  constexpr int TB = 64 * RS * 2;
+  constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH;
+  constexpr int TB = tile_bytes<D>(64), STAGE = 2 * TB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsK = smem;
-  char* ldsV = smem + TB;
-  uint8_t* lcls = (uint8_t*)(smem + 2 * TB);
+  uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
 
-  const int b = blockIdx.z, h = blockIdx.y, qt = blockIdx.x;
+  const int b = blockIdx.z, qt = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int h = blockIdx.y * NH + (w >> 2), wq = w & 3;
   const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int L = a.L;
-  const int qi = qt * 64 + 16 * w + c;
+  const int qi = qt * 64 + 16 * wq + c;
   const bool qvalid = qi < L;
   const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
   const bf16_t* obase = dout + (int64_t)b * L * lddo + (int64_t)h * D;
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
-  const uint8_t* cls = a.kv_class ? a.kv_class + (int64_t)b * L : nullptr;
 
+  load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 64 * NW);
   bf16x8 qf[NKS], of[NKS];
-  load_row_frags<D, ROPE>(qf, qbase + (int64_t)qi * a.ldq, qvalid, a, qi, lane);
-  load_row_frags<D, false>(of, obase + (int64_t)qi * lddo, qvalid, a, qi, lane);
+  load_row_frags<D>(qf, qbase + (int64_t)qi * a.ldq, qvalid, lane);
+  load_row_frags<D>(of, obase + (int64_t)qi * lddo, qvalid, lane);
   const float lq = qvalid ? lse[((int64_t)b * a.Hq + h) * L + qi] : 0.f;
   const float dq_ = qvalid ? delta[((int64_t)b * a.Hq + h) * L + qi] : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nkt = (L + 63) / 64;
+  glds_tile<RS, 64, NW>(smem, kbase, a.ldk, L, D, w, lane);
+  glds_tile<RS, 64, NW>(smem + TB, vbase, a.ldv, L, D, w, lane);
 
   f32x4 acc[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float LOG2E = 1.4426950408889634f;
-  const int nkt = (L + 63) / 64;
   for (int kt = 0; kt < nkt; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    stage_tile<D, ROPE>(ldsK, kbase, a.ldk, kt * 64, L, a, t);
-    stage_tile<D, false>(ldsV, vbase, a.ldv, kt * 64, L, a, t);
-    if (t < 64) lcls[t] = (cls && kt * 64 + t < L) ? cls[kt * 64 + t] : 0;
-    __syncthreads();
+    const char* ldsK = smem + (kt & 1) * STAGE;
+    const char* ldsV = ldsK + TB;
+    if (kt + 1 < nkt) {
+      char* nx = smem + ((kt + 1) & 1) * STAGE;
+      const int r0 = (kt + 1) * 64;
+      glds_tile<RS, 64, NW>(nx, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
+      glds_tile<RS, 64, NW>(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
+    }
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -490,11 +525,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(svla_attn_args a, c
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int kl = 16 * nt + 4 * g + j, kj = kt * 64 + kl;
+        const int kj = kt * 64 + 16 * nt + 4 * g + j;
         float z = 0.f;
         if (qvalid && kj < L) {
           const float sc = softcap_f(s[nt][j] * a.scale, a.softcap);
-          const float xv = visible(a.kv_class ? lcls : nullptr, kl, qi - kt * 64, a.sliding_window) ? sc : MASKVAL;
+          const float xv = visible(lcls[kj], kj, qi, a.sliding_window) ? sc : MASKVAL;
           const float p = exp2f((xv - lq) * LOG2E);
           const float ds = p * (dp[nt][j] - dq_);
           const float dcap = a.softcap > 0.f ? (1.0f - (sc / a.softcap) * (sc / a.softcap)) : 1.0f;
@@ -507,29 +542,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(svla_attn_args a, c
       float zv[8] = {zz[2 * ks][0], zz[2 * ks][1], zz[2 * ks][2], zz[2 * ks][3],
                      zz[2 * ks + 1][0], zz[2 * ks + 1][1], zz[2 * ks + 1][2], zz[2 * ks + 1][3]};
       const bf16x8 za = pack_frag(zv);
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za, frag_tr<RS>(ldsK, 32 * ks, 16 * dt, lane), acc[dt], 0, 0, 0);
+      mfma_tr_sweep<RS, NDT, false>(acc, ldsK, 32 * ks, za, lane);
     }
   }
-  // acc: C[q = 16w + 4g + j][d = 16dt + c]
-  if constexpr (ROPE) {
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = qt * 64 + 16 * w + 4 * g + j;
-        if (q < L) {
-          const int d = 16 * dt + c;
-          const float cs = bf2f(((const bf16_t*)a.rope_cos)[(int64_t)q * a.rope_ld + d]);
-          const float sn = bf2f(((const bf16_t*)a.rope_sin)[(int64_t)q * a.rope_ld + d]);
-          float lo = acc[dt][j], hi = acc[dt + 8][j];
-          rope_pair_t(lo, hi, cs, sn);
-          acc[dt][j] = lo;
-          acc[dt + 8][j] = hi;
-        }
-      }
-  }
+  // acc: C[q = 16wq + 4g + j][d = 16dt + c]
+  if constexpr (ROPE) rope_t_acc<NDT>(acc, a, qt * 64 + 16 * wq, L, g, c);
   __syncthreads();
   bf16_t* img = (bf16_t*)smem + w * 16 * DV;
 #pragma unroll
@@ -540,7 +557,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(svla_attn_args a, c
   constexpr int CPR = D / 8;
   for (int idx = lane; idx < 16 * CPR; idx += 64) {
     const int r = idx / CPR, ch = idx % CPR;
-    const int q = qt * 64 + 16 * w + r;
+    const int q = qt * 64 + 16 * wq + r;
     if (q < L)
       *reinterpret_cast<u32x4*>(dq + ((int64_t)b * L + q) * lddq + (int64_t)h * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(img + r * DV + ch * 8);
@@ -556,48 +573,65 @@ void set_lds_once(int bytes) {
   }
 }
 
-int check_args(const svla_attn_args* a, bool rope) {
+int check_args(const svla_attn_args* a) {
   SVLA_CHECK_ARG(a, "attn: args NULL");
-  SVLA_CHECK_ARG(a->B > 0 && a->L > 0 && a->Hq > 0 && a->Hkv > 0 && a->Hq % a->Hkv == 0, "attn: bad B/L/H");
+  SVLA_CHECK_ARG(a->B > 0 && a->L > 0 && a->L <= 8192 && a->Hq > 0 && a->Hkv > 0 && a->Hq % a->Hkv == 0,
+                 "attn: bad B/L/H (L <= 8192)");
   SVLA_CHECK_ARG(a->D == 256 || a->D == 72, "attn: head_dim %d unsupported (256 or 72)", a->D);
   SVLA_CHECK_ARG(a->q && a->k && a->v, "attn: q/k/v NULL");
   SVLA_CHECK_ARG(a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0, "attn: ld must be multiples of 8");
   SVLA_CHECK_ARG(((uintptr_t)a->q & 15) == 0 && ((uintptr_t)a->k & 15) == 0 && ((uintptr_t)a->v & 15) == 0,
                  "attn: q/k/v must be 16-B aligned");
-  if (rope) SVLA_CHECK_ARG(a->D == 256 && a->rope_sin && a->rope_ld % 8 == 0, "attn: RoPE needs D=256, sin, ld%8");
   return 0;
+}
+
+int round16(int x) { return (x + 15) & ~15; }
+
+template <int D, int NH>
+int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
+  const int lds = 4 * tile_bytes<D>(64) + round16(a.L);
+  dim3 grid((a.L + 63) / 64, a.Hq / NH, a.B), block(256 * NH);
+  set_lds_once<attn_fwd_kernel<D, NH>>(lds);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NH>), grid, block, lds, s, a, out, ldo, lse);
+  return svla::check_launch("attn_fwd");
+}
+
+template <int D, int NH, bool ROPE>
+int bwd_launch(const svla_attn_args& a, const bf16_t* dout, int64_t lddo, const float* lse, const float* delta,
+               bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv, int64_t lddv, hipStream_t s) {
+  const int grp = a.Hq / a.Hkv;
+  const int lds_kv = 2 * tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + round16(8 * grp * a.L) + round16(a.L);
+  SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
+  const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
+  const int nt = (a.L + 63) / 64;
+  set_lds_once<attn_bwd_dkv_kernel<D, ROPE>>(lds_kv);
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE>), dim3(nt, a.Hkv, a.B), dim3(256), lds_kv, s, a, dout, lddo, lse,
+                     delta, dk, lddk, dv, lddv);
+  set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE>>(lds_q);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE>), dim3(nt, a.Hq / NH, a.B), dim3(256 * NH), lds_q, s, a, dout,
+                     lddo, lse, delta, dq, lddq);
+  return svla::check_launch("attn_bwd");
 }
 
 }  // namespace
 
 extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, float* lse, void* stream) {
-  const bool rope = a && a->rope_cos;
-  if (int rc = check_args(a, rope)) return rc;
+  if (int rc = check_args(a)) return rc;
   SVLA_CHECK_ARG(out && lse && ldo % 8 == 0, "attn_fwd: out/lse");
-  dim3 grid((a->L + 63) / 64, a->Hq, a->B), block(256);
+  SVLA_CHECK_ARG(!a->rope_cos && !a->rope_sin, "attn_fwd: q/k must arrive rotated (RoPE is a GEMM epilogue)");
   hipStream_t s = (hipStream_t)stream;
-  if (a->D == 256) {
-    const int lds = 2 * 64 * 256 * 2 + 64;
-    if (rope) {
-      set_lds_once<attn_fwd_kernel<256, true>>(lds);
-      hipLaunchKernelGGL((attn_fwd_kernel<256, true>), grid, block, lds, s, *a, (bf16_t*)out, ldo, lse);
-    } else {
-      set_lds_once<attn_fwd_kernel<256, false>>(lds);
-      hipLaunchKernelGGL((attn_fwd_kernel<256, false>), grid, block, lds, s, *a, (bf16_t*)out, ldo, lse);
-    }
-  } else {
-    const int lds = 2 * 64 * 128 * 2 + 64;
-    set_lds_once<attn_fwd_kernel<72, false>>(lds);
-    hipLaunchKernelGGL((attn_fwd_kernel<72, false>), grid, block, lds, s, *a, (bf16_t*)out, ldo, lse);
-  }
-  return svla::check_launch("attn_fwd");
+  const bool pair = (a->Hq / a->Hkv) % 2 == 0;  // two query heads of a GQA group share the K/V stream
+  if (a->D == 256) return pair ? fwd_launch<256, 2>(*a, (bf16_t*)out, ldo, lse, s)
+                               : fwd_launch<256, 1>(*a, (bf16_t*)out, ldo, lse, s);
+  return fwd_launch<72, 1>(*a, (bf16_t*)out, ldo, lse, s);
 }
 
 extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                              const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
                              float* workspace, void* stream) {
-  const bool rope = a && a->rope_cos;
-  if (int rc = check_args(a, rope)) return rc;
+  if (int rc = check_args(a)) return rc;
+  const bool rope = a->rope_cos != nullptr;
+  if (rope) SVLA_CHECK_ARG(a->D == 256 && a->rope_sin && a->rope_ld % 8 == 0, "attn_bwd: RoPE needs D=256, sin, ld%8");
   SVLA_CHECK_ARG(out && dout && lse && dq && dk && dv && workspace, "attn_bwd: NULL buffer");
   SVLA_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 8 == 0 && lddk % 8 == 0 && lddv % 8 == 0,
                  "attn_bwd: ld must be multiples of 8");
@@ -606,35 +640,19 @@ extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t l
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a->B, a->L, a->Hq, a->D,
                      (const bf16_t*)out, ldo, (const bf16_t*)dout, lddo, workspace);
   if (int rc = svla::check_launch("attn_delta")) return rc;
-  const int nt = (a->L + 63) / 64;
-  dim3 gkv(nt, a->Hkv, a->B), gq(nt, a->Hq, a->B), block(256);
+  const bool pair = (a->Hq / a->Hkv) % 2 == 0;
+  const bf16_t* d_o = (const bf16_t*)dout;
   if (a->D == 256) {
-    const int lds_kv = 4 * 64 * 256 * 2 + 64 * 8 + 64;
-    const int lds_q = 2 * 64 * 256 * 2 + 64;
-    if (rope) {
-      set_lds_once<attn_bwd_dkv_kernel<256, true>>(lds_kv);
-      set_lds_once<attn_bwd_dq_kernel<256, true>>(lds_q);
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<256, true>), gkv, block, lds_kv, s, *a, (const bf16_t*)dout, lddo, lse,
-                         workspace, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<256, true>), gq, block, lds_q, s, *a, (const bf16_t*)dout, lddo, lse,
-                         workspace, (bf16_t*)dq, lddq);
-    } else {
-      set_lds_once<attn_bwd_dkv_kernel<256, false>>(lds_kv);
-      set_lds_once<attn_bwd_dq_kernel<256, false>>(lds_q);
-      hipLaunchKernelGGL((attn_bwd_dkv_kernel<256, false>), gkv, block, lds_kv, s, *a, (const bf16_t*)dout, lddo, lse,
-                         workspace, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<256, false>), gq, block, lds_q, s, *a, (const bf16_t*)dout, lddo, lse,
-                         workspace, (bf16_t*)dq, lddq);
-    }
-  } else {
-    const int lds_kv = 4 * 64 * 128 * 2 + 64 * 8 + 64;
-    const int lds_q = 2 * 64 * 128 * 2 + 64;
-    set_lds_once<attn_bwd_dkv_kernel<72, false>>(lds_kv);
-    set_lds_once<attn_bwd_dq_kernel<72, false>>(lds_q);
-    hipLaunchKernelGGL((attn_bwd_dkv_kernel<72, false>), gkv, block, lds_kv, s, *a, (const bf16_t*)dout, lddo, lse,
-                       workspace, (bf16_t*)dk, lddk, (bf16_t*)dv, lddv);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<72, false>), gq, block, lds_q, s, *a, (const bf16_t*)dout, lddo, lse,
-                       workspace, (bf16_t*)dq, lddq);
+    if (pair)
+      return rope ? bwd_launch<256, 2, true>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
+                                             (bf16_t*)dv, lddv, s)
+                  : bwd_launch<256, 2, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
+                                              (bf16_t*)dv, lddv, s);
+    return rope ? bwd_launch<256, 1, true>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
+                                           (bf16_t*)dv, lddv, s)
+                : bwd_launch<256, 1, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
+                                            (bf16_t*)dv, lddv, s);
   }
-  return svla::check_launch("attn_bwd");
+  return bwd_launch<72, 1, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk, (bf16_t*)dv,
+                                  lddv, s);
 }

@@ -49,15 +49,6 @@ using CfgSmall = Cfg<128, 128, 2, 2>;
 // RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
-  // T20: make the descriptor provably wave-uniform (else hipcc wraps every load in a waterfall loop)
-  const uint64_t a = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  void* pb = (void*)(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)OOB, 0x00020000);
-}
-
 // segment pointer for outer tile start / k-tile start (scalar selects, no dynamic indexing)
 __device__ __forceinline__ const bf16_t* seg_ptr(const svla_operand& op, int64_t idx, int64_t& base_idx) {
   const bf16_t* p = (const bf16_t*)op.ptr[0];
@@ -349,6 +340,29 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           continue;
         }
         if (m >= M || nv <= 0) continue;
+        if (kind == SVLA_EPI_ROPE) {
+          // q/k columns: rotate with the partner chunk D/2 away inside the same head (same tile); reference
+          // rounding: x = bf16(acc); out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin))
+          if (n < E.rope_cols) {
+            const int hd = E.rope_D, half = hd >> 1;
+            const int d = (int)(n % hd);
+            const bool lo = d < half;
+            const float* pp = Ei + rr * EPI_LD + 8 * cc + (lo ? half : -half);
+            const int64_t pos = m % E.rope_L;
+            float cs[8], sn[8];
+            const int dd = lo ? d : d - half;
+            unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.rope_cos + pos * E.rope_ld + dd), cs);
+            unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.rope_sin + pos * E.rope_ld + dd), sn);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float x = round_bf(v[j]), y = round_bf(pp[j]);
+              const float rot = lo ? -y : y;
+              v[j] = round_bf(x * cs[j]) + round_bf(rot * sn[j]);
+            }
+          }
+          store8(cbase + (m - cm0) * Cd.ld + n, v, nv);
+          continue;
+        }
         epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
       }
     }
@@ -1065,6 +1079,13 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
       break;
     case SVLA_EPI_GELU_BWD: SVLA_CHECK_ARG(epi->in0, "gemm: GELU_BWD needs in0"); break;
     case SVLA_EPI_SOFTCAP_CE: SVLA_CHECK_ARG(epi->row_stats && epi->cap > 0.f, "gemm: SOFTCAP_CE needs row_stats, cap"); break;
+    case SVLA_EPI_ROPE:
+      SVLA_CHECK_ARG(epi->rope_cos && epi->rope_sin && epi->rope_L > 0 && epi->rope_D >= 16 &&
+                         epi->rope_D % 16 == 0 && epi->rope_D <= 256 && (256 % epi->rope_D) == 0 &&
+                         epi->rope_ld % 8 == 0 && epi->rope_cols % epi->rope_D == 0 && epi->rope_cols <= N,
+                     "gemm: ROPE needs cos/sin tables, rope_L, rope_D in {16,32,64,128,256}, rope_cols a multiple of D");
+      SVLA_CHECK_ARG(c_nseg == 1, "gemm: ROPE writes one C matrix");
+      break;
     default: SVLA_CHECK_ARG(false, "gemm: unknown epilogue %d", epi->kind);
   }
   if (epi->accumulate) SVLA_CHECK_ARG(epi->kind == SVLA_EPI_STORE, "gemm: accumulate only with EPI_STORE");
@@ -1085,6 +1106,11 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
   const int64_t nk = (K + BK - 1) / BK;
   const bool sk_ok = g_variant == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
+    SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
+    if (g_variant != 1 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
+    return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
+  }
   if (g_variant != 1 && !kseg && seg_ok(256, 256) &&
       (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
     return launch8(M, N, K, *A, *B, C, *epi, s);

@@ -108,3 +108,15 @@ __device__ __forceinline__ int xcd_remap(int pid, int nwg) {
   int xcd = pid % nx, idx = pid / nx;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
+
+// wave-uniform buffer descriptor over [base, base + 2 GiB): loads beyond num_records return zeros (the OOB
+// voffset 0x80000000 is how the kernels zero-fill ragged tile edges).  readfirstlane makes the base provably
+// uniform, else hipcc wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20).
+constexpr uint32_t SVLA_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pb = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)SVLA_OOB, 0x00020000);
+}

@@ -208,7 +208,9 @@ class GemmaAttnCfg:
 class GemmaAttentionFn(torch.autograd.Function):
     """Gemma2Attention.forward (modeling_gemma2.py:364-413): q/k/v projections, rotary embedding
     (:95-154), eager prefix-LM GQA attention with logit softcap (:169-195), o_proj — as one fused
-    QKV GEMM, one attention kernel with RoPE applied on load, one O GEMM."""
+    QKV GEMM whose epilogue applies RoPE to q/k (bf16 rounding of the reference), one attention kernel,
+    one O GEMM.  The saved qkv holds the rotated q/k; the attention backward returns dq/dk w.r.t. the
+    pre-rotation q/k (RoPE transpose), which is what the projection backward needs."""
 
     @staticmethod
     def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg):
@@ -216,12 +218,11 @@ class GemmaAttentionFn(torch.autograd.Function):
         M, H = x.shape
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
-        K.linear_fwd(x, [wq, wk, wv], qkv)
+        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, cfg.L, cfg.D, qd + kd))
         attn = _empty(M, qd, like=x)
         lse = _empty(cfg.B, cfg.Hq, cfg.L, dtype=F32, like=x)
         a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
-                        qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window,
-                        cos, sin)
+                        qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window)
         K.attn_fwd(a, attn, lse)
         out = _empty(M, wo.shape[0], like=x)
         K.linear_fwd(attn, [wo], out)

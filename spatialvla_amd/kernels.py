@@ -59,7 +59,7 @@ def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUT
 
 
 def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=None, in1=None, out1=None,
-         out2=None, row_stats=None) -> L.Epilogue:
+         out2=None, row_stats=None, rope=None) -> L.Epilogue:
     e = L.Epilogue()
     e.kind = kind
     e.accumulate = 1 if accumulate else 0
@@ -75,6 +75,11 @@ def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=
     if out2 is not None:
         e.out2, e.ld_out2 = out2.data_ptr(), _ld(out2)
     e.row_stats = _ptr(row_stats)
+    if rope is not None:  # (cos [L, D/2] bf16, sin, L, D, rotated columns)
+        cos, sin, Lr, D, cols = rope
+        _req(cos.stride(1) == 1 and sin.stride() == cos.stride(), "rope tables must share a row-major layout")
+        e.rope_cos, e.rope_sin, e.rope_ld = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
+        e.rope_L, e.rope_D, e.rope_cols = int(Lr), int(D), int(cols)
     return e
 
 
@@ -134,7 +139,7 @@ def _aligned(sizes, mult):
 
 
 def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, kind=L.EPI_STORE, bias=None,
-               alpha=1.0, in0=None, out1=None, out2=None, row_stats=None, cap=0.0):
+               alpha=1.0, in0=None, out1=None, out2=None, row_stats=None, cap=0.0, rope=None):
     """out[M, sum N_i] = epi(x[M,K] @ cat(weights)^T).  Weights [N_i, K] are read in place."""
     M, K = x.shape
     sizes = [w.shape[0] for w in weights]
@@ -149,7 +154,7 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
     A = _operand([x], L.LAYOUT_KC)
     B = _operand(weights, L.LAYOUT_KC, L.SEG_OUTER, starts)
     gemm(M, N, K, A, B, [out], [0], _ld(out),
-         _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap))
+         _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap, rope=rope))
 
 
 # Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch

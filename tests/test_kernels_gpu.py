@@ -348,6 +348,8 @@ def _ref_attn(q, k, v, scale, cap, kv_class, window, cos=None, sin=None):
 
 
 @pytest.mark.parametrize("D,Hq,Hkv,L,rope,cap", [(256, 2, 1, 140, True, 50.0), (256, 8, 4, 312, True, 50.0),
+                                                 (256, 4, 1, 200, True, 50.0), (256, 3, 3, 100, True, 50.0),
+                                                 (256, 2, 2, 65, False, 0.0),
                                                  (72, 2, 2, 256, False, 0.0), (72, 3, 3, 70, False, 0.0)])
 def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
     from spatialvla_amd import kernels as Kn
@@ -367,11 +369,20 @@ def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
             inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
             f = (torch.arange(L, device=cuda).float() + 1)[:, None] * inv[None]
             cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
-    a = Kn.attn_args(B, L, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap, kv_class, 0,
-                     cos, sin)
+    # q/k reach the kernels rotated (RoPE is the QKV GEMM's epilogue); the backward returns dq/dk w.r.t. the
+    # pre-rotation q/k when given the tables
+    qkv_in = qkv.clone()
+    if cos is not None:
+        nrot = (Hq + Hkv) * D
+        qkv_in[:, :nrot] = _rope_bf16(qkv[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
+    qi_, ki_, vi_ = qkv_in[:, :Hq * D], qkv_in[:, Hq * D:(Hq + Hkv) * D], qkv_in[:, (Hq + Hkv) * D:]
+    a = Kn.attn_args(B, L, Hq, Hkv, D, qi_, qkv.stride(0), ki_, qkv.stride(0), vi_, qkv.stride(0), scale, cap,
+                     kv_class, 0)
     out = torch.empty(B * L, Hq * D, dtype=BF, device=cuda)
     lse = torch.empty(B, Hq, L, device=cuda)
     Kn.attn_fwd(a, out, lse)
+    a = Kn.attn_args(B, L, Hq, Hkv, D, qi_, qkv.stride(0), ki_, qkv.stride(0), vi_, qkv.stride(0), scale, cap,
+                     kv_class, 0, cos, sin)
     qr = q.view(B, L, Hq, D).float().requires_grad_(True)
     kr = k.view(B, L, Hkv, D).float().requires_grad_(True)
     vr = v.view(B, L, Hkv, D).float().requires_grad_(True)
@@ -385,6 +396,37 @@ def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
     assert rel_l2(dqkv[:, :Hq * D].view(B, L, Hq, D), qr.grad) < 2e-2
     assert rel_l2(dqkv[:, Hq * D:(Hq + Hkv) * D].view(B, L, Hkv, D), kr.grad) < 2e-2
     assert rel_l2(dqkv[:, (Hq + Hkv) * D:].view(B, L, Hkv, D), vr.grad) < 2e-2
+
+
+def _rope_bf16(x, cos, sin):
+    """Gemma2 apply_rotary_pos_emb in bf16 (modeling_gemma2.py:123-154): x [B, L, H, D] bf16, tables [L, D/2]."""
+    c = torch.cat([cos, cos], -1)[None, :, None, :]
+    s_ = torch.cat([sin, sin], -1)[None, :, None, :]
+    h = x.shape[-1] // 2
+    rot = torch.cat([-x[..., h:], x[..., :h]], -1)
+    return (x * c) + (rot * s_)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,L", [(256, 8, 4, 312), (16, 4, 1, 40)])
+def test_gemm_rope_epilogue(cuda, D, Hq, Hkv, L):
+    """SVLA_EPI_ROPE rotates q/k columns exactly as the reference's bf16 eager RoPE on the GEMM's own bf16
+    output (bitwise), and leaves v columns alone."""
+    from spatialvla_amd import kernels as Kn, _lib as L_
+    torch.manual_seed(11)
+    B, K = 3, 320
+    N = (Hq + 2 * Hkv) * D
+    x, w = _r(B * L, K), _r(N, K, scale=0.1)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    f = (torch.arange(L, device=cuda).float() + 1)[:, None] * inv[None]
+    cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
+    plain = torch.empty(B * L, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], plain)
+    rot = torch.empty_like(plain)
+    nrot = (Hq + Hkv) * D
+    Kn.linear_fwd(x, [w], rot, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
+    ref = plain.clone()
+    ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
+    assert torch.equal(rot, ref)
 
 
 def test_gemma2_attention_plugin_signature(cuda):
