@@ -20,6 +20,7 @@ from transformers import PreTrainedModel
 from transformers.utils import ModelOutput
 
 from . import functional as Fn
+from . import zoe_fast
 from . import kernels as K
 from .configuration_spatialvla import SpatialVLAConfig
 from .modeling_gemma2 import Gemma2ForCausalLM, KVMask
@@ -119,6 +120,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         if config.use_vision_zoe:
             from transformers import ZoeDepthForDepthEstimation  # frozen 3p depth estimator (stock torch ops)
             self.vision_zoe_model = vision_zoe_model or ZoeDepthForDepthEstimation(config.vision_zoe_config)
+            zoe_fast.install(self.vision_zoe_model)
             self.position_embedding_3d = Ego3DPositionEmbeddingMLP(
                 config.ego3d_patch_reso ** 2 * 3, num_pos_feats=config.vision_config.hidden_size,
                 n_freqs=config.n_freqs)

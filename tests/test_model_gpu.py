@@ -55,6 +55,24 @@ def test_tiny_depth_estimator(cuda):
     assert H.rel_l2(d, g["out.depth"].float()) < 2e-2
 
 
+def test_zoe_fast_paths_bitwise(cuda):
+    """zoe_fast.install (cached BEiT relative-position bias, NCHW concat in the log-binomial head) leaves the
+    frozen estimator's output bitwise unchanged, on repeated calls too (the cache path)."""
+    from transformers import ZoeDepthForDepthEstimation
+    from spatialvla_amd import zoe_fast
+    cfg = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0").config.vision_zoe_config
+    torch.manual_seed(3)
+    ref = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
+    fast = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
+    fast.load_state_dict(ref.state_dict())
+    zoe_fast.install(fast)
+    x = torch.randn(2, 3, 384, 384, device=cuda).to(torch.bfloat16)
+    with torch.no_grad():
+        d0 = ref(pixel_values=x).predicted_depth
+        for _ in range(2):
+            assert torch.equal(fast(pixel_values=x).predicted_depth, d0)
+
+
 def test_tiny_prefill_vs_reference_golden(cuda):
     g = _load("tiny_train.safetensors")
     gp = _load("tiny_prefill.safetensors")
