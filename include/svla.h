@@ -234,6 +234,21 @@ int svla_adamw(int64_t n, float* master, void* param_bf16, const void* grad_bf16
 /* clip_scale[0] = min(1, max_norm / (sqrt(sumsq[0]) + 1e-6)); norm_out[0] = sqrt(sumsq[0]). */
 int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float* norm_out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * ZoeDepth metric head tail, fused (frozen depth estimator; reference model/modeling_spatialvla.py:314-323
+ * calls transformers ZoeDepthMetricDepthEstimationHead.forward [3p], whose tail after the last attractor is
+ * replaced): cat(outconv activation, relative depth) + bilinear(align_corners) bin embedding -> 1x1 conv
+ * (+bias) -> GELU(erf) -> 1x1 conv (+bias) -> softplus -> probability / temperature -> log-binomial
+ * softmax over NBins -> expectation over bilinear(align_corners) bin centres.  Inputs bf16 with arbitrary
+ * element strides (b, c, y, x) / (b, y, x) (channel stride 1 = channels-last, 16-B aligned).  params fp32:
+ * W1^T [CF+1+CE][Hid], W2 [4][Hid], b1 [Hid], b2 [4], log_binom(NBins-1, k) [NBins] (as the reference computes
+ * it).  out [B, H, W] fp32.  Built for NBins = 64, Hid = 80, CF and CE multiples of 8. */
+int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
+                         const void* feat, const int64_t* feat_strides, const void* rel, const int64_t* rel_strides,
+                         const void* emb, const int64_t* emb_strides, const void* ctr, const int64_t* ctr_strides,
+                         const float* params, float p_eps, float max_t, float min_t, float clamp_eps, float* out,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

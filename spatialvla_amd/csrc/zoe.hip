@@ -1,0 +1,234 @@
+// ZoeDepth metric head tail, fused (frozen depth estimator, reference model/modeling_spatialvla.py:314-323 ->
+// transformers ZoeDepthMetricDepthEstimationHead.forward [3p]).  Per output pixel (b, i, j):
+//
+//   last   = cat(outconv_activation[b, :, i, j] (C_F channels), relative_depth[b, i, j])
+//   cond   = bilinear_align_corners(bin_embedding_lowres)[b, :, i, j]            (C_E channels)
+//   h      = GELU(conv1x1_W1(cat(last, cond)) + b1)                               (HID = (C_F+1+C_E)/2)
+//   s      = softplus(conv1x1_W2(h) + b2)                                          (4 channels)
+//   p      = (s0+eps)/((s0+eps)+(s1+eps)),  t = (max_t-min_t)*(s2+eps)/((s2+eps)+(s3+eps)) + min_t
+//   y_k    = logbinom(NB-1, k) + k*log(clamp(p)) + (NB-1-k)*log(clamp(1-p)),   x = softmax_k(y / t)
+//   depth  = sum_k x_k * bilinear_align_corners(bin_centers_lowres)[b, k, i, j]
+//
+// The stock path materialises [B,161,H,W] bf16, [B,64,H,W] fp32 probabilities and two upsampled
+// copies (several GB at B=32, 384x384); here every intermediate stays in registers.  Every bf16 rounding
+// point of the eager reference (interpolation outputs, conv outputs, GELU, softplus, the elementwise bf16
+// ops on p and t, k*log(p)) is reproduced; accumulation orders of the 1x1 convs and the final sum are
+// fp32 but not bit-identical to MIOpen / torch.sum.
+#include "svla_common.h"
+
+namespace {
+
+struct ZoeTailArgs {
+  int B, H, W, h, w;            // output and low-resolution sizes
+  int CF;                       // outconv_activation channels (main feature without the relative depth)
+  int CE;                       // bin-embedding channels
+  const bf16_t* feat; int64_t fs[4];   // [B, CF, H, W] element strides (b, c, y, x)
+  const bf16_t* rel;  int64_t rs[3];   // [B, H, W]
+  const bf16_t* emb;  int64_t es[4];   // [B, CE, h, w]
+  const bf16_t* ctr;  int64_t cs[4];   // [B, NB, h, w]
+  float p_eps, max_t, min_t, clamp_eps;
+  float* out;                   // [B, H, W] fp32
+};
+
+constexpr int HID = 80, NB = 64, CIN_MAX = 192;
+
+// branch-free erfc (Numerical Recipes erfcc, Chebyshev fit; fractional error < 1.2e-7 everywhere): libm's erff
+// branches per argument range, which diverges across a wave and dominated this kernel.  The GELU output is
+// rounded to bf16, far coarser than the fit error.
+__device__ __forceinline__ float erfc_pos(float z) {  // z >= 0
+  const float t = 1.0f / (1.0f + 0.5f * z);
+  const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
+                  t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
+  return t * __expf(-z * z + p);
+}
+// nn.GELU() (erf form): 0.5*x*(1+erf(x/sqrt2)); 1+erf(u) = erfc(-u) keeps negative arguments exact
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float u = x * 0.70710678118654752f;
+  const float one_plus_erf = u >= 0.f ? 2.0f - erfc_pos(u) : erfc_pos(-u);
+  return 0.5f * x * one_plus_erf;
+}
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
+
+// align_corners=True bilinear source coordinate (ATen area_pixel_compute_source_index, fp32)
+struct Tap {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ Tap tap(int dst, int in, int out) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float src = scale * (float)dst;
+  Tap t;
+  t.i0 = (int)src;
+  t.i1 = t.i0 + ((t.i0 < in - 1) ? 1 : 0);
+  t.l1 = src - (float)t.i0;
+  t.l0 = 1.f - t.l1;
+  return t;
+}
+struct Taps2 {  // the four source offsets (elements) and weights of one output pixel
+  int64_t o00, o01, o10, o11;
+  float ly0, ly1, lx0, lx1;
+};
+__device__ __forceinline__ Taps2 taps2(const int64_t* s, const Tap& ty, const Tap& tx) {
+  Taps2 t;
+  t.o00 = ty.i0 * s[2] + tx.i0 * s[3];
+  t.o01 = ty.i0 * s[2] + tx.i1 * s[3];
+  t.o10 = ty.i1 * s[2] + tx.i0 * s[3];
+  t.o11 = ty.i1 * s[2] + tx.i1 * s[3];
+  t.ly0 = ty.l0; t.ly1 = ty.l1; t.lx0 = tx.l0; t.lx1 = tx.l1;
+  return t;
+}
+// ATen upsample_bilinear2d (align_corners) value in fp32, rounded to the bf16 output
+__device__ __forceinline__ float bilerp(const bf16_t* p, const Taps2& t) {
+  const float a = bf2f(p[t.o00]), b = bf2f(p[t.o01]), c = bf2f(p[t.o10]), d = bf2f(p[t.o11]);
+  return round_bf(t.ly0 * (t.lx0 * a + t.lx1 * b) + t.ly1 * (t.lx0 * c + t.lx1 * d));
+}
+
+// Parameters, fp32, one buffer (prepared once per module by the host): W1^T [CIN][HID], W2 [4][HID], b1 [HID],
+// b2 [4], logbinom [NB].  Every read is at a wave-uniform address, so hipcc keeps them in SGPRs (s_load):
+// the 1x1-conv FMAs take their weight as a scalar operand, no LDS traffic.
+__device__ __forceinline__ void load8(const bf16_t* p, int64_t stride, bool vec, float* v) {
+  if (vec) {
+    unpack8(*reinterpret_cast<const u32x4*>(p), v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(p[j * stride]);
+  }
+}
+
+__global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const float* __restrict__ prm) {
+  const int CIN = a.CF + 1 + a.CE;
+  const float* __restrict__ pw1 = prm;
+  const float* __restrict__ pw2 = pw1 + CIN * HID;
+  const float* __restrict__ pb1 = pw2 + 4 * HID;
+  const float* __restrict__ pb2 = pb1 + HID;
+  const float* __restrict__ plb = pb2 + 4;
+
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (int64_t)a.B * a.H * a.W) return;
+  const int x = (int)(pix % a.W);
+  const int y = (int)((pix / a.W) % a.H);
+  const int b = (int)(pix / ((int64_t)a.W * a.H));
+  const Tap ty = tap(y, a.h, a.H), tx = tap(x, a.w, a.W);
+
+  float h[HID];
+#pragma unroll
+  for (int o = 0; o < HID; ++o) h[o] = pb1[o];
+  auto accum8 = [&](const float* v, int c0) {  // channels c0..c0+7
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* wr = pw1 + (c0 + j) * HID;
+#pragma unroll
+      for (int o = 0; o < HID; ++o) h[o] += wr[o] * v[j];
+    }
+  };
+  // main feature (CF channels, CF % 8 == 0) and the relative depth
+  {
+    const bf16_t* fp = a.feat + (int64_t)b * a.fs[0] + y * a.fs[2] + x * a.fs[3];
+    const bool vec = a.fs[1] == 1;
+#pragma unroll 1
+    for (int c = 0; c < a.CF; c += 8) {
+      float v[8];
+      load8(fp + c * a.fs[1], a.fs[1], vec, v);
+      accum8(v, c);
+    }
+    const float r = bf2f(a.rel[(int64_t)b * a.rs[0] + y * a.rs[1] + x * a.rs[2]]);
+    const float* wr = pw1 + a.CF * HID;
+#pragma unroll
+    for (int o = 0; o < HID; ++o) h[o] += wr[o] * r;
+  }
+  // bilinear-upsampled bin embedding (CE channels, CE % 8 == 0)
+  {
+    const Taps2 te = taps2(a.es, ty, tx);
+    const bf16_t* eb = a.emb + (int64_t)b * a.es[0];
+    const bool vec = a.es[1] == 1;
+#pragma unroll 1
+    for (int c = 0; c < a.CE; c += 8) {
+      float q00[8], q01[8], q10[8], q11[8], v[8];
+      const bf16_t* pc = eb + c * a.es[1];
+      load8(pc + te.o00, a.es[1], vec, q00);
+      load8(pc + te.o01, a.es[1], vec, q01);
+      load8(pc + te.o10, a.es[1], vec, q10);
+      load8(pc + te.o11, a.es[1], vec, q11);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = round_bf(te.ly0 * (te.lx0 * q00[j] + te.lx1 * q01[j]) + te.ly1 * (te.lx0 * q10[j] + te.lx1 * q11[j]));
+      accum8(v, a.CF + 1 + c);
+    }
+  }
+
+  float s4[4] = {pb2[0], pb2[1], pb2[2], pb2[3]};
+#pragma unroll
+  for (int o = 0; o < HID; ++o) {
+    const float g = round_bf(gelu_erf(round_bf(h[o])));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s4[q] += pw2[q * HID + o] * g;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s4[q] = round_bf(softplus_f(round_bf(s4[q])));
+  // probabilities / temperature with the reference's bf16 elementwise ops
+  const float p0 = round_bf(s4[0] + a.p_eps), p1 = round_bf(s4[1] + a.p_eps);
+  float p = round_bf(p0 / round_bf(p0 + p1));
+  const float t0 = round_bf(s4[2] + a.p_eps), t1 = round_bf(s4[3] + a.p_eps);
+  const float tq = round_bf(t0 / round_bf(t0 + t1));
+  const float temp = round_bf(round_bf((a.max_t - a.min_t) * tq) + a.min_t);
+  // LogBinomialSoftmax: om = clamp(1 - p), p = clamp(p); y_k = lb_k + bf16(k*log p) + bf16((NB-1-k)*log om)
+  const float om = round_bf(fminf(fmaxf(round_bf(1.f - p), a.clamp_eps), 1.f));
+  p = round_bf(fminf(fmaxf(p, a.clamp_eps), 1.f));
+  const float lp = round_bf(__logf(p)), lom = round_bf(__logf(om));
+  auto zk = [&](int k) {
+    return __fdividef(plb[k] + round_bf((float)k * lp) + round_bf((float)(NB - 1 - k) * lom), temp);
+  };
+  float zmax = -INFINITY;
+#pragma unroll 8
+  for (int k = 0; k < NB; ++k) zmax = fmaxf(zmax, zk(k));
+  float se = 0.f, acc = 0.f;
+  const Taps2 tc = taps2(a.cs, ty, tx);
+  const bf16_t* cb = a.ctr + (int64_t)b * a.cs[0];
+  const bool cvec = a.cs[1] == 1;
+#pragma unroll 1
+  for (int k0 = 0; k0 < NB; k0 += 8) {
+    float q00[8], q01[8], q10[8], q11[8];
+    const bf16_t* pc = cb + k0 * a.cs[1];
+    load8(pc + tc.o00, a.cs[1], cvec, q00);
+    load8(pc + tc.o01, a.cs[1], cvec, q01);
+    load8(pc + tc.o10, a.cs[1], cvec, q10);
+    load8(pc + tc.o11, a.cs[1], cvec, q11);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float bc =
+          round_bf(tc.ly0 * (tc.lx0 * q00[j] + tc.lx1 * q01[j]) + tc.ly1 * (tc.lx0 * q10[j] + tc.lx1 * q11[j]));
+      const float e = __expf(zk(k0 + j) - zmax);
+      se += e;
+      acc += e * bc;
+    }
+  }
+  a.out[pix] = acc / se;
+}
+
+}  // namespace
+
+extern "C" int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
+                                    const void* feat, const int64_t* feat_strides, const void* rel,
+                                    const int64_t* rel_strides, const void* emb, const int64_t* emb_strides,
+                                    const void* ctr, const int64_t* ctr_strides, const float* params, float p_eps,
+                                    float max_t, float min_t, float clamp_eps, float* out, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && H > 1 && W > 1 && h > 1 && w > 1 && CF > 0 && CE > 0, "zoe_tail: bad sizes");
+  SVLA_CHECK_ARG(NBins == NB && Hid == HID && (CF + 1 + CE) / 2 == HID && CF % 8 == 0 && CE % 8 == 0,
+                 "zoe_tail: built for %d bins, %d hidden channels, channel counts multiples of 8 (got %d, %d, %d, %d)",
+                 NB, HID, NBins, Hid, CF, CE);
+  SVLA_CHECK_ARG(feat && rel && emb && ctr && params && out, "zoe_tail: NULL pointer");
+  const bool vf = feat_strides[1] == 1, ve = emb_strides[1] == 1, vc = ctr_strides[1] == 1;
+  SVLA_CHECK_ARG((!vf || ((uintptr_t)feat & 15) == 0) && (!ve || ((uintptr_t)emb & 15) == 0) &&
+                     (!vc || ((uintptr_t)ctr & 15) == 0),
+                 "zoe_tail: channels-last inputs must be 16-B aligned");
+  ZoeTailArgs a;
+  a.B = B; a.H = H; a.W = W; a.h = h; a.w = w; a.CF = CF; a.CE = CE;
+  a.feat = (const bf16_t*)feat; a.rel = (const bf16_t*)rel; a.emb = (const bf16_t*)emb; a.ctr = (const bf16_t*)ctr;
+  for (int i = 0; i < 4; ++i) { a.fs[i] = feat_strides[i]; a.es[i] = emb_strides[i]; a.cs[i] = ctr_strides[i]; }
+  for (int i = 0; i < 3; ++i) a.rs[i] = rel_strides[i];
+  a.p_eps = p_eps; a.max_t = max_t; a.min_t = min_t; a.clamp_eps = clamp_eps; a.out = out;
+  const int64_t npix = (int64_t)B * H * W;
+  hipLaunchKernelGGL(zoe_tail_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
+                     params);
+  return svla::check_launch("zoe_metric_tail");
+}

@@ -400,3 +400,37 @@ def ceil_div(a: int, b: int) -> int:
 
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["math"]
+
+
+# ---------------------------------------------------------------------------------------- Zoe metric tail
+def zoe_metric_tail(clb, feat, rel, emb, ctr):
+    """Fused ZoeDepthMetricDepthEstimationHead tail (csrc/zoe.hip): clb = the
+    ZoeDepthConditionalLogBinomialSoftmax module (its 1x1-conv MLP weights, eps and temperature bounds);
+    feat [B, CF, H, W] outconv activation, rel [B, H, W] relative depth, emb [B, CE, h, w] bin embedding,
+    ctr [B, NB, h, w] bin centres (any strides).  Returns the metric depth [B, 1, H, W] fp32."""
+    B, CF, H, W = feat.shape
+    _req(rel.shape == (B, H, W), "zoe_tail: relative depth must match the outconv activation's size")
+    _, CE, h, w = emb.shape
+    NB = ctr.shape[1]
+    _req(ctr.shape[2:] == emb.shape[2:], "zoe_tail: bin centres and embedding must share the low resolution")
+    for t in (feat, rel, emb, ctr):
+        _chk_bf16(t, "zoe_tail input")
+    c1, c2 = clb.mlp[0], clb.mlp[2]
+    key = (feat.device, c1.weight.data_ptr(), c1.weight._version, c2.weight._version)
+    hit = getattr(clb, "_svla_params", None)
+    if hit is None or hit[0] != key:  # frozen: one fp32 parameter block per module
+        from transformers.models.zoedepth.modeling_zoedepth import log_binom
+        lbt = clb.log_binomial_transform
+        lb = log_binom(lbt.k_minus_1, lbt.k_idx).reshape(-1).float()
+        w1t = c1.weight.reshape(c1.out_channels, -1).float().t().contiguous()
+        w2 = c2.weight.reshape(c2.out_channels, -1).float()
+        prm = torch.cat([w1t.reshape(-1), w2.reshape(-1), c1.bias.float(), c2.bias.float(), lb.to(feat.device)])
+        clb._svla_params = hit = (key, prm.contiguous())
+    prm = hit[1]
+    out = torch.empty(B, 1, H, W, dtype=torch.float32, device=feat.device)
+    i64 = lambda t: (ctypes.c_int64 * t.dim())(*t.stride())  # noqa: E731
+    L.check(L.lib().svla_zoe_metric_tail(B, H, W, h, w, CF, CE, NB, c1.out_channels, feat.data_ptr(), i64(feat),
+                                         rel.data_ptr(), i64(rel), emb.data_ptr(), i64(emb), ctr.data_ptr(), i64(ctr),
+                                         prm.data_ptr(), float(clb.p_eps), float(clb.max_temp), float(clb.min_temp),
+                                         1e-4, out.data_ptr(), _stream()), "zoe_metric_tail")
+    return out

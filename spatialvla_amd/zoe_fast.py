@@ -8,6 +8,10 @@ by the reference at model/modeling_spatialvla.py:314-323).  Installed per instan
 * Conditional log-binomial head (ZoeDepthConditionalLogBinomialSoftmax.forward): the channel concat of the
   contiguous main feature with the channels-last interpolated bin embedding runs as a mixed-layout copy
   (~10 ms at B=32, 384x384).  Concatenating after one explicit NCHW copy gives the same tensor.
+* Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
+  relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
+  and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
+  path's bf16 rounding points; the seed regressor, projectors and attractors stay stock modules.
 """
 import types
 
@@ -37,8 +41,34 @@ def _logbinomial_forward(self, main_feature, condition_feature):
     return type(self).forward(self, main_feature, condition_feature)
 
 
-def install(zoe: torch.nn.Module) -> torch.nn.Module:
-    """Patch the instances inside `zoe` (idempotent)."""
+def _metric_head_forward(self, outconv_activation, bottleneck, feature_blocks, relative_depth):
+    """ZoeDepthMetricDepthEstimationHead.forward (transformers zoedepth [3p]) with the fused tail."""
+    clb = self.conditional_log_binomial
+    if (not outconv_activation.is_cuda or clb.mlp[0].out_channels != 80 or clb.log_binomial_transform.k != 64
+            or outconv_activation.dtype != torch.bfloat16):
+        # the kernel is built for the nyu-kitti head (64 bins, 80 hidden channels, bf16); other configs
+        # (e.g. the tiny test estimator) keep the stock tail
+        return type(self).forward(self, outconv_activation, bottleneck, feature_blocks, relative_depth)
+    x = self.conv2(bottleneck)
+    _, seed_bin_centers = self.seed_bin_regressor(x)
+    if self.bin_centers_type in ["normed", "hybrid2"]:
+        prev_bin = (seed_bin_centers - self.min_depth) / (self.max_depth - self.min_depth)
+    else:
+        prev_bin = seed_bin_centers
+    prev_bin_embedding = self.seed_projector(x)
+    for projector, attractor, feature in zip(self.projectors, self.attractors, feature_blocks):
+        bin_embedding = projector(feature)
+        bin, bin_centers = attractor(bin_embedding, prev_bin, prev_bin_embedding, interpolate=True)
+        prev_bin = bin.clone()
+        prev_bin_embedding = bin_embedding.clone()
+    from . import kernels as K
+    return K.zoe_metric_tail(self.conditional_log_binomial, outconv_activation, relative_depth, bin_embedding,
+                             bin_centers), None
+
+
+def install(zoe: torch.nn.Module, tail: bool = True) -> torch.nn.Module:
+    """Patch the instances inside `zoe` (idempotent).  tail=False keeps the stock metric-head tail (the other
+    two paths are bitwise identical to the stock module)."""
     for m in zoe.modules():
         name = type(m).__name__
         if name == "BeitRelativePositionBias" and not getattr(m, "_svla_fast", False):
@@ -46,5 +76,8 @@ def install(zoe: torch.nn.Module) -> torch.nn.Module:
             m._svla_fast = True
         elif name == "ZoeDepthConditionalLogBinomialSoftmax" and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_logbinomial_forward, m)
+            m._svla_fast = True
+        elif name == "ZoeDepthMetricDepthEstimationHead" and tail and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_metric_head_forward, m)
             m._svla_fast = True
     return zoe

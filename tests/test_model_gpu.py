@@ -65,12 +65,46 @@ def test_zoe_fast_paths_bitwise(cuda):
     ref = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
     fast = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
     fast.load_state_dict(ref.state_dict())
-    zoe_fast.install(fast)
+    zoe_fast.install(fast, tail=False)
     x = torch.randn(2, 3, 384, 384, device=cuda).to(torch.bfloat16)
     with torch.no_grad():
         d0 = ref(pixel_values=x).predicted_depth
         for _ in range(2):
             assert torch.equal(fast(pixel_values=x).predicted_depth, d0)
+
+
+def test_zoe_fused_metric_tail(cuda):
+    """The fused metric-head tail (csrc/zoe.hip) on the nyu-kitti head shapes (64 bins, 161->80->4 MLP) at
+    384x384 vs the stock transformers tail on the same features; random-init weights, B=2.  The stock path
+    is the eager bf16 reference; the kernel reproduces its bf16 rounding points, so the depth agrees to
+    fp32-accumulation-order noise (tolerance 2e-3)."""
+    from transformers import ZoeDepthForDepthEstimation, CONFIG_MAPPING
+    from spatialvla_amd import zoe_fast, presets
+    cfg = CONFIG_MAPPING["zoedepth"](**{k: v for k, v in presets._zoe_large().items() if k != "model_type"})
+    torch.manual_seed(4)
+    zoe = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
+    head = zoe.metric_head
+    B, H, W, h, w = 2, 384, 384, 192, 192
+    feat = torch.rand(B, 32, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    rel = torch.rand(B, H, W, device=cuda).mul(3).to(torch.bfloat16)
+    emb = torch.randn(B, 128, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ctr = torch.rand(B, 64, h, w, device=cuda).mul(10).to(torch.bfloat16)
+    with torch.no_grad():
+        # stock tail, exactly as ZoeDepthMetricDepthEstimationHead.forward runs it
+        rc = torch.nn.functional.interpolate(rel.unsqueeze(1), size=(H, W), mode="bilinear", align_corners=True)
+        last = torch.cat([feat, rc], dim=1)
+        be = torch.nn.functional.interpolate(emb, (H, W), mode="bilinear", align_corners=True)
+        x = head.conditional_log_binomial(last, be)
+        bc = torch.nn.functional.interpolate(ctr, x.shape[-2:], mode="bilinear", align_corners=True)
+        ref = torch.sum(x * bc, dim=1, keepdim=True)
+        from spatialvla_amd import kernels as Kn
+        out = Kn.zoe_metric_tail(head.conditional_log_binomial, feat, rel, emb, ctr)
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    assert H_rel(out, ref) < 2e-3
+
+
+def H_rel(a, b):
+    return H.rel_l2(a, b)
 
 
 def test_tiny_prefill_vs_reference_golden(cuda):

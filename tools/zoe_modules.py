@@ -11,6 +11,9 @@ B = int(os.environ.get("ZB", "32"))
 cfg = CONFIG_MAPPING["zoedepth"](**{k: v for k, v in presets._zoe_large().items() if k != "model_type"})
 with torch.device("cuda"):
     zoe = ZoeDepthForDepthEstimation(cfg).to(torch.bfloat16).eval()
+if os.environ.get("ZFAST", "1") == "1":  # the product's fast paths (spatialvla_amd/zoe_fast.py)
+    from spatialvla_amd import zoe_fast
+    zoe_fast.install(zoe)
 pix = torch.rand(B, 3, 224, 224, device="cuda").to(torch.bfloat16)
 stats = collections.OrderedDict()
 ev = {}
