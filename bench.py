@@ -78,6 +78,25 @@ def make_batch(cfgd, B, seed, device):
     return {k: v.to(device, non_blocking=True) for k, v in t.items()}
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of the same build
+    (profiles/<tag>_pmc_fetch.json + <tag>_pmc_write.json, written by tools/r1_measure.sh: FETCH_SIZE doubled
+    per the gfx950 note of MI355X_MICROARCH.md, WRITE_SIZE as read); None when absent."""
+    import glob
+    tags = sorted(os.path.basename(f)[: -len("_pmc_fetch.json")]
+                  for f in glob.glob(os.path.join(REPO, "profiles", "*_pmc_fetch.json")))
+    for tag in reversed(tags):
+        try:
+            f = json.load(open(os.path.join(REPO, "profiles", f"{tag}_pmc_fetch.json")))
+            w = json.load(open(os.path.join(REPO, "profiles", f"{tag}_pmc_write.json")))
+            return {"bytes": round(f["hbm_read_bytes_per_launch"] + w["hbm_write_bytes_per_launch"]),
+                    "read": round(f["hbm_read_bytes_per_launch"]), "write": round(w["hbm_write_bytes_per_launch"]),
+                    "source": f"profiles/{tag}_pmc_fetch.json + {tag}_pmc_write.json"}
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
+
+
 def dominant_kernel_roofline(records):
     """Roofline of the Gemma2 gate/up GEMM with the fused GeGLU epilogue (the largest kernel of the step):
     its launches inside the timed region, each bracketed by HIP events on the stream it was launched on."""
@@ -89,7 +108,7 @@ def dominant_kernel_roofline(records):
     bytes_alg = 2.0 * (M * K + N * K + 3 * M * (N // 2))   # x, Wg, Wu read; h, g, u written (bf16)
     return {"kernel": "svla gemm8_kernel<KC,KC> (256x256 8-phase) EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "avg_launch_ms": round(avg, 4),
+            "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(), "avg_launch_ms": round(avg, 4),
             "launches_timed": len(ms), "algorithmic_flops_per_launch": flops,
             "algorithmic_bytes_per_launch": bytes_alg}
 

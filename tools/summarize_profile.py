@@ -77,7 +77,7 @@ def pmc(d, out):
     gcol = "Grid_Size" if "Grid_Size" in cols else "Grid_Size_X"
     per = collections.defaultdict(dict)
     for r in rows:
-        if "gemm_kernel" not in r["Kernel_Name"] or int(float(r[gcol])) != DOM_GRID:
+        if re.search(r"gemm8?_kernel", r["Kernel_Name"]) is None or int(float(r[gcol])) != DOM_GRID:
             continue
         per[r.get("Dispatch_Id", r.get("Correlation_Id"))][r["Counter_Name"]] = float(r["Counter_Value"])
     vals = collections.defaultdict(list)
