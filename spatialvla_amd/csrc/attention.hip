@@ -154,7 +154,7 @@ __device__ __forceinline__ bool visible(int c, int kj, int qi, int window) {
   return v;
 }
 
-__device__ __forceinline__ float softcap_f(float z, float cap) { return cap > 0.f ? cap * tanhf(z / cap) : z; }
+__device__ __forceinline__ float softcap_f(float z, float cap) { return cap > 0.f ? cap * fast_tanh(z / cap) : z; }
 
 // key classes of the whole sequence -> LDS (plain loads, before any LDS-DMA is in flight)
 __device__ __forceinline__ void load_classes(uint8_t* lcls, const uint8_t* cls, int L, int t, int nth) {

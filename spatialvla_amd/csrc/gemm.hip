@@ -312,7 +312,7 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           const float cap = E.cap, icap = 1.0f / E.cap;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf(cap * tanhf(round_bf(v[j]) * icap));
+            v[j] = round_bf(cap * fast_tanh(round_bf(v[j]) * icap));
             if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
           }
 #pragma unroll
