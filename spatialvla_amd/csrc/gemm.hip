@@ -21,6 +21,9 @@
 //    along N, every epilogue input (bias, residual, saved activations) a 16-B vector load.
 //  * Block ids are remapped XCD-aware (consecutive tiles share an XCD L2) and grouped along M.
 #include "svla_common.h"
+#include "agpr.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -895,6 +898,356 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, 4 waves (one per SIMD), 128x128 outputs per wave, two 64-k LDS buffers.
+//
+//  * Each wave keeps 64 16x16 accumulators (256 registers, AGPR-resident) and two fragment sets in VGPRs:
+//    F0 = k 0..31 and F1 = k 32..63 of the current k-tile (8 A + 8 B ds_read_b128 each), half the LDS reads per
+//    MFMA of the 8-wave tile.  Buffers are the KC images of the 8-wave kernel ([256][64], 128-B rows, chunk
+//    p of row r holding global chunk p ^ (r & 7)), filled by LDS-DMA (8 rows per 1 KiB wave instruction).
+//  * One k-tile = 128 MFMAs per wave with everything else issued in their gaps:
+//      MFMA 0..15          read F1 (this tile, buffer b)
+//      after MFMA RB1      lgkmcnt(0) + barrier: every wave holds the whole tile, buffer b is free
+//      from MFMA DA0/DB0   LDS-DMA of k-tile kt+2 into buffer b (A then B, one piece every DST MFMAs)
+//      after MFMA RB2      vmcnt(16) + barrier: k-tile kt+1 (buffer b^1) has landed everywhere
+//      next 16 MFMAs       read F0 of kt+1
+//    so every DMA has ~1.6 k-tiles to land and the matrix pipe never waits for a fragment.
+// ---------------------------------------------------------------------------------------------
+#ifndef G4_RB1
+#define G4_RB1 23
+#endif
+#ifndef G4_DA0
+#define G4_DA0 26
+#endif
+#ifndef G4_DB0
+#define G4_DB0 66
+#endif
+#ifndef G4_DST
+#define G4_DST 4
+#endif
+#ifndef G4_RB2
+#define G4_RB2 103
+#endif
+#ifndef G4_PRIO
+#define G4_PRIO 0
+#endif
+namespace p4 {
+constexpr int BM = 256, BN = 256, NTH = 256;
+constexpr int OPB = BM * BK * 2;  // bytes per operand image per buffer (32 KiB)
+constexpr int STAGE = 2 * OPB;    // A | B
+constexpr int LDS = 2 * STAGE;    // 128 KiB (the 66.5 KiB epilogue image reuses it)
+static_assert(64 * (BN + 4) * 4 <= LDS, "epilogue image must fit");
+static_assert(G4_RB1 >= 15 && G4_DA0 > G4_RB1 && G4_DB0 >= G4_DA0 + 8 * G4_DST && G4_RB2 >= G4_DB0 + 8 * G4_DST - 1 &&
+                  G4_RB2 + 16 < 128,
+              "gemm4 schedule knobs out of order");
+}  // namespace p4
+
+template <int X, int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  if constexpr (X < N) {
+    f(std::integral_constant<int, X>{});
+    static_for<X + 1, N>(f);
+  }
+}
+
+struct Op4 {
+  uint32_t v0;   // per-lane byte offset of piece 0 (piece n adds n * 8 rows through the scalar soffset)
+  int nvalid;    // pieces whose row of this lane is inside the valid extent
+  int kq;        // k offset (elements) of this lane's chunk within a k-tile
+  uint32_t rs8;  // 8 rows in bytes (wave-uniform)
+};
+
+// piece n of wave w covers tile rows 64w + 8n .. +7 (waves 0,1: rows 0..127, waves 2,3: rows 128..255); offsets
+// are relative to the base of the wave's 128-row half.  GEGLU: rows 0..127 are gate rows r0/2.., 128..255 the
+// up rows r0/2.. of the second tensor.  Few registers on purpose: the 4-wave kernel runs at 512 VGPRs.
+__device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane, Op4& st) {
+  const int64_t ldb = op.ld * 2;
+  const int gc = (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
+  st.kq = gc * 8;
+  const int row = 64 * w + (lane >> 3);
+  const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + (row & 127) : r0 + row;
+  const int64_t nv = (rv - grow + 7) / 8;
+  st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, 8);
+  st.v0 = (uint32_t)((row & 127) * ldb + gc * 16);
+  st.rs8 = __builtin_amdgcn_readfirstlane((uint32_t)(8 * ldb));
+}
+
+// base address of a 128-row half of the operand tile at k = 0 (GEGLU: half 0 = gate, half 1 = up tensor)
+__device__ __forceinline__ const char* op4_base(const svla_operand& op, int64_t r0, int half) {
+  if (op.seg_dim == SVLA_SEG_GEGLU) return (const char*)((const bf16_t*)op.ptr[half] + (r0 >> 1) * op.ld);
+  int64_t rb = 0;
+  const int64_t rh = r0 + 128 * half;
+  const bf16_t* p = seg_ptr(op, rh, rb);
+  return (const char*)(p + (rh - rb) * op.ld);
+}
+
+// The 64 accumulator quads of a wave live in fixed AGPRs (quad q = 8 * A-fragment + B-fragment in a[4q:4q+3]) and
+// are touched only by the inline asm below (agpr.h): with compiler-allocated accumulators hipcc renames them between
+// the MFMAs of a k-tile and pays ~250 v_accvgpr moves per k-tile at the loop back edge.
+template <int Q>
+__device__ __forceinline__ void agpr_mfma(const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(4 * Q), "i"(4 * Q + 3)
+               : SVLA_AGPR_CLOBBERS);
+}
+__device__ __forceinline__ void agpr_zero() { asm volatile(SVLA_AGPR_ZERO_ASM ::: SVLA_AGPR_CLOBBERS); }
+// MFMA results -> v_accvgpr_read: 12 wait states (8-pass XDL)
+__device__ __forceinline__ void agpr_fence() { asm volatile("s_nop 7\n\ts_nop 4" ::: SVLA_AGPR_CLOBBERS); }
+template <int Q>
+__device__ __forceinline__ f32x4 agpr_get() {
+  float r0, r1, r2, r3;
+  asm volatile(
+      "v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\tv_accvgpr_read_b32 %2, a%c6\n\t"
+      "v_accvgpr_read_b32 %3, a%c7"
+      : "=v"(r0), "=v"(r1), "=v"(r2), "=v"(r3)
+      : "i"(4 * Q), "i"(4 * Q + 1), "i"(4 * Q + 2), "i"(4 * Q + 3));
+  return f32x4{r0, r1, r2, r3};
+}
+template <int Q>
+__device__ __forceinline__ void agpr_set(const f32x4& v) {
+  asm volatile(
+      "v_accvgpr_write_b32 a%c4, %0\n\tv_accvgpr_write_b32 a%c5, %1\n\tv_accvgpr_write_b32 a%c6, %2\n\t"
+      "v_accvgpr_write_b32 a%c7, %3\n\ts_nop 1" ::"v"(v[0]),
+      "v"(v[1]), "v"(v[2]), "v"(v[3]), "i"(4 * Q), "i"(4 * Q + 1), "i"(4 * Q + 2), "i"(4 * Q + 3)
+      : SVLA_AGPR_CLOBBERS);
+}
+
+#define P4_FOR_ACC(BODY)                           \
+  _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) \
+  _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) { BODY; }
+
+__global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
+                                                        svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
+  using namespace p4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t_in = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(t_in >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int tiles_n = (int)((N + BN - 1) / BN), tiles_m = (int)((M + BM - 1) / BM);
+  const int L = xcd_remap(blockIdx.x, sk.grid);
+  const int nk = sk.nk;
+  const int64_t rvA = A.r_valid > 0 ? A.r_valid : M;
+  const int64_t kvA = A.k_valid > 0 ? A.k_valid : K;
+  const int64_t rvB = B.r_valid > 0 ? B.r_valid : (B.seg_dim == SVLA_SEG_GEGLU ? B.seg_start[1] : N);
+  const int64_t kvB = B.k_valid > 0 ? B.k_valid : K;
+
+  auto coords = [&](int tile, int64_t& m0, int64_t& n0) {
+    const int group = GROUP_M * tiles_n;
+    const int first_m = (tile / group) * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    m0 = (int64_t)(first_m + (tile % group) % gsz) * BM;
+    n0 = (int64_t)((tile % group) / gsz) * BN;
+  };
+
+  auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
+    agpr_zero();
+    Op4 sa, sb;
+    op4_setup(A, m0, rvA, w, lane, sa);
+    op4_setup(B, n0, rvB, w, lane, sb);
+    const char* const abase = op4_base(A, m0, w >> 1);
+    const char* const bbase = op4_base(B, n0, w >> 1);
+    // one DMA piece: n < 8 -> A piece n, else B piece n - 8, of k-tile kt into buffer buf
+    auto piece = [&](const __amdgpu_buffer_rsrc_t& rs, bool ok, const Op4& st, int n, char* img) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(img + (8 * w + n) * 1024), 16,
+                                               (ok && n < st.nvalid) ? st.v0 : OOB, n * st.rs8, 0, 0);
+    };
+    auto issue_all = [&](int kt, char* stage) {
+      const int64_t k0 = (int64_t)kt * BK;
+      const __amdgpu_buffer_rsrc_t rsa = make_rsrc(abase + k0 * 2), rsb = make_rsrc(bbase + k0 * 2);
+      const bool oka = sa.kq < kvA - k0, okb = sb.kq < kvB - k0;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) piece(rsa, oka, sa, n, stage);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) piece(rsb, okb, sb, n, stage + OPB);
+    };
+    const int nq = ke - kb;
+    issue_all(kb, smem);
+    if (nq > 1) {
+      issue_all(kb + 1, smem + STAGE);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    P8_BARRIER();
+    bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0a[i] = read_frag<SVLA_LAYOUT_KC, 256>(smem, 128 * wr + 16 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f0b[j] = read_frag<SVLA_LAYOUT_KC, 256>(smem + OPB, 128 * wc + 16 * j, 0, lane);
+
+    // one k-tile; DMA: stage k-tile kt+2 into this buffer; NEXT: k-tile kt+1 exists (wait for it, read its F0)
+    auto ktile = [&](int kt, auto DMA, auto NEXT) {
+      char* const cur = smem + ((kt - kb) & 1) * STAGE;
+      char* const nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
+      const int64_t k2 = (int64_t)(kt + 2) * BK;
+      __amdgpu_buffer_rsrc_t rsa, rsb;
+      bool oka = false, okb = false;
+      if constexpr (decltype(DMA)::value) {
+        rsa = make_rsrc(abase + k2 * 2);
+        rsb = make_rsrc(bbase + k2 * 2);
+        oka = sa.kq < kvA - k2;
+        okb = sb.kq < kvB - k2;
+      }
+      if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
+      static_for<0, 128>([&](auto XC) {
+        constexpr int x = decltype(XC)::value;
+        constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
+        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii], f0b[jj]);
+        else agpr_mfma<ii * 8 + jj>(f1a[ii], f1b[jj]);
+        if constexpr (x < 8) f1a[x] = read_frag<SVLA_LAYOUT_KC, 256>(cur, 128 * wr + 16 * x, 1, lane);
+        else if constexpr (x < 16) f1b[x - 8] = read_frag<SVLA_LAYOUT_KC, 256>(cur + OPB, 128 * wc + 16 * (x - 8), 1, lane);
+        if constexpr (x == G4_RB1) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (decltype(DMA)::value) {
+          if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0)
+            piece(rsa, oka, sa, (x - G4_DA0) / G4_DST, cur);
+          if constexpr (x >= G4_DB0 && x < G4_DB0 + 8 * G4_DST && (x - G4_DB0) % G4_DST == 0)
+            piece(rsb, okb, sb, (x - G4_DB0) / G4_DST, cur + OPB);
+        }
+        if constexpr (decltype(NEXT)::value) {
+          if constexpr (x == G4_RB2) {
+            if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+          }
+          constexpr int r = x - G4_RB2 - 1;
+          if constexpr (r >= 0 && r < 8) f0a[r] = read_frag<SVLA_LAYOUT_KC, 256>(nxt, 128 * wr + 16 * r, 0, lane);
+          else if constexpr (r >= 8 && r < 16)
+            f0b[r - 8] = read_frag<SVLA_LAYOUT_KC, 256>(nxt + OPB, 128 * wc + 16 * (r - 8), 0, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (G4_PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    int kt = kb;
+#pragma unroll 1
+    for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{});
+    if (kt + 1 < ke) {
+      ktile(kt, F{}, T{});
+      ++kt;
+    }
+    ktile(kt, F{}, F{});
+    agpr_fence();  // MFMA results -> epilogue / slab readers
+    __syncthreads();
+  };
+
+  auto epilogue = [&](int64_t m0, int64_t n0, const int t) {
+    const int lane = t & 63;
+    tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+      // pass p holds rows [64p, 64p+64): wave row wr = p >> 1, fragments 4(p&1)..4(p&1)+3
+      if ((pass >> 1) == wr) {
+        auto rows = [&](auto H) {
+          static_for<0, 32>([&](auto IJ) {
+            constexpr int i = decltype(IJ)::value >> 3, j = decltype(IJ)::value & 7;
+            const f32x4 v = agpr_get<(4 * decltype(H)::value + i) * 8 + j>();
+            const int col = 128 * wc + 16 * j + (lane & 15);
+            const int r = 16 * i + 4 * (lane >> 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = v[q];
+          });
+        };
+        if (pass & 1) rows(std::integral_constant<int, 1>{});
+        else rows(std::integral_constant<int, 0>{});
+      }
+    });
+  };
+
+  const int64_t I = sk.sk_iters, G = sk.grid;
+  const int64_t it1 = ((int64_t)L + 1) * I / G;
+  int* sflag = reinterpret_cast<int*>(smem);
+  int dp_tile = L;
+  int64_t it = (int64_t)L * I / G;
+#pragma unroll 1
+  while (true) {
+    int tile, kb, ke, st = 0;
+    if (dp_tile < sk.dp_tiles) {
+      tile = dp_tile;
+      dp_tile += sk.grid;
+      kb = 0;
+      ke = nk;
+    } else {
+      if (it >= it1) break;
+      st = (int)(it / nk);
+      kb = (int)(it - (int64_t)st * nk);
+      ke = (int)min((int64_t)nk, kb + (it1 - it));
+      it += ke - kb;
+      tile = sk.dp_tiles + st;
+    }
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t_in));
+    int64_t m0, n0;
+    coords(tile, m0, n0);
+    mainloop(m0, n0, kb, ke, t & 63);
+    if (kb != 0 || ke != nk) {
+      // partial tile: the stream-K hand-off of gemm8_kernel (slab per segment, last arriver reduces in k order)
+      const int64_t T0 = (int64_t)st * nk, T1 = T0 + nk;
+      const int Lh = (int)(((T0 + 1) * G + I - 1) / I - 1);
+      const int Ll = (int)min(G - 1, (T1 * G + I - 1) / I - 1);
+      const int nseg = Ll - Lh + 1, j = L - Lh;
+      auto slab = [&](int seg) {
+        return make_rsrc(reinterpret_cast<const f32x4*>(sk.slabs) +
+                         (int64_t)(2 * (Lh + seg) + (seg == 0 ? 1 : 0)) * (64 * NTH));
+      };
+      int* cnt = sk.counters + st;
+      bool last = false;
+      if (j == 0) {
+        if (t == 0) {
+          const int c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sflag[0] = (c == nseg - 1);
+          if (c == nseg - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        last = sflag[0] != 0;
+        __syncthreads();
+      }
+      if (!last) {
+        const __amdgpu_buffer_rsrc_t rs = slab(j);
+        uint32_t vo = t * 16;
+        static_for<0, 64>([&](auto Q) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, agpr_get<decltype(Q)::value>()), rs, vo, 0,
+                                                 16);
+          vo += NTH * 16;
+          asm volatile("" : "+v"(vo));
+        });
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+          const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sflag[0] = (old == nseg - 1);
+          if (old == nseg - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        last = sflag[0] != 0;
+        __syncthreads();
+      }
+      if (!last) continue;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int sg = (j != 0) ? 0 : 1; sg < nseg; ++sg) {
+        const __amdgpu_buffer_rsrc_t rs = slab(sg);
+        const bool first = sg == 0;
+        uint32_t vo = t * 16;
+        static_for<0, 4>([&](auto A4) {  // 16 accumulator quads in flight per step
+          constexpr int a = decltype(A4)::value;
+          f32x4 x[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            x[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, u * NTH * 16, 16));
+          static_for<0, 16>([&](auto U) {
+            constexpr int u = decltype(U)::value;
+            agpr_set<16 * a + u>(first ? x[u] : agpr_get<16 * a + u>() + x[u]);
+          });
+          vo += 16 * NTH * 16;
+          asm volatile("" : "+v"(vo));
+        });
+      }
+    }
+    epilogue(m0, n0, t);
+  }
+}
+
 template <auto KERN>
 void set_lds_once(int bytes) {
   static bool done = false;
@@ -986,6 +1339,32 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   else SVLA_LAUNCH8(1, 1)
 #undef SVLA_LAUNCH8
   return svla::check_launch("gemm8");
+}
+
+int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
+            const svla_epilogue& E, hipStream_t s) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  SKArgs sk;
+  memset(&sk, 0, sizeof(sk));
+  sk.nk = (int)((K + BK - 1) / BK);
+  sk.dp_tiles = (int)tiles;
+  sk.grid = (int)tiles;
+  const int G = num_cus();
+  const int64_t rem = tiles % G;
+  int64_t sk_tiles = tiles < G ? tiles : rem;
+  if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
+  if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;
+  const size_t need = sk_workspace_bytes(G);
+  if (g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G && sk_tiles * sk.nk >= 8 * G) {
+    sk.dp_tiles = (int)(tiles - sk_tiles);
+    sk.grid = G;
+    sk.sk_iters = sk_tiles * sk.nk;
+    sk.slabs = reinterpret_cast<float*>(g_ws.ptr);
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(g_ws.ptr) + (size_t)2 * G * 32 * p8::NTH * 16);
+  }
+  set_lds_once<gemm4_kernel>(p4::LDS);
+  hipLaunchKernelGGL(gemm4_kernel, dim3((unsigned)sk.grid), dim3(p4::NTH), p4::LDS, s, M, N, K, A, B, Cd, E, sk);
+  return svla::check_launch("gemm4");
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -1111,6 +1490,10 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
     if (g_variant != 1 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
     return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   }
+  const bool kckc = A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC;
+  if (g_variant == 3 && kckc && !kseg && seg_ok(256, 256) &&
+      (tiles(256, 256) >= 512 || (g_ws.ptr && tiles(256, 256) * nk >= 8 * num_cus())))
+    return launch4(M, N, K, *A, *B, C, *epi, s);
   if (g_variant != 1 && !kseg && seg_ok(256, 256) &&
       (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
     return launch8(M, N, K, *A, *B, C, *epi, s);

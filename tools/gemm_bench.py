@@ -16,6 +16,7 @@ SHAPES = [  # name, M, N, K, layouts
     ("siglip fc2 fwd", 8192, 1152, 4304, "nt"), ("siglip fc2 dgrad", 8192, 4304, 1152, "nn"),
     ("siglip fc1 wgrad", 4304, 1152, 8192, "tn"), ("siglip o wgrad", 1152, 1152, 8192, "tn"),
     ("qkv wgrad", 4096, 2304, M, "tn"), ("o dgrad", M, 2048, 2304, "nn"),
+    ("square 4k", 4096, 4096, 4096, "nt"), ("square 8k", 8192, 8192, 8192, "nt"),
 ]
 
 
@@ -53,11 +54,15 @@ def run(name, m, n, k, lay, reps=10):
             e1.record(); e1.synchronize()
             ms = e0.elapsed_time(e1) / reps
             best[tag] = min(best.get(tag, 1e30), ms)
+    r = ref().float()
+    errs = []
+    for v in variants:
+        L.lib().svla_gemm_set_variant(v)
+        c.fill_(float("nan")); f(); torch.cuda.synchronize()
+        errs.append(f"{((c.float() - r).norm() / r.norm()).item():.1e}")
     L.lib().svla_gemm_set_variant(variants[0])
-    f(); torch.cuda.synchronize()
-    err = ((c.float() - ref().float()).norm() / ref().float().norm()).item()
     cols = "  ".join(f"{t} {best[t]:7.3f} ms {2.0 * m * n * k / best[t] / 1e9:7.1f} TF" for t, _, _ in arms)
-    print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} {cols}  relerr {err:.1e}", flush=True)
+    print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} {cols}  relerr {'/'.join(errs)}", flush=True)
 
 
 def stamps(m, n, k, lay="nt"):
