@@ -11,6 +11,8 @@ Extra objects:
   roofline     — the dominant kernel (the Gemma2 gate/up GeGLU GEMM, M=B*312, N=2*9216, K=2304): every
                  launch of it inside the timed steps is bracketed by HIP events on its launch stream;
                  algorithmic FLOPs per launch / mean launch time vs the bf16 dense MFMA peak (2.5 PFLOP/s).
+  gemma2_block — the north-star target: one Gemma2 decoder layer fwd+bwd at B=32 timed in isolation (untimed
+                 region), algorithmic FLOPs / time vs the same peak (target frac >= 0.40).
   cpu_baseline — the CPU oracle (oracle/spatialvla_oracle.py, the reference eager restatement) fwd+bwd
                  at B=1 on this host's cores, rank 0 / N=1 only.
 """
@@ -106,11 +108,54 @@ def dominant_kernel_roofline(records):
     flops = 2.0 * M * N * K                          # algorithmic: M x (2I) x H multiply-adds
     ach = flops / (avg * 1e-3) / 1e12
     bytes_alg = 2.0 * (M * K + N * K + 3 * M * (N // 2))   # x, Wg, Wu read; h, g, u written (bf16)
-    return {"kernel": "svla gemm8_kernel<KC,KC> (256x256 8-phase) EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
+    return {"kernel": "svla gemm4_kernel_00 (256x256 tile, 4 waves x 128x128, AGPR accumulators) EPI_GEGLU "
+                      "(Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(), "avg_launch_ms": round(avg, 4),
             "launches_timed": len(ms), "algorithmic_flops_per_launch": flops,
             "algorithmic_bytes_per_launch": bytes_alg}
+
+
+def gemma2_block_roofline(model, B, L, device, iters=5):
+    """The north-star target: one Gemma2DecoderLayer fwd+bwd at B episodes x L tokens (sandwich norms, QKV+RoPE,
+    prefix-LM GQA attention with softcap, o_proj, GeGLU MLP; every dW written), timed in isolation with HIP
+    events on the stream the kernels run on.  Algorithmic FLOPs = 3 x fwd matmul FLOPs (SURVEY §8a a14:
+    1283.9 GFLOP/episode over 26 layers)."""
+    from spatialvla_amd.modeling_gemma2 import KVMask
+    lm = model.language_model.model
+    layer = lm.layers[1]
+    cfg = lm.config
+    tt = torch.zeros(B, L, dtype=torch.long, device=device)
+    tt[:, L - 13:] = 1
+    mask = KVMask.build(torch.ones(B, L, dtype=torch.long, device=device), tt, True, B, L, device)
+    pos = torch.arange(1, L + 1, device=device).unsqueeze(0).expand(B, L)
+    rope = layer.self_attn.rotary_emb.tables(pos, torch.bfloat16)
+    g = torch.Generator(device=device).manual_seed(5)
+    x = torch.randn(B, L, cfg.hidden_size, device=device, generator=g).to(torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(B, L, cfg.hidden_size, device=device, generator=g).to(torch.bfloat16)
+    H, I, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    hq, hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+    mac_tok = H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I + 2 * hq * L * D
+    flops = 3 * 2.0 * mac_tok * B * L
+    stream = torch.cuda.current_stream()
+    fwd_ms, tot_ms = [], []
+    for it in range(iters + 2):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        x.grad = None
+        e0.record(stream)
+        y = layer(x, mask, rope)
+        e1.record(stream)
+        y.backward(gy)
+        e2.record(stream)
+        e2.synchronize()
+        if it >= 2:
+            fwd_ms.append(e0.elapsed_time(e1)); tot_ms.append(e0.elapsed_time(e2))
+    ms = float(np.mean(tot_ms))
+    ach = flops / (ms * 1e-3) / 1e12
+    return {"what": f"Gemma2DecoderLayer fwd+bwd, B={B} x L={L} (M={B * L} token rows)", "bound": "mfma",
+            "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+            "ms_fwd_bwd": round(ms, 3), "ms_fwd": round(float(np.mean(fwd_ms)), 3),
+            "algorithmic_flops": flops, "target_frac": 0.40}
 
 
 def cpu_baseline(cfgd, iters):
@@ -217,6 +262,8 @@ def main():
     }
     if rank == 0:
         result["roofline"] = dominant_kernel_roofline(geglu_events)
+        if args.config == "spatialvla_4b":
+            result["gemma2_block"] = gemma2_block_roofline(model, B, 312, device)
         if world == 1 and not args.no_cpu_baseline:
             del batches, engine
             torch.cuda.empty_cache()

@@ -920,16 +920,19 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #define G4_DA0 26
 #endif
 #ifndef G4_DB0
-#define G4_DB0 66
+#define G4_DB0 62
 #endif
 #ifndef G4_DST
 #define G4_DST 4
 #endif
 #ifndef G4_RB2
-#define G4_RB2 103
+#define G4_RB2 95
 #endif
 #ifndef G4_PRIO
 #define G4_PRIO 0
+#endif
+#ifndef G4_GROUP_M
+#define G4_GROUP_M GROUP_M
 #endif
 namespace p4 {
 constexpr int BM = 256, BN = 256, NTH = 256;
@@ -950,35 +953,81 @@ __device__ __forceinline__ void static_for(Fn&& f) {
   }
 }
 
+template <int LAYOUT>
 struct Op4 {
-  uint32_t v0;   // per-lane byte offset of piece 0 (piece n adds n * 8 rows through the scalar soffset)
-  int nvalid;    // pieces whose row of this lane is inside the valid extent
-  int kq;        // k offset (elements) of this lane's chunk within a k-tile
-  uint32_t rs8;  // 8 rows in bytes (wave-uniform)
+  uint32_t v0, v1;  // per-lane byte offsets of piece 0 (RC: pieces with n & 2 use v1); piece n adds n * rs via soffset
+  int kq;           // KC: k offset (elements) of this lane's chunk; RC: k-row of this lane in piece 0
+  int nvalid;       // KC: pieces whose row of this lane is inside the valid extent
+  bool ok0, ok1;    // RC: this lane's outer chunk (v0 / v1 variant) starts inside the valid extent
+  uint32_t rs;      // wave-uniform byte step per piece: KC 8 rows, RC 4 k-rows
 };
 
-// piece n of wave w covers tile rows 64w + 8n .. +7 (waves 0,1: rows 0..127, waves 2,3: rows 128..255); offsets
-// are relative to the base of the wave's 128-row half.  GEGLU: rows 0..127 are gate rows r0/2.., 128..255 the
-// up rows r0/2.. of the second tensor.  Few registers on purpose: the 4-wave kernel runs at 512 VGPRs.
-__device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane, Op4& st) {
+// Staging of a 256-outer x 64-k operand tile: waves 0,1 stage outer half 0, waves 2,3 half 1, 8 pieces (1 KiB
+// LDS-DMA wave instructions) each; offsets are relative to the base of the wave's half (op4_base).
+//  KC: image [256][64] (128-B rows, chunk p of row r = global chunk p ^ (r & 7)); piece n of wave w = rows
+//      64w + 8n .. +7.  GEGLU: rows 0..127 are gate rows r0/2.., 128..255 the up rows of the second tensor.
+//  RC: two half images [64 k][128 outer] (256-B rows, chunk p of k-row k = global chunk p ^ rc_swz(k)); piece n
+//      of wave w = k-rows 4j .. 4j+3 of its half, j = 8 (w & 1) + n.  rc_swz depends on n only through n & 2.
+template <int LAYOUT>
+__device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane,
+                                          Op4<LAYOUT>& st) {
   const int64_t ldb = op.ld * 2;
-  const int gc = (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
-  st.kq = gc * 8;
-  const int row = 64 * w + (lane >> 3);
-  const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + (row & 127) : r0 + row;
-  const int64_t nv = (rv - grow + 7) / 8;
-  st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, 8);
-  st.v0 = (uint32_t)((row & 127) * ldb + gc * 16);
-  st.rs8 = __builtin_amdgcn_readfirstlane((uint32_t)(8 * ldb));
+  if (LAYOUT == SVLA_LAYOUT_KC) {
+    const int gc = (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
+    st.kq = gc * 8;
+    const int row = 64 * w + (lane >> 3);
+    const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + (row & 127) : r0 + row;
+    const int64_t nv = (rv - grow + 7) / 8;
+    st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, 8);
+    st.v0 = st.v1 = (uint32_t)((row & 127) * ldb + gc * 16);
+    st.ok0 = st.ok1 = true;
+    st.rs = __builtin_amdgcn_readfirstlane((uint32_t)(8 * ldb));
+  } else {
+    const int kr = 32 * (w & 1) + (lane >> 4);  // k-row of piece 0 (piece n: + 4n)
+    st.kq = kr;
+    st.nvalid = 8;
+    const int64_t o = r0 + 128 * (w >> 1);
+    const int gc0 = (lane & 15) ^ rc_swz(kr), gc1 = (lane & 15) ^ rc_swz(kr + 8);
+    st.ok0 = o + gc0 * 8 < rv;
+    st.ok1 = o + gc1 * 8 < rv;
+    st.v0 = (uint32_t)(kr * ldb + gc0 * 16);
+    st.v1 = (uint32_t)(kr * ldb + gc1 * 16);
+    st.rs = __builtin_amdgcn_readfirstlane((uint32_t)(4 * ldb));
+  }
 }
 
-// base address of a 128-row half of the operand tile at k = 0 (GEGLU: half 0 = gate, half 1 = up tensor)
+// voffset of piece n of the wave at krem = valid k extent left in the k-tile (OOB -> zero-fill).  Plain overloads,
+// not templates: the lambdas of gemm4_body are also analysed for the host, where a device-only function template
+// called from them fails to substitute.
+__device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_KC>& st, int n, int64_t krem) {
+  return (st.kq < krem && n < st.nvalid) ? st.v0 : OOB;
+}
+__device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_RC>& st, int n, int64_t krem) {
+  return (st.kq + 4 * n < krem && ((n & 2) ? st.ok1 : st.ok0)) ? ((n & 2) ? st.v1 : st.v0) : OOB;
+}
+
+// piece n of the wave for the k-tile whose half-tile base address is kbase
+__device__ __forceinline__ void op4_piece(const char* kbase, uint32_t voff, uint32_t soff, int n, char* img, int w) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(kbase), (LDS_AS void*)(img + (8 * w + n) * 1024), 16, voff, soff,
+                                           0, 0);
+}
+
+// base address of the wave's 128-outer half of the operand tile at k = 0 (GEGLU: half 0 = gate, 1 = up tensor)
+template <int LAYOUT>
 __device__ __forceinline__ const char* op4_base(const svla_operand& op, int64_t r0, int half) {
-  if (op.seg_dim == SVLA_SEG_GEGLU) return (const char*)((const bf16_t*)op.ptr[half] + (r0 >> 1) * op.ld);
+  if (LAYOUT == SVLA_LAYOUT_KC && op.seg_dim == SVLA_SEG_GEGLU)
+    return (const char*)((const bf16_t*)op.ptr[half] + (r0 >> 1) * op.ld);
   int64_t rb = 0;
   const int64_t rh = r0 + 128 * half;
   const bf16_t* p = seg_ptr(op, rh, rb);
-  return (const char*)(p + (rh - rb) * op.ld);
+  return (const char*)(p + (rh - rb) * (LAYOUT == SVLA_LAYOUT_KC ? op.ld : 1));
+}
+
+// MFMA fragment of rows 16i of the wave's 128-outer block ob (= 128 wr or 128 wc) of an operand image
+template <int LAYOUT>
+__device__ __forceinline__ void frag4_load(Frag<LAYOUT>& f, const char* img, int ob, int i, int ks, int lane) {
+  if (LAYOUT == SVLA_LAYOUT_KC) f.load(img, ob + 16 * i, ks, lane);
+  else f.load(img + (ob >> 7) * (128 * BK * 2), 16 * i, ks, lane);
 }
 
 // The 64 accumulator quads of a wave live in fixed AGPRs (quad q = 8 * A-fragment + B-fragment in a[4q:4q+3]) and
@@ -1015,8 +1064,13 @@ __device__ __forceinline__ void agpr_set(const f32x4& v) {
   _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) \
   _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) { BODY; }
 
-__global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
-                                                        svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
+// The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
+// template are also instantiated for the host, where the device-only helpers they call fail to substitute and
+// the kernel stub silently disappears.
+template <int LA, int LB>
+__device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
+                                           const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
+                                           const SKArgs& sk) {
   using namespace p4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t_in = threadIdx.x;
@@ -1031,33 +1085,36 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int
   const int64_t kvB = B.k_valid > 0 ? B.k_valid : K;
 
   auto coords = [&](int tile, int64_t& m0, int64_t& n0) {
-    const int group = GROUP_M * tiles_n;
-    const int first_m = (tile / group) * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int group = G4_GROUP_M * tiles_n;
+    const int first_m = (tile / group) * G4_GROUP_M;
+    const int gsz = min(tiles_m - first_m, G4_GROUP_M);
     m0 = (int64_t)(first_m + (tile % group) % gsz) * BM;
     n0 = (int64_t)((tile % group) / gsz) * BN;
   };
 
+  const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
+
   auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
     agpr_zero();
-    Op4 sa, sb;
-    op4_setup(A, m0, rvA, w, lane, sa);
-    op4_setup(B, n0, rvB, w, lane, sb);
-    const char* const abase = op4_base(A, m0, w >> 1);
-    const char* const bbase = op4_base(B, n0, w >> 1);
-    // one DMA piece: n < 8 -> A piece n, else B piece n - 8, of k-tile kt into buffer buf
-    auto piece = [&](const __amdgpu_buffer_rsrc_t& rs, bool ok, const Op4& st, int n, char* img) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(img + (8 * w + n) * 1024), 16,
-                                               (ok && n < st.nvalid) ? st.v0 : OOB, n * st.rs8, 0, 0);
-    };
+    Op4<LA> sa;
+    Op4<LB> sb;
+    op4_setup<LA>(A, m0, rvA, w, lane, sa);
+    op4_setup<LB>(B, n0, rvB, w, lane, sb);
+    const char* const abase = op4_base<LA>(A, m0, w >> 1);
+    const char* const bbase = op4_base<LB>(B, n0, w >> 1);
+    // piece n of the wave for the k-tile at krem = valid k extent left (KC: per-lane chunk check, RC: k-row check)
+    // (the LDS-DMA itself lives in a __device__ function: lambdas of a kernel template are instantiated for the
+    // host too, where the address-space cast would be a substitution failure and the kernel stub would vanish)
+    auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w); };
+    auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
     auto issue_all = [&](int kt, char* stage) {
       const int64_t k0 = (int64_t)kt * BK;
-      const __amdgpu_buffer_rsrc_t rsa = make_rsrc(abase + k0 * 2), rsb = make_rsrc(bbase + k0 * 2);
-      const bool oka = sa.kq < kvA - k0, okb = sb.kq < kvB - k0;
+      const char* const ka = abase + k0 * ksa;
+      const char* const kbb = bbase + k0 * ksb;
 #pragma unroll
-      for (int n = 0; n < 8; ++n) piece(rsa, oka, sa, n, stage);
+      for (int n = 0; n < 8; ++n) pieceA(ka, kvA - k0, n, stage);
 #pragma unroll
-      for (int n = 0; n < 8; ++n) piece(rsb, okb, sb, n, stage + OPB);
+      for (int n = 0; n < 8; ++n) pieceB(kbb, kvB - k0, n, stage + OPB);
     };
     const int nq = ke - kb;
     issue_all(kb, smem);
@@ -1068,42 +1125,42 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     P8_BARRIER();
-    bf16x8 f0a[8], f0b[8], f1a[8], f1b[8];
+    Frag<LA> f0a[8], f1a[8];
+    Frag<LB> f0b[8], f1b[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f0a[i] = read_frag<SVLA_LAYOUT_KC, 256>(smem, 128 * wr + 16 * i, 0, lane);
+    for (int i = 0; i < 8; ++i) frag4_load<LA>(f0a[i], smem, 128 * wr, i, 0, lane);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f0b[j] = read_frag<SVLA_LAYOUT_KC, 256>(smem + OPB, 128 * wc + 16 * j, 0, lane);
+    for (int j = 0; j < 8; ++j) frag4_load<LB>(f0b[j], smem + OPB, 128 * wc, j, 0, lane);
 
-    // one k-tile; DMA: stage k-tile kt+2 into this buffer; NEXT: k-tile kt+1 exists (wait for it, read its F0)
+    // one k-tile; DMA: stage k-tile kt+2 into this buffer; NEXT: k-tile kt+1 exists (wait for it, read its F0).
+    // RC fragments come from asm transpose reads (hipcc would drain every LDS-DMA before a builtin one), which
+    // the waitcnt pass cannot see: the fragments of a set are combined into MFMA operands only after an
+    // explicit lgkmcnt(0) (set 0: at the top of the k-tile, set 1: at RB1).
     auto ktile = [&](int kt, auto DMA, auto NEXT) {
       char* const cur = smem + ((kt - kb) & 1) * STAGE;
       char* const nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
       const int64_t k2 = (int64_t)(kt + 2) * BK;
-      __amdgpu_buffer_rsrc_t rsa, rsb;
-      bool oka = false, okb = false;
-      if constexpr (decltype(DMA)::value) {
-        rsa = make_rsrc(abase + k2 * 2);
-        rsb = make_rsrc(bbase + k2 * 2);
-        oka = sa.kq < kvA - k2;
-        okb = sb.kq < kvB - k2;
-      }
+      const char* const rsa = abase + k2 * ksa;
+      const char* const rsb = bbase + k2 * ksb;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
       static_for<0, 128>([&](auto XC) {
         constexpr int x = decltype(XC)::value;
         constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
-        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii], f0b[jj]);
-        else agpr_mfma<ii * 8 + jj>(f1a[ii], f1b[jj]);
-        if constexpr (x < 8) f1a[x] = read_frag<SVLA_LAYOUT_KC, 256>(cur, 128 * wr + 16 * x, 1, lane);
-        else if constexpr (x < 16) f1b[x - 8] = read_frag<SVLA_LAYOUT_KC, 256>(cur + OPB, 128 * wc + 16 * (x - 8), 1, lane);
+        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii].get(), f0b[jj].get());
+        else agpr_mfma<ii * 8 + jj>(f1a[ii].get(), f1b[jj].get());
+        if constexpr (x < 8) frag4_load<LA>(f1a[x], cur, 128 * wr, x, 1, lane);
+        else if constexpr (x < 16) frag4_load<LB>(f1b[x - 8], cur + OPB, 128 * wc, x - 8, 1, lane);
         if constexpr (x == G4_RB1) {
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
           __builtin_amdgcn_s_barrier();
         }
         if constexpr (decltype(DMA)::value) {
           if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0)
-            piece(rsa, oka, sa, (x - G4_DA0) / G4_DST, cur);
+            pieceA(rsa, kvA - k2, (x - G4_DA0) / G4_DST, cur);
           if constexpr (x >= G4_DB0 && x < G4_DB0 + 8 * G4_DST && (x - G4_DB0) % G4_DST == 0)
-            piece(rsb, okb, sb, (x - G4_DB0) / G4_DST, cur + OPB);
+            pieceB(rsb, kvB - k2, (x - G4_DB0) / G4_DST, cur + OPB);
         }
         if constexpr (decltype(NEXT)::value) {
           if constexpr (x == G4_RB2) {
@@ -1112,9 +1169,8 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int
             __builtin_amdgcn_s_barrier();
           }
           constexpr int r = x - G4_RB2 - 1;
-          if constexpr (r >= 0 && r < 8) f0a[r] = read_frag<SVLA_LAYOUT_KC, 256>(nxt, 128 * wr + 16 * r, 0, lane);
-          else if constexpr (r >= 8 && r < 16)
-            f0b[r - 8] = read_frag<SVLA_LAYOUT_KC, 256>(nxt + OPB, 128 * wc + 16 * (r - 8), 0, lane);
+          if constexpr (r >= 0 && r < 8) frag4_load<LA>(f0a[r], nxt, 128 * wr, r, 0, lane);
+          else if constexpr (r >= 8 && r < 16) frag4_load<LB>(f0b[r - 8], nxt + OPB, 128 * wc, r - 8, 0, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1248,6 +1304,17 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(int64_t M, int64_t N, int
   }
 }
 
+#define SVLA_GEMM4_KERNEL(LA_, LB_)                                                                      \
+  __global__ __launch_bounds__(256, 1) void gemm4_kernel_##LA_##LB_(                                     \
+      int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) { \
+    gemm4_body<LA_, LB_>(M, N, K, A, B, Cd, E, sk);                                                      \
+  }
+SVLA_GEMM4_KERNEL(0, 0)
+SVLA_GEMM4_KERNEL(0, 1)
+SVLA_GEMM4_KERNEL(1, 0)
+SVLA_GEMM4_KERNEL(1, 1)
+#undef SVLA_GEMM4_KERNEL
+
 template <auto KERN>
 void set_lds_once(int bytes) {
   static bool done = false;
@@ -1276,8 +1343,9 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   return svla::check_launch("gemm");
 }
 
-// main-loop variant of the 256x256 tile (A/B tuning knob): 0 = 8-phase + stream-K, 1 = 2-barrier kernel,
-// 2 = 8-phase without stream-K
+// main-loop choice for the 256x256 tile (A/B tuning knob): 0 = auto (4-wave kernel for long-K GEMMs with more
+// than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
+// without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel
 int g_variant = 0;
 
 struct SKWorkspace {
@@ -1318,7 +1386,7 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;  // last wave nearly full: nothing to balance
   const size_t need = sk_workspace_bytes(G);
-  if (g_variant == 0 && g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
+  if ((g_variant == 0 || g_variant >= 3) && g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
       sk_tiles * sk.nk >= 8 * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
@@ -1362,8 +1430,23 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     sk.slabs = reinterpret_cast<float*>(g_ws.ptr);
     sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(g_ws.ptr) + (size_t)2 * G * 32 * p8::NTH * 16);
   }
-  set_lds_once<gemm4_kernel>(p4::LDS);
-  hipLaunchKernelGGL(gemm4_kernel, dim3((unsigned)sk.grid), dim3(p4::NTH), p4::LDS, s, M, N, K, A, B, Cd, E, sk);
+  dim3 grid((unsigned)sk.grid), block(p4::NTH);
+#define SVLA_LAUNCH4(LA_, LB_)                                                                       \
+  {                                                                                                  \
+    static bool lds_set = false;                                                                     \
+    if (!lds_set) {                                                                                  \
+      (void)hipFuncSetAttribute((const void*)gemm4_kernel_##LA_##LB_, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                p4::LDS);                                                            \
+      lds_set = true;                                                                                \
+    }                                                                                                \
+    hipLaunchKernelGGL(gemm4_kernel_##LA_##LB_, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);   \
+  }
+  const int la = A.layout, lb = B.layout;
+  if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(0, 0)
+  else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH4(0, 1)
+  else if (la == SVLA_LAYOUT_RC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(1, 0)
+  else SVLA_LAUNCH4(1, 1)
+#undef SVLA_LAUNCH4
   return svla::check_launch("gemm4");
 }
 
@@ -1484,16 +1567,20 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   };
   const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
   const int64_t nk = (K + BK - 1) / BK;
-  const bool sk_ok = g_variant == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  const bool sk_ok = (g_variant == 0 || g_variant >= 3) && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  // 4-wave kernel: measured ahead of the 8-phase one (every operand layout) once the k-loop is long enough to
+  // amortise its tile prologue/epilogue and the grid has more than a wave of tiles (tools/gemm_bench.py,
+  // SVLA_VARIANTS=4,3); behind it on short-K or sub-wave shapes (SigLIP, qkv wgrad, o dgrad)
+  const int64_t t256 = tiles(256, 256);
+  const bool use4 = !kseg && seg_ok(256, 256) &&
+                    (g_variant == 3 || (g_variant == 0 && K >= 2048 && t256 >= num_cus() && (t256 >= 512 || K >= 4096)));
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
+    if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);
     if (g_variant != 1 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
     return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   }
-  const bool kckc = A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC;
-  if (g_variant == 3 && kckc && !kseg && seg_ok(256, 256) &&
-      (tiles(256, 256) >= 512 || (g_ws.ptr && tiles(256, 256) * nk >= 8 * num_cus())))
-    return launch4(M, N, K, *A, *B, C, *epi, s);
+  if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);
   if (g_variant != 1 && !kseg && seg_ok(256, 256) &&
       (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
     return launch8(M, N, K, *A, *B, C, *epi, s);

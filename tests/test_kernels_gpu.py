@@ -40,13 +40,14 @@ def test_gemm_layouts(cuda, M, N, K, layouts):
 
 
 def _variants(fn):
-    """Run fn() under the 256x256 main-loop variants: 1 = 2-barrier, 2 = 8-phase, 0 = 8-phase + stream-K
-    (twice).  Returns {variant: result}."""
+    """Run fn() under the 256x256 main-loop variants: 1 = 2-barrier, 2 = 8-phase, 0 = product dispatch
+    (twice), 3 = 4-wave kernel wherever both operands are KC (twice), 4 = 8-phase + stream-K.
+    Returns {variant: result}."""
     from spatialvla_amd import _lib as L
     outs = {}
     try:
-        for v in (1, 2, 0, "0b"):
-            L.lib().svla_gemm_set_variant(0 if v == "0b" else v)
+        for v in (1, 2, 0, "0b", 3, "3b", 4):
+            L.lib().svla_gemm_set_variant({"0b": 0, "3b": 3}.get(v, v))
             outs[v] = fn()
             torch.cuda.synchronize()
     finally:
@@ -66,7 +67,10 @@ def _check_variants(outs, tol=2e-3):
         assert torch.equal(a, b)
     for a, b in zip(f(0), f("0b")):
         assert torch.equal(a, b)
-    assert rel_l2(_flat(outs[0]), _flat(outs[1])) < tol
+    for a, b in zip(f(3), f("3b")):
+        assert torch.equal(a, b)
+    for v in (0, 3, 4):
+        assert rel_l2(_flat(outs[v]), _flat(outs[1])) < tol, v
 
 
 @pytest.mark.parametrize("M,N,K", [(2000, 16500, 200), (2304, 14336, 1000), (4100, 8200, 64), (9984, 2304, 2048),
@@ -427,6 +431,15 @@ def test_gemm_rope_epilogue(cuda, D, Hq, Hkv, L):
     ref = plain.clone()
     ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
     assert torch.equal(rot, ref)
+    if D == 256:  # the same through the 4-wave kernel (same k order per output: bitwise equal)
+        try:
+            L_.lib().svla_gemm_set_variant(3)
+            rot4 = torch.empty_like(plain)
+            Kn.linear_fwd(x, [w], rot4, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
+            torch.cuda.synchronize()
+        finally:
+            L_.lib().svla_gemm_set_variant(0)
+        assert torch.equal(rot4, ref)
 
 
 def test_gemma2_attention_plugin_signature(cuda):

@@ -19,7 +19,9 @@ import shutil
 import sys
 
 M, I, H = 32 * 312, 9216, 2304
-DOM_GRID = ((M + 255) // 256) * ((2 * I + 255) // 256) * 512
+DOM_TILES = ((M + 255) // 256) * ((2 * I + 255) // 256)
+DOM_GRID = DOM_TILES * 512  # 8-wave kernel; the 4-wave kernel launches DOM_TILES * 256 threads
+DOM_GRIDS = (DOM_TILES * 512, DOM_TILES * 256)
 
 
 def _find(d, suffix):
@@ -36,7 +38,7 @@ def _key(n):
 
 
 def _is_dom(r):
-    return re.search(r"gemm8?_kernel", r["Kernel_Name"]) is not None and int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) == DOM_GRID
+    return re.search(r"gemm[48]?_kernel", r["Kernel_Name"]) is not None and int(r["Grid_Size_X"]) * int(r.get("Grid_Size_Y", 1) or 1) in DOM_GRIDS
 
 
 def trace(d, out):
@@ -77,7 +79,7 @@ def pmc(d, out):
     gcol = "Grid_Size" if "Grid_Size" in cols else "Grid_Size_X"
     per = collections.defaultdict(dict)
     for r in rows:
-        if re.search(r"gemm8?_kernel", r["Kernel_Name"]) is None or int(float(r[gcol])) != DOM_GRID:
+        if re.search(r"gemm[48]?_kernel", r["Kernel_Name"]) is None or int(float(r[gcol])) not in DOM_GRIDS:
             continue
         per[r.get("Dispatch_Id", r.get("Correlation_Id"))][r["Counter_Name"]] = float(r["Counter_Value"])
     vals = collections.defaultdict(list)
