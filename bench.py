@@ -236,7 +236,12 @@ def main():
     geglu_events = K.launch_timer["geglu"] = []
     t_start = time.perf_counter()
     for s in range(args.steps):
+        if s == args.steps - 1 and os.environ.get("SVLA_GEMM_LOG"):  # tools/ab_trace.py: GEMM call sequence
+            K.gemm_log = []
         losses.append(engine.train_step(batches[args.warmup + s]))
+    if K.gemm_log is not None:
+        json.dump(K.gemm_log, open(os.environ["SVLA_GEMM_LOG"], "w"))
+        K.gemm_log = None
     torch.cuda.synchronize()
     K.launch_timer.pop("geglu")
     if world > 1:

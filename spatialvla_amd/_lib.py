@@ -112,6 +112,9 @@ def lib() -> ctypes.CDLL:
         with _lock:
             if _lib is None:
                 _lib = load()
+                v = os.environ.get("SVLA_GEMM_VARIANT")  # A/B knob of the 256x256 GEMM main loop (gemm.hip)
+                if v:
+                    _lib.svla_gemm_set_variant(int(v))
     return _lib
 
 

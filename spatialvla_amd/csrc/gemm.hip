@@ -1568,12 +1568,15 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
   const int64_t nk = (K + BK - 1) / BK;
   const bool sk_ok = (g_variant == 0 || g_variant >= 3) && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
-  // 4-wave kernel: measured ahead of the 8-phase one (every operand layout) once the k-loop is long enough to
-  // amortise its tile prologue/epilogue and the grid has more than a wave of tiles (tools/gemm_bench.py,
-  // SVLA_VARIANTS=4,3); behind it on short-K or sub-wave shapes (SigLIP, qkv wgrad, o dgrad)
+  // 4-wave kernel: ahead of the 8-phase one in the training step (tools/ab_prof.sh: kernel traces of bench.py
+  // paired per call) once the k-loop is long enough to amortise its tile prologue/epilogue, the grid has more
+  // than a wave of tiles and the epilogue is light -- it runs the epilogue on half the waves, so GEGLU-backward
+  // (+31%), softcap-CE (+9%) and RoPE (+2%) stay on the 8-wave kernel, as do short-K / sub-wave shapes
   const int64_t t256 = tiles(256, 256);
+  const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (g_variant == 3 || (g_variant == 0 && K >= 2048 && t256 >= num_cus() && (t256 >= 512 || K >= 4096)));
+                    (g_variant == 3 || (g_variant == 0 && light_epi && K >= 2048 && t256 >= num_cus() &&
+                                        (t256 >= 512 || K >= 4096)));
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
     if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);

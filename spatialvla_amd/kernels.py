@@ -96,10 +96,15 @@ def _ensure_gemm_workspace():
         _gemm_ws[dev] = buf
 
 
+gemm_log: Optional[list] = None  # tools: when a list, every svla_gemm_bf16 call appends its shape/layouts/epilogue
+
+
 def gemm(M: int, N: int, K: int, A: L.Operand, B: L.Operand, c_mats: Sequence[Optional[torch.Tensor]],
          c_starts: Sequence[int], ldc: int, epi: L.Epilogue):
     if not _gemm_ws:
         _ensure_gemm_workspace()
+    if gemm_log is not None:
+        gemm_log.append((M, N, K, int(A.layout), int(B.layout), int(epi.kind), int(epi.accumulate)))
     n = len(c_mats)
     cp = (ctypes.c_void_p * 4)(*([_ptr(c) for c in c_mats] + [None] * (4 - n)))
     cs = (ctypes.c_int64 * 5)(*([int(s) for s in c_starts] + [0] * (5 - n)))
