@@ -274,6 +274,32 @@ def test_gemm_softcap_ce(cuda):
     assert d[:, V:].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("M,H,V,every", [(300, 256, 1000, 7), (9984 // 8, 2304, 4099, 24), (64, 128, 300, 0)])
+def test_lm_head_ce_fn_label_rows(cuda, M, H, V, every):
+    """LMHeadCEFn's backward runs the softmax gradient and both lm_head GEMMs over the labelled rows only;
+    dh / dW must equal the dense fp32 reference (softcap 30, CE with ignored rows) -- including no label at
+    all (every=0: zero gradients)."""
+    from spatialvla_amd import functional as Fn, _lib as L
+    torch.manual_seed(12)
+    h = _r(M, H).requires_grad_(True)
+    w = _r(V, H, scale=0.2).requires_grad_(True)
+    tgt = torch.full((M,), -100, dtype=torch.int64, device=cuda)
+    if every:
+        tgt[::every] = torch.randint(0, V, (len(range(0, M, every)),), device=cuda)
+    stash = {}
+    logits, loss = Fn.LMHeadCEFn.apply(h, w, tgt, 30.0, stash)
+    loss.backward()
+    hf, wf = h.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    y = 30.0 * torch.tanh(hf @ wf.T / 30.0)
+    valid = tgt >= 0
+    if every:
+        F.cross_entropy(y[valid], tgt[valid]).backward()
+        assert rel_l2(h.grad, hf.grad) < 2e-2 and rel_l2(w.grad, wf.grad) < 2e-2
+        assert h.grad[~valid].abs().sum().item() == 0
+    else:
+        assert h.grad.abs().sum().item() == 0 and w.grad.abs().sum().item() == 0
+
+
 # ------------------------------------------------------------------------------------------ norms
 def test_rmsnorm(cuda):
     from spatialvla_amd import kernels as Kn
