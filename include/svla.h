@@ -243,6 +243,13 @@ int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float
  * element strides (b, c, y, x) / (b, y, x) (channel stride 1 = channels-last, 16-B aligned).  params fp32:
  * W1^T [CF+1+CE][Hid], W2 [4][Hid], b1 [Hid], b2 [4], log_binom(NBins-1, k) [NBins] (as the reference computes
  * it).  out [B, H, W] fp32.  Built for NBins = 64, Hid = 80, CF and CE multiples of 8. */
+/* Bilinear resize of a channels-last bf16 map [B, H1, W1, C] -> [B, H2, W2, C] with torch's
+ * upsample_bilinear2d semantics (transformers ZoeDepthFeatureFusionLayer.forward interpolate(scale_factor=2,
+ * align_corners=True) and the relative head's nn.Upsample, called from modeling_spatialvla.py:317-323's Zoe
+ * forward).  rh/rw = torch's area_pixel_compute_scale: (in-1)/(out-1) with align_corners, else 1/scale_factor or
+ * in/out.  C multiple of 8, 16-B aligned buffers. */
+int svla_upsample_bilinear_nhwc(int B, int C, int H1, int W1, int H2, int W2, int align_corners, float rh, float rw,
+                                const void* in, void* out, void* stream);
 int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
                          const void* feat, const int64_t* feat_strides, const void* rel, const int64_t* rel_strides,
                          const void* emb, const int64_t* emb_strides, const void* ctr, const int64_t* ctr_strides,

@@ -205,6 +205,64 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   a.out[pix] = acc / se;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Bilinear resize of a channels-last bf16 map (torch upsample_bilinear2d_nhwc_out_frame semantics, used by the
+// ZoeDepth DPT neck: ZoeDepthFeatureFusionLayer's interpolate(scale_factor=2, align_corners=True) and the
+// relative head's nn.Upsample).  One thread = one output pixel x 8 channels (four 16-B loads, one 16-B store)
+// instead of torch's one element per thread; source index, lambdas and the blend in fp32 in torch's order.
+struct UpsArgs {
+  int B, C, H1, W1, H2, W2, align;
+  float rh, rw;
+  const bf16_t* in;
+  bf16_t* out;
+};
+
+__device__ __forceinline__ float ups_src(float scale, int dst, int align) {
+  if (align) return scale * (float)dst;
+  const float src = scale * ((float)dst + 0.5f) - 0.5f;
+  return src < 0.f ? 0.f : src;
+}
+
+__global__ __launch_bounds__(256) void upsample_bilinear_nhwc_kernel(UpsArgs a) {
+  const int cg = a.C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.H2 * a.W2 * cg;
+  if (idx >= total) return;
+  const int c8 = (int)(idx % cg);
+  int64_t r = idx / cg;
+  const int w2 = (int)(r % a.W2);
+  r /= a.W2;
+  const int h2 = (int)(r % a.H2);
+  const int n = (int)(r / a.H2);
+  const float h1r = ups_src(a.rh, h2, a.align);
+  const int h1 = (int)h1r;
+  const int h1p = (h1 < a.H1 - 1) ? 1 : 0;
+  const float h1lambda = h1r - (float)h1;
+  const float h0lambda = 1.f - h1lambda;
+  const float w1r = ups_src(a.rw, w2, a.align);
+  const int w1 = (int)w1r;
+  const int w1p = (w1 < a.W1 - 1) ? 1 : 0;
+  const float w1lambda = w1r - (float)w1;
+  const float w0lambda = 1.f - w1lambda;
+  const int64_t rowb = (int64_t)n * a.H1;
+  auto at = [&](int y, int x) {
+    return *reinterpret_cast<const u32x4*>(a.in + ((rowb + y) * a.W1 + x) * a.C + 8 * c8);
+  };
+  float p00[8], p01[8], p10[8], p11[8], o[8];
+  unpack8(at(h1, w1), p00);
+  unpack8(at(h1, w1 + w1p), p01);
+  unpack8(at(h1 + h1p, w1), p10);
+  unpack8(at(h1 + h1p, w1 + w1p), p11);
+  // torch's expression as hipcc contracts it (the one ordering found bitwise-equal to the stock NHWC kernel
+  // on MI355X, tools/ups_variants.py): fma over the w-pairs, then over the h-pair
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float t0 = fmaf(w0lambda, p00[j], w1lambda * p01[j]), t1 = fmaf(w0lambda, p10[j], w1lambda * p11[j]);
+    o[j] = fmaf(h0lambda, t0, h1lambda * t1);
+  }
+  *reinterpret_cast<u32x4*>(a.out + (((int64_t)n * a.H2 + h2) * a.W2 + w2) * a.C + 8 * c8) = pack8(o);
+}
+
 }  // namespace
 
 extern "C" int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
@@ -231,4 +289,19 @@ extern "C" int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, i
   hipLaunchKernelGGL(zoe_tail_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
                      params);
   return svla::check_launch("zoe_metric_tail");
+}
+
+extern "C" int svla_upsample_bilinear_nhwc(int B, int C, int H1, int W1, int H2, int W2, int align_corners,
+                                           float rh, float rw, const void* in, void* out, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && C > 0 && H1 > 0 && W1 > 0 && H2 > 0 && W2 > 0, "upsample: bad sizes");
+  SVLA_CHECK_ARG(C % 8 == 0, "upsample: channel count must be a multiple of 8 (got %d)", C);
+  SVLA_CHECK_ARG(in && out && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0,
+                 "upsample: NULL or misaligned pointer");
+  UpsArgs a;
+  a.B = B; a.C = C; a.H1 = H1; a.W1 = W1; a.H2 = H2; a.W2 = W2; a.align = align_corners ? 1 : 0;
+  a.rh = rh; a.rw = rw; a.in = (const bf16_t*)in; a.out = (bf16_t*)out;
+  const int64_t total = (int64_t)B * H2 * W2 * (C / 8);
+  hipLaunchKernelGGL(upsample_bilinear_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return svla::check_launch("upsample_bilinear_nhwc");
 }

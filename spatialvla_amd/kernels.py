@@ -439,3 +439,31 @@ def zoe_metric_tail(clb, feat, rel, emb, ctr):
                                          prm.data_ptr(), float(clb.p_eps), float(clb.max_temp), float(clb.min_temp),
                                          1e-4, out.data_ptr(), _stream()), "zoe_metric_tail")
     return out
+
+
+# ---------------------------------------------------------------------------------------- Zoe DPT neck resize
+def upsample_bilinear_cl(x: torch.Tensor, size=None, scale_factor=None, align_corners: bool = False):
+    """torch.nn.functional.interpolate(x, size / scale_factor, mode="bilinear", align_corners) for a channels-last
+    bf16 [B, C, H, W] map (C % 8 == 0) through svla_upsample_bilinear_nhwc; returns a channels-last tensor.
+    Scales follow torch's area_pixel_compute_scale (recompute_scale_factor unset)."""
+    B, C, H1, W1 = x.shape
+    _req(x.dtype == torch.bfloat16 and x.is_cuda and C % 8 == 0, "upsample_bilinear_cl: bf16 CUDA map, C % 8 == 0")
+    _req(x.is_contiguous(memory_format=torch.channels_last), "upsample_bilinear_cl: input must be channels-last")
+    if size is None:
+        sf = scale_factor if isinstance(scale_factor, (tuple, list)) else (scale_factor, scale_factor)
+        H2, W2 = int(math.floor(H1 * float(sf[0]))), int(math.floor(W1 * float(sf[1])))
+    else:
+        H2, W2 = (size, size) if isinstance(size, int) else (int(size[0]), int(size[1]))
+        sf = None
+
+    def scale(i, o, s):  # torch area_pixel_compute_scale<float>: float divisions, 1/scale in double then float
+        import numpy as np
+        if align_corners:
+            return float(np.float32(i - 1) / np.float32(o - 1)) if o > 1 else 0.0
+        return float(np.float32(1.0 / float(s))) if s is not None and float(s) > 0 else float(np.float32(i) / np.float32(o))
+    rh = scale(H1, H2, sf[0] if sf is not None else None)
+    rw = scale(W1, W2, sf[1] if sf is not None else None)
+    out = torch.empty(B, C, H2, W2, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    L.check(L.lib().svla_upsample_bilinear_nhwc(B, C, H1, W1, H2, W2, int(bool(align_corners)), float(rh), float(rw),
+                                                x.data_ptr(), out.data_ptr(), _stream()), "upsample_bilinear_nhwc")
+    return out

@@ -8,6 +8,9 @@ by the reference at model/modeling_spatialvla.py:314-323).  Installed per instan
 * Conditional log-binomial head (ZoeDepthConditionalLogBinomialSoftmax.forward): the channel concat of the
   contiguous main feature with the channels-last interpolated bin embedding runs as a mixed-layout copy
   (~10 ms at B=32, 384x384).  Concatenating after one explicit NCHW copy gives the same tensor.
+* DPT neck resizes (ZoeDepthFeatureFusionLayer's interpolate(scale_factor=2, align_corners=True) and the relative
+  head's nn.Upsample) on channels-last bf16 maps: svla_upsample_bilinear_nhwc (csrc/zoe.hip), torch's NHWC bilinear
+  arithmetic at 8 channels per thread instead of one element (the stock kernel moved ~0.5 TB/s).
 * Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
   relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
   and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
@@ -66,6 +69,37 @@ def _metric_head_forward(self, outconv_activation, bottleneck, feature_blocks, r
                              bin_centers), None
 
 
+def _interp(x, size=None, scale_factor=None, mode="bilinear", align_corners=None):
+    """nn.functional.interpolate for the DPT neck: channels-last bf16 maps go through the HIP resize kernel
+    (svla_upsample_bilinear_nhwc, torch's NHWC bilinear arithmetic, 8 channels per thread); anything else
+    keeps the stock op."""
+    if (mode == "bilinear" and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()):
+        from . import kernels as K
+        return K.upsample_bilinear_cl(x, size=size, scale_factor=scale_factor, align_corners=bool(align_corners))
+    return torch.nn.functional.interpolate(x, size=size, scale_factor=scale_factor, mode=mode,
+                                           align_corners=align_corners)
+
+
+def _fusion_forward(self, hidden_state, residual=None):
+    """ZoeDepthFeatureFusionLayer.forward (transformers zoedepth / dpt [3p]) with the resize on the HIP kernel."""
+    if residual is not None:
+        if hidden_state.shape != residual.shape:
+            residual = _interp(residual, size=(hidden_state.shape[2], hidden_state.shape[3]), mode="bilinear",
+                               align_corners=False)
+        hidden_state = hidden_state + self.residual_layer1(residual)
+    hidden_state = self.residual_layer2(hidden_state)
+    hidden_state = _interp(hidden_state, scale_factor=2, mode="bilinear", align_corners=self.align_corners)
+    return self.projection(hidden_state)
+
+
+def _upsample_forward(self, x):
+    """nn.Upsample(scale_factor, mode="bilinear", align_corners) of the relative-depth head."""
+    if self.size is None and self.recompute_scale_factor is None:
+        return _interp(x, scale_factor=self.scale_factor, mode=self.mode, align_corners=self.align_corners)
+    return type(self).forward(self, x)
+
+
 def install(zoe: torch.nn.Module, tail: bool = True) -> torch.nn.Module:
     """Patch the instances inside `zoe` (idempotent).  tail=False keeps the stock metric-head tail (the other
     two paths are bitwise identical to the stock module)."""
@@ -76,6 +110,12 @@ def install(zoe: torch.nn.Module, tail: bool = True) -> torch.nn.Module:
             m._svla_fast = True
         elif name == "ZoeDepthConditionalLogBinomialSoftmax" and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_logbinomial_forward, m)
+            m._svla_fast = True
+        elif name == "ZoeDepthFeatureFusionLayer" and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_fusion_forward, m)
+            m._svla_fast = True
+        elif (isinstance(m, torch.nn.Upsample) and m.mode == "bilinear" and not getattr(m, "_svla_fast", False)):
+            m.forward = types.MethodType(_upsample_forward, m)
             m._svla_fast = True
         elif name == "ZoeDepthMetricDepthEstimationHead" and tail and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_metric_head_forward, m)

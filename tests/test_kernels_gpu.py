@@ -552,3 +552,20 @@ def test_adamw_and_norm(cuda):
     Kn.adamw(master, pb, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, 1, clip)
     assert torch.allclose(master, ref_p.detach(), atol=1e-6, rtol=1e-5)
     assert torch.equal(pb, master.to(BF))
+
+
+@pytest.mark.parametrize("B,C,H,W,kw", [(2, 256, 24, 24, dict(scale_factor=2, align_corners=True)),
+                                        (2, 128, 192, 192, dict(scale_factor=2, align_corners=True)),
+                                        (3, 64, 17, 30, dict(size=(40, 33), align_corners=True)),
+                                        (2, 32, 12, 20, dict(size=(24, 31), align_corners=False)),
+                                        (1, 16, 9, 9, dict(scale_factor=2, align_corners=False))])
+def test_upsample_bilinear_channels_last(cuda, B, C, H, W, kw):
+    """svla_upsample_bilinear_nhwc reproduces torch's bilinear interpolate on channels-last bf16 maps bitwise
+    (the ZoeDepth DPT neck resizes it replaces)."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(13)
+    x = torch.randn(B, C, H, W, device=cuda).to(BF).contiguous(memory_format=torch.channels_last)
+    ref = F.interpolate(x, mode="bilinear", **kw)
+    out = Kn.upsample_bilinear_cl(x, **kw)
+    assert out.shape == ref.shape
+    assert torch.equal(out, ref)
