@@ -181,23 +181,37 @@ __global__ void add_kernel(int64_t n, const bf16_t* __restrict__ a, const bf16_t
 }
 
 // ------------------------------------------------------------------ softcapped CE
-__global__ void ce_finalize_kernel(int64_t M, int64_t N, int64_t ntiles, const float* __restrict__ rs,
-                                   const bf16_t* __restrict__ logits, int64_t ldl, const int64_t* __restrict__ target,
-                                   float* __restrict__ lse, int64_t* __restrict__ argmax, float* __restrict__ loss_rows) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// merge two online-softmax partials (max, sum of exp, argmax; ties to the smaller column)
+__device__ __forceinline__ void ce_merge(float& mx, float& se, int& am, float m2, float s2, int a2) {
+  if (m2 == -INFINITY) return;
+  const float mn = fmaxf(mx, m2);
+  se = (mx == -INFINITY ? 0.f : se * __expf(mx - mn)) + s2 * __expf(m2 - mn);
+  if (m2 > mx || (m2 == mx && a2 < am)) am = a2;
+  mx = mn;
+}
+
+// one wave per row: lanes stride over the row's 128-column partials (coalesced 12-B records), then a fixed
+// butterfly merge -- deterministic, and every CU busy (a thread per row left the GPU on 39 CUs)
+__global__ __launch_bounds__(256) void ce_finalize_kernel(int64_t M, int64_t N, int64_t ntiles,
+                                                          const float* __restrict__ rs,
+                                                          const bf16_t* __restrict__ logits, int64_t ldl,
+                                                          const int64_t* __restrict__ target, float* __restrict__ lse,
+                                                          int64_t* __restrict__ argmax, float* __restrict__ loss_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
   float mx = -INFINITY, se = 0.f;
   int am = 0x7fffffff;
-  for (int64_t t = 0; t < ntiles; ++t) {
-    const float* p = rs + (m * ntiles + t) * 3;
-    const float m2 = p[0], s2 = p[1];
-    const int a2 = __float_as_int(p[2]);
-    if (m2 == -INFINITY) continue;
-    const float mn = fmaxf(mx, m2);
-    se = (mx == -INFINITY ? 0.f : se * __expf(mx - mn)) + s2 * __expf(m2 - mn);
-    if (m2 > mx || (m2 == mx && a2 < am)) am = a2;
-    mx = mn;
+  const float* row = rs + m * ntiles * 3;
+  for (int64_t t = lane; t < ntiles; t += 64)
+    ce_merge(mx, se, am, row[t * 3], row[t * 3 + 1], __float_as_int(row[t * 3 + 2]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(se, o, 64);
+    const int a2 = __shfl_xor(am, o, 64);
+    ce_merge(mx, se, am, m2, s2, a2);
   }
+  if (lane != 0) return;
   const float l = mx + __logf(se);
   lse[m] = l;
   argmax[m] = am;
@@ -431,7 +445,7 @@ extern "C" int svla_ce_finalize(int64_t M, int64_t N, int64_t ntiles, const floa
                                 float* loss_out, void* stream) {
   SVLA_CHECK_ARG(M > 0 && N > 0 && row_stats && logits && lse && argmax && loss_rows && loss_out, "ce_finalize: args");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(ce_finalize_kernel, dim3(nblk(M, 256)), dim3(256), 0, s, M, N, ntiles, row_stats,
+  hipLaunchKernelGGL(ce_finalize_kernel, dim3(nblk(M, 4)), dim3(256), 0, s, M, N, ntiles, row_stats,
                      (const bf16_t*)logits, ldl, target, lse, argmax, loss_rows);
   if (int rc = svla::check_launch("ce_finalize")) return rc;
   hipLaunchKernelGGL(ce_loss_kernel, dim3(1), dim3(1024), 0, s, M, loss_rows, target, loss_out);
