@@ -203,6 +203,10 @@ int svla_affine_bf16(int64_t n, const void* x, float scale, float offset, void* 
 int svla_relu_fwd(int64_t n, const void* x, void* y, void* stream);
 int svla_relu_bwd(int64_t n, const void* x, const void* dy, void* dx, void* stream);
 /* out = bf16(a + b) */
+/* GeGLU backward of Gemma2MLP (modeling_gemma2.py:91-92): dg = bf16(dh*u)*gelu_tanh'(g), du = dh*bf16(gelu_tanh(g))
+ * over [M, I] bf16 rows with leading dimensions (I % 8 == 0, 16-B aligned rows); dg may alias dh. */
+int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg, const void* u,
+                   int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* stream);
 int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------

@@ -1576,7 +1576,8 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
   const bool use4 = !kseg && seg_ok(256, 256) &&
                     (g_variant == 3 || (g_variant == 0 && light_epi && K >= 2048 && t256 >= num_cus() &&
-                                        (t256 >= 512 || K >= 4096)));
+                                        (t256 >= 512 || K >= 4096) &&
+                                        (B->layout == SVLA_LAYOUT_KC || K >= 4096)));  // short-K x RC B: +4%
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
     if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);

@@ -164,6 +164,32 @@ __global__ void relu_bwd_kernel(int64_t n, const bf16_t* __restrict__ x, const b
   if (i >= n) return;
   for (int64_t j = i; j < min(n, i + 8); ++j) dx[j] = bf2f(x[j]) > 0.f ? dy[j] : (bf16_t)0;
 }
+// GeGLU backward (Gemma2MLP, modeling_gemma2.py:91-92, autograd of gelu_tanh(g) * u): dg = bf16(dh*u) * gelu'(g),
+// du = dh * bf16(gelu(g)) with the reference's bf16 rounding points (the GEGLU_BWD GEMM epilogue's arithmetic).
+// 8 columns per thread; dh may alias dg (each element is read before it is written).
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, const bf16_t* dh, int64_t ldh,
+                                                        const bf16_t* __restrict__ g, int64_t ldg,
+                                                        const bf16_t* __restrict__ u, int64_t ldu, bf16_t* dg,
+                                                        int64_t lddg, bf16_t* __restrict__ du, int64_t lddu) {
+  const int64_t cpr = I / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * cpr) return;
+  const int64_t m = idx / cpr, c = (idx % cpr) * 8;
+  float d[8], gv[8], uv[8], og[8], ou[8];
+  unpack8(*reinterpret_cast<const u32x4*>(dh + m * ldh + c), d);
+  unpack8(*reinterpret_cast<const u32x4*>(g + m * ldg + c), gv);
+  unpack8(*reinterpret_cast<const u32x4*>(u + m * ldu + c), uv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float act = round_bf(gelu_tanh(gv[j]));
+    const float dact = round_bf(d[j] * uv[j]);
+    ou[j] = d[j] * act;
+    og[j] = dact * gelu_tanh_grad(gv[j]);
+  }
+  *reinterpret_cast<u32x4*>(dg + m * lddg + c) = pack8(og);
+  *reinterpret_cast<u32x4*>(du + m * lddu + c) = pack8(ou);
+}
+
 __global__ void add_kernel(int64_t n, const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
                            bf16_t* __restrict__ y) {
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
@@ -490,4 +516,17 @@ extern "C" int svla_adamw(int64_t n, float* master, void* param_bf16, const void
   hipLaunchKernelGGL(adamw_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n, master, (bf16_t*)param_bf16,
                      (const bf16_t*)grad_bf16, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, clip_scale);
   return svla::check_launch("adamw");
+}
+
+extern "C" int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg,
+                              const void* u, int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu,
+                              void* stream) {
+  SVLA_CHECK_ARG(M > 0 && I > 0 && I % 8 == 0 && dh && g && u && dg && du, "geglu_bwd: bad args");
+  SVLA_CHECK_ARG(ldh % 8 == 0 && ldg % 8 == 0 && ldu % 8 == 0 && lddg % 8 == 0 && lddu % 8 == 0 && al16(dh) &&
+                     al16(g) && al16(u) && al16(dg) && al16(du),
+                 "geglu_bwd: rows must be 16-B aligned");
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(nblk(M * (I / 8), 256)), dim3(256), 0, (hipStream_t)stream, M, I,
+                     (const bf16_t*)dh, ldh, (const bf16_t*)g, ldg, (const bf16_t*)u, ldu, (bf16_t*)dg, lddg,
+                     (bf16_t*)du, lddu);
+  return svla::check_launch("geglu_bwd");
 }

@@ -467,3 +467,13 @@ def upsample_bilinear_cl(x: torch.Tensor, size=None, scale_factor=None, align_co
     L.check(L.lib().svla_upsample_bilinear_nhwc(B, C, H1, W1, H2, W2, int(bool(align_corners)), float(rh), float(rw),
                                                 x.data_ptr(), out.data_ptr(), _stream()), "upsample_bilinear_nhwc")
     return out
+
+
+def geglu_bwd(dh: torch.Tensor, g: torch.Tensor, u: torch.Tensor, dg: torch.Tensor, du: torch.Tensor):
+    """svla_geglu_bwd over [M, I] row-strided bf16 views (dg may be dh itself)."""
+    M, I = g.shape
+    for t in (dh, g, u, dg, du):
+        _req(t.shape == (M, I) and t.dtype == torch.bfloat16 and t.stride(1) == 1, "geglu_bwd: [M, I] bf16 rows")
+    L.check(L.lib().svla_geglu_bwd(M, I, dh.data_ptr(), dh.stride(0), g.data_ptr(), g.stride(0), u.data_ptr(),
+                                   u.stride(0), dg.data_ptr(), dg.stride(0), du.data_ptr(), du.stride(0), _stream()),
+            "geglu_bwd")

@@ -569,3 +569,31 @@ def test_upsample_bilinear_channels_last(cuda, B, C, H, W, kw):
     out = Kn.upsample_bilinear_cl(x, **kw)
     assert out.shape == ref.shape
     assert torch.equal(out, ref)
+
+
+def test_geglu_bwd_kernel_matches_epilogue(cuda):
+    """svla_geglu_bwd (plain dH GEMM + one elementwise pass, the product path of GemmaMLPFn.backward) is
+    bitwise equal to the GEGLU_BWD GEMM epilogue it replaced (same main loop, no stream-K: variant 2), in place."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(14)
+    M, K, I = 1000, 320, 2048
+    g, u = _r(M, I), _r(M, I)
+    wd, dout = _r(K, I, scale=0.1), _r(M, K)
+    try:
+        L.lib().svla_gemm_set_variant(2)
+        ref = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+        Kn.linear_dgrad(dout, [wd], ref[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=ref[:, :I], out2=ref[:, I:])
+        new = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+        Kn.linear_dgrad(dout, [wd], new[:, :I])
+        Kn.geglu_bwd(new[:, :I], g, u, new[:, :I], new[:, I:])
+        torch.cuda.synchronize()
+    finally:
+        L.lib().svla_gemm_set_variant(0)
+    assert torch.equal(new, ref)
+    dh = (dout.float() @ wd.float()).to(BF).float()
+    gf, uf = g.float(), u.float()
+    act = F.gelu(gf, approximate="tanh")
+    gl = gf.clone().requires_grad_(True)
+    F.gelu(gl, approximate="tanh").backward(torch.ones_like(gl))
+    assert rel_l2(new[:, I:], dh * act) < 1e-2
+    assert rel_l2(new[:, :I], (dh * uf) * gl.grad) < 1e-2
