@@ -128,6 +128,106 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
   }
 }
 
+// ------------------------------------------------------------------ wave-per-row backward (N <= 1536 / 2048)
+// One wave per row (lane l owns 16-B chunks l, l+64, ..): the row reductions are wave shuffles, so the four waves
+// of a block work on four rows at once with no barrier; each block still covers RPB rows and writes one weight-
+// gradient partial row (its four waves' sums combined through LDS in a fixed order).  Per-element arithmetic is
+// that of the block-per-row kernels above.
+constexpr int WCH = 5;  // chunks per lane: rows up to 64*5*8 = 2560 elements
+
+template <bool LN>
+__global__ __launch_bounds__(256) void norm_bwd_wave_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ w, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const bf16_t* __restrict__ dy,
+                                                            const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                            float* __restrict__ partial) {
+  extern __shared__ float sred[];  // [4][N] (LN: [4][2N])
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nch = (int)(N >> 3);
+  float dwacc[WCH][8], dbacc[LN ? WCH : 1][8];
+#pragma unroll
+  for (int c = 0; c < WCH; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dwacc[c][j] = 0.f;
+      if (LN) dbacc[LN ? c : 0][j] = 0.f;
+    }
+  const int64_t r0 = (int64_t)blockIdx.x * RPB;
+  for (int rr = wv; rr < RPB; rr += 4) {
+    const int64_t row = r0 + rr;
+    if (row >= rows) break;
+    const float rs = rstd[row];
+    const float mu = LN ? mean[row] : 0.f;
+    float xh[WCH][8], gv[WCH][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < WCH; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float d[8], wf[8];
+        ld8(x + row * N + ch * 8, xh[c]);
+        ld8(dy + row * N + ch * 8, d);
+        ld8(w + ch * 8, wf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (LN) {
+            xh[c][j] = (xh[c][j] - mu) * rs;
+            gv[c][j] = d[j] * wf[j];
+            s1 += gv[c][j];
+            s2 += gv[c][j] * xh[c][j];
+            dbacc[LN ? c : 0][j] += d[j];
+          } else {
+            xh[c][j] = xh[c][j] * rs;
+            gv[c][j] = d[j] * (1.0f + wf[j]);
+            s2 += gv[c][j] * xh[c][j];
+          }
+          dwacc[c][j] += d[j] * xh[c][j];
+        }
+      }
+    }
+    s2 = wave_sum(s2) / (float)N;
+    if (LN) s1 = wave_sum(s1) / (float)N;
+#pragma unroll
+    for (int c = 0; c < WCH; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = LN ? rs * (gv[c][j] - s1 - xh[c][j] * s2) : rs * (gv[c][j] - xh[c][j] * s2);
+        if (dres) {
+          float r[8];
+          ld8(dres + row * N + ch * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]) + r[j];
+        }
+        st8(dx + row * N + ch * 8, o);
+      }
+    }
+  }
+  // combine the four waves' weight-gradient sums in wave order, one partial row per block
+  const int nv = LN ? 2 : 1;
+#pragma unroll
+  for (int c = 0; c < WCH; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sred[(wv * nv) * N + ch * 8 + j] = dwacc[c][j];
+        if (LN) sred[(wv * nv + 1) * N + ch * 8 + j] = dbacc[LN ? c : 0][j];
+      }
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < nv * N; i += 256) {
+    const int v = (int)(i / N);
+    const int64_t k = i % N;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc += sred[(q * nv + v) * N + k];
+    partial[((int64_t)blockIdx.x * nv + v) * N + k] = acc;
+  }
+}
+
 // ------------------------------------------------------------------ LayerNorm
 __global__ __launch_bounds__(NTH) void ln_fwd_kernel(int64_t N, const bf16_t* __restrict__ x,
                                                      const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
@@ -315,9 +415,16 @@ extern "C" int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const vo
   SVLA_CHECK_ARG(x && w && rstd && dy && dx && dw_partial, "rmsnorm_bwd: null pointer");
   const int64_t nb = (rows + RPB - 1) / RPB;
   if (n_partial) *n_partial = nb;
-  hipLaunchKernelGGL(rms_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
-                     (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
-                     dw_partial);
+  if (N <= 1536) {  // measured: at N = 2304 (5 chunks a lane) the block-per-row kernel is faster (43 vs 58 us)
+    const size_t lds = (size_t)4 * N * sizeof(float);
+    hipLaunchKernelGGL(norm_bwd_wave_kernel<false>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, (const float*)nullptr, rstd, (const bf16_t*)dy,
+                       (const bf16_t*)dres, (bf16_t*)dx, dw_partial);
+  } else {
+    hipLaunchKernelGGL(rms_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                       dw_partial);
+  }
   return svla::check_launch("rmsnorm_bwd");
 }
 
@@ -337,9 +444,16 @@ extern "C" int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const 
   SVLA_CHECK_ARG(x && w && mean && rstd && dy && dx && dwb_partial, "layernorm_bwd: null pointer");
   const int64_t nb = (rows + RPB - 1) / RPB;
   if (n_partial) *n_partial = nb;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
-                     (const bf16_t*)x, (const bf16_t*)w, mean, rstd, (const bf16_t*)dy, (const bf16_t*)dres,
-                     (bf16_t*)dx, dwb_partial);
+  if (N <= 2048) {  // 8N fp32 of LDS must stay within the default 64 KiB dynamic limit
+    const size_t lds = (size_t)8 * N * sizeof(float);
+    hipLaunchKernelGGL(norm_bwd_wave_kernel<true>, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, mean, rstd, (const bf16_t*)dy, (const bf16_t*)dres,
+                       (bf16_t*)dx, dwb_partial);
+  } else {
+    hipLaunchKernelGGL(ln_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, mean, rstd, (const bf16_t*)dy, (const bf16_t*)dres,
+                       (bf16_t*)dx, dwb_partial);
+  }
   return svla::check_launch("layernorm_bwd");
 }
 
