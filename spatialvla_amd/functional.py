@@ -369,13 +369,18 @@ class SiglipAttentionFn(torch.autograd.Function):
         if dx is not None:
             K.linear_dgrad(dqkv, [wq, wk, wv], dx)
         rets = []
-        for i, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv))):
-            dw, accw, retw = _grad_dest(w, nig[2 + 2 * i])
-            seg = _c(dqkv[:, i * Hd:(i + 1) * Hd])
-            if dw is not None:
-                K.linear_wgrad(seg, x, [dw], accumulate=accw)
-            retb = _bias_grad(seg, b, nig[3 + 2 * i])
-            rets += [retw, retb]
+        dws = [_grad_dest(w, nig[2 + 2 * i]) for i, w in enumerate((wq, wk, wv))]
+        if all(d[0] is not None for d in dws) and len({d[1] for d in dws}) == 1:
+            # q, k and v weight gradients in one GEMM (C row segments): three 1152x1152 wgrads launched
+            # separately filled ~20 of the 256 CUs each
+            K.linear_wgrad(dqkv, x, [d[0] for d in dws], accumulate=dws[0][1])
+        else:
+            for i, (dw, accw, _r) in enumerate(dws):
+                if dw is not None:
+                    K.linear_wgrad(_c(dqkv[:, i * Hd:(i + 1) * Hd]), x, [dw], accumulate=accw)
+        for i, b in enumerate((bq, bk, bv)):
+            retb = _bias_grad(dqkv[:, i * Hd:(i + 1) * Hd], b, nig[3 + 2 * i])  # strided view, no copy
+            rets += [dws[i][2], retb]
         return (dx, dout, *rets, ret_wo, ret_bo, None)
 
 
