@@ -16,12 +16,37 @@ Design (one process per GPU, torch.distributed over RCCL/xGMI):
 import math
 from typing import Dict, List, Optional
 
+import re
+
 import torch
 import torch.distributed as dist
 
 from . import kernels as K
 
 BF16 = torch.bfloat16
+
+
+def _group_params(gmod) -> List[torch.nn.Parameter]:
+    """gmod's parameters in registration order, except that the q, k, v projection weights of an attention
+    module sit back to back (q|k|v) ahead of their biases: the flat buffer then holds the fused q|k|v weight as
+    one [3H, H] matrix, so the forward and dgrad GEMMs see one unsegmented operand and the three weight
+    gradients one output (SigLIP registers k, v, q with biases in between)."""
+    named = list(gmod.named_parameters())
+    pmap = dict(named)
+    out, done = [], set()
+    for n, p in named:
+        m = re.match(r"(.*self_attn\.)[qkv]_proj\.(weight|bias)$", n)
+        if m is None:
+            out.append(p)
+            continue
+        pre = m.group(1)
+        if pre in done:
+            continue
+        done.add(pre)
+        for suf in ("q_proj.weight", "k_proj.weight", "v_proj.weight", "q_proj.bias", "k_proj.bias", "v_proj.bias"):
+            if pre + suf in pmap:
+                out.append(pmap[pre + suf])
+    return out
 
 
 def _forward_order(model) -> List[torch.nn.Parameter]:
@@ -37,7 +62,7 @@ def _forward_order(model) -> List[torch.nn.Parameter]:
     vt = model.vision_tower.vision_model
     groups += [vt.post_layernorm] + list(reversed(list(vt.encoder.layers))) + [vt.embeddings]
     for gmod in groups:
-        for p in gmod.parameters():
+        for p in _group_params(gmod):
             if p.requires_grad and id(p) not in seen:
                 seen.add(id(p))
                 order.append(p)

@@ -128,6 +128,17 @@ class ReLUFn(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------------------------ linear
+def _cat_views(ts):
+    """torch.cat of 1-D tensors that already sit back to back in one storage (the engine's flat buffer) as a
+    view; otherwise a copy."""
+    nxt, st = ts[0].data_ptr(), ts[0].untyped_storage().data_ptr()
+    for t in ts:
+        if t.dim() != 1 or not t.is_contiguous() or t.data_ptr() != nxt or t.untyped_storage().data_ptr() != st:
+            return torch.cat(ts)
+        nxt += t.numel() * t.element_size()
+    return torch.as_strided(ts[0], (sum(t.numel() for t in ts),), (1,))
+
+
 def _bias_grad(dy, b, needed):
     db, acc, ret = _grad_dest(b, needed)
     if db is not None:
@@ -333,7 +344,7 @@ class SiglipAttentionFn(torch.autograd.Function):
     def forward(ctx, x, res, wq, bq, wk, bk, wv, bv, wo, bo, cfg: SiglipAttnCfg):
         x, res = _c(x), _c(res)
         M, Hd = x.shape
-        bqkv = torch.cat([bq, bk, bv])
+        bqkv = _cat_views([bq, bk, bv])
         qkv = _empty(M, 3 * Hd, like=x)
         K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_BIAS, bias=bqkv)
         attn = _empty(M, Hd, like=x)
