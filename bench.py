@@ -116,7 +116,7 @@ def dominant_kernel_roofline(records):
             "algorithmic_bytes_per_launch": bytes_alg}
 
 
-def gemma2_block_roofline(model, B, L, device, iters=5):
+def gemma2_block_roofline(model, B, L, device, iters=20):
     """The north-star target: one Gemma2DecoderLayer fwd+bwd at B episodes x L tokens (sandwich norms, QKV+RoPE,
     prefix-LM GQA attention with softcap, o_proj, GeGLU MLP; every dW written), timed in isolation with HIP
     events on the stream the kernels run on.  Algorithmic FLOPs = 3 x fwd matmul FLOPs (SURVEY §8a a14:
@@ -150,11 +150,11 @@ def gemma2_block_roofline(model, B, L, device, iters=5):
         e2.synchronize()
         if it >= 2:
             fwd_ms.append(e0.elapsed_time(e1)); tot_ms.append(e0.elapsed_time(e2))
-    ms = float(np.mean(tot_ms))
+    ms = float(np.median(tot_ms))
     ach = flops / (ms * 1e-3) / 1e12
     return {"what": f"Gemma2DecoderLayer fwd+bwd, B={B} x L={L} (M={B * L} token rows)", "bound": "mfma",
             "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-            "ms_fwd_bwd": round(ms, 3), "ms_fwd": round(float(np.mean(fwd_ms)), 3),
+            "ms_fwd_bwd": round(ms, 3), "ms_fwd": round(float(np.median(fwd_ms)), 3), "iters": iters,
             "algorithmic_flops": flops, "target_frac": 0.40}
 
 

@@ -39,17 +39,37 @@ def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
+class ResidualSlot:
+    """Hand-off of a residual-stream gradient between the two consumers of one tensor: the residual branch
+    (add + post-norm, or a GEMM epilogue's residual input) and the pre-norm that reads the same tensor.  The
+    residual branch's backward always runs first (the pre-norm feeds it), so it parks its gradient here instead
+    of returning it, and the pre-norm's backward adds it inside the norm-backward kernel (dres) -- the sum
+    autograd would otherwise form with a separate elementwise add over the residual stream."""
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+    def put(self, g):
+        self.g = g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
+
+
 # ------------------------------------------------------------------------------------ norms
 class RMSNormFn(torch.autograd.Function):
     """Gemma2RMSNorm.forward (reference model/modeling_gemma2.py:69-74)."""
 
     @staticmethod
-    def forward(ctx, x, w, eps):
+    def forward(ctx, x, w, eps, slot=None):
         x = _c(x)
         y = torch.empty_like(x)
         rstd = _empty(x.shape[0], dtype=F32, like=x)
         K.rmsnorm_fwd(x, w, eps, y, rstd)
         ctx.save_for_backward(x, w, rstd)
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -57,20 +77,22 @@ class RMSNormFn(torch.autograd.Function):
         x, w, rstd = ctx.saved_tensors
         dx = torch.empty_like(x)
         dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[1])
-        K.rmsnorm_bwd(x, w, rstd, _c(dy), None, dx, dw, dw_accumulate=acc)
-        return dx, ret, None
+        dres = ctx.slot.take() if ctx.slot is not None else None
+        K.rmsnorm_bwd(x, w, rstd, _c(dy), None if dres is None else _c(dres), dx, dw, dw_accumulate=acc)
+        return dx, ret, None, None
 
 
 class AddRMSNormFn(torch.autograd.Function):
     """h = res + Gemma2RMSNorm(y)  (decoder-layer sandwich norm + residual, modeling_gemma2.py:489-496)."""
 
     @staticmethod
-    def forward(ctx, res, y, w, eps):
+    def forward(ctx, res, y, w, eps, slot=None):
         res, y = _c(res), _c(y)
         h = torch.empty_like(y)
         rstd = _empty(y.shape[0], dtype=F32, like=y)
         K.add_rmsnorm_fwd(res, y, w, eps, h, rstd)
         ctx.save_for_backward(y, w, rstd)
+        ctx.slot = slot
         return h
 
     @staticmethod
@@ -80,20 +102,24 @@ class AddRMSNormFn(torch.autograd.Function):
         dy = torch.empty_like(y)
         dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[2])
         K.rmsnorm_bwd(y, w, rstd, dh, None, dy, dw, dw_accumulate=acc)
-        return dh, dy, ret, None
+        if ctx.slot is not None:  # the pre-norm reading `res` adds dh in its backward kernel
+            ctx.slot.put(dh)
+            return None, dy, ret, None, None
+        return dh, dy, ret, None, None
 
 
 class LayerNormFn(torch.autograd.Function):
     """nn.LayerNorm (SigLIP layer_norm1/2/post_layernorm [3p]; Ego3D head.1, modeling_spatialvla.py:61)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, eps):
+    def forward(ctx, x, w, b, eps, slot=None):
         x = _c(x)
         y = torch.empty_like(x)
         mean = _empty(x.shape[0], dtype=F32, like=x)
         rstd = _empty(x.shape[0], dtype=F32, like=x)
         K.layernorm_fwd(x, w, b, eps, y, mean, rstd)
         ctx.save_for_backward(x, w, b, mean, rstd)
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -104,8 +130,9 @@ class LayerNormFn(torch.autograd.Function):
         db, accb, retb = _grad_dest(b, ctx.needs_input_grad[2])
         if dw is not None and db is not None and accw != accb:
             raise RuntimeError("LayerNorm weight/bias grads must share accumulate mode")
-        K.layernorm_bwd(x, w, mean, rstd, _c(dy), None, dx, dw, db, accumulate=accw)
-        return dx, retw, retb, None
+        dres = ctx.slot.take() if ctx.slot is not None else None
+        K.layernorm_bwd(x, w, mean, rstd, _c(dy), None if dres is None else _c(dres), dx, dw, db, accumulate=accw)
+        return dx, retw, retb, None, None
 
 
 class ReLUFn(torch.autograd.Function):
@@ -341,7 +368,8 @@ class SiglipAttentionFn(torch.autograd.Function):
     (head_dim 72), out_proj with bias and the residual add fused in its epilogue."""
 
     @staticmethod
-    def forward(ctx, x, res, wq, bq, wk, bk, wv, bv, wo, bo, cfg: SiglipAttnCfg):
+    def forward(ctx, x, res, wq, bq, wk, bk, wv, bv, wo, bo, cfg: SiglipAttnCfg, slot=None):
+        ctx.slot = slot
         x, res = _c(x), _c(res)
         M, Hd = x.shape
         bqkv = _cat_views([bq, bk, bv])
@@ -392,7 +420,11 @@ class SiglipAttentionFn(torch.autograd.Function):
         for i, b in enumerate((bq, bk, bv)):
             retb = _bias_grad(dqkv[:, i * Hd:(i + 1) * Hd], b, nig[3 + 2 * i])  # strided view, no copy
             rets += [dws[i][2], retb]
-        return (dx, dout, *rets, ret_wo, ret_bo, None)
+        dres = dout
+        if ctx.slot is not None:  # handed to layer_norm1's backward (ResidualSlot)
+            ctx.slot.put(dout)
+            dres = None
+        return (dx, dres, *rets, ret_wo, ret_bo, None, None)
 
 
 class SiglipMLPFn(torch.autograd.Function):
@@ -400,7 +432,8 @@ class SiglipMLPFn(torch.autograd.Function):
     fc2 bias+residual fused in GEMM epilogues, GELU derivative fused into the fc2 dgrad epilogue."""
 
     @staticmethod
-    def forward(ctx, x, res, w1, b1, w2, b2):
+    def forward(ctx, x, res, w1, b1, w2, b2, slot=None):
+        ctx.slot = slot
         x, res = _c(x), _c(res)
         M = x.shape[0]
         I = w1.shape[0]
@@ -430,7 +463,11 @@ class SiglipMLPFn(torch.autograd.Function):
         if dw1 is not None:
             K.linear_wgrad(dpre, x, [dw1], accumulate=acc1)
         ret_b1 = _bias_grad(dpre, b1, nig[3])
-        return dx, dout, ret_w1, ret_b1, ret_w2, ret_b2
+        dres = dout
+        if ctx.slot is not None:  # handed to layer_norm2's backward (ResidualSlot)
+            ctx.slot.put(dout)
+            dres = None
+        return dx, dres, ret_w1, ret_b1, ret_w2, ret_b2, None
 
 
 class PatchEmbedFn(torch.autograd.Function):

@@ -53,15 +53,15 @@ class Gemma2RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.zeros(dim))
 
-    def forward(self, x):
+    def forward(self, x, slot=None):
         shp = x.shape
-        return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps).view(shp)
+        return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps, slot).view(shp)
 
-    def add_forward(self, residual, y):
+    def add_forward(self, residual, y, slot=None):
         """residual + self(y) (decoder-layer residual branches)."""
         shp = y.shape
         return Fn.AddRMSNormFn.apply(residual.reshape(-1, shp[-1]), y.reshape(-1, shp[-1]), self.weight,
-                                     self.eps).view(shp)
+                                     self.eps, slot).view(shp)
 
     def extra_repr(self):
         return f"{tuple(self.weight.shape)}, eps={self.eps}"
@@ -183,12 +183,15 @@ class Gemma2DecoderLayer(nn.Module):
 
     def forward(self, hidden_states, attention_mask: KVMask, rope: tuple):
         # reference :475-496 (sandwich norms + residuals)
-        x = self.input_layernorm(hidden_states)
+        # each residual-stream tensor has two consumers (pre-norm, residual add): a ResidualSlot sums their
+        # gradients inside the pre-norm's backward kernel instead of an autograd add
+        s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
+        x = self.input_layernorm(hidden_states, s1)
         a = self.self_attn(x, attention_mask, rope)
-        h = self.post_attention_layernorm.add_forward(hidden_states, a)
-        x = self.pre_feedforward_layernorm(h)
+        h = self.post_attention_layernorm.add_forward(hidden_states, a, s1)
+        x = self.pre_feedforward_layernorm(h, s2)
         m = self.mlp(x)
-        return self.post_feedforward_layernorm.add_forward(h, m)
+        return self.post_feedforward_layernorm.add_forward(h, m, s2)
 
 
 class Gemma2Model(nn.Module):

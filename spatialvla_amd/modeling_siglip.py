@@ -49,11 +49,11 @@ class SiglipAttention(nn.Module):
         self.q_proj = nn.Linear(self.embed_dim, self.embed_dim)
         self.out_proj = nn.Linear(self.embed_dim, self.embed_dim)
 
-    def forward_residual(self, x2d, res2d, B, Lq):
+    def forward_residual(self, x2d, res2d, B, Lq, slot=None):
         cfg = Fn.SiglipAttnCfg(B, Lq, self.num_heads, self.head_dim, self.scale)
         return Fn.SiglipAttentionFn.apply(x2d, res2d, self.q_proj.weight, self.q_proj.bias, self.k_proj.weight,
                                           self.k_proj.bias, self.v_proj.weight, self.v_proj.bias,
-                                          self.out_proj.weight, self.out_proj.bias, cfg)
+                                          self.out_proj.weight, self.out_proj.bias, cfg, slot)
 
 
 class SiglipMLP(nn.Module):
@@ -65,8 +65,8 @@ class SiglipMLP(nn.Module):
         self.fc1 = nn.Linear(config.hidden_size, config.intermediate_size)
         self.fc2 = nn.Linear(config.intermediate_size, config.hidden_size)
 
-    def forward_residual(self, x2d, res2d):
-        return Fn.SiglipMLPFn.apply(x2d, res2d, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+    def forward_residual(self, x2d, res2d, slot=None):
+        return Fn.SiglipMLPFn.apply(x2d, res2d, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, slot)
 
 
 class SiglipEncoderLayer(nn.Module):
@@ -79,10 +79,11 @@ class SiglipEncoderLayer(nn.Module):
         self.mlp = SiglipMLP(config)
 
     def forward(self, h2d, B, Lq):
-        x = Fn.LayerNormFn.apply(h2d, self.layer_norm1.weight, self.layer_norm1.bias, self.layer_norm1.eps)
-        h2d = self.self_attn.forward_residual(x, h2d, B, Lq)
-        x = Fn.LayerNormFn.apply(h2d, self.layer_norm2.weight, self.layer_norm2.bias, self.layer_norm2.eps)
-        return self.mlp.forward_residual(x, h2d)
+        s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()  # see Fn.ResidualSlot
+        x = Fn.LayerNormFn.apply(h2d, self.layer_norm1.weight, self.layer_norm1.bias, self.layer_norm1.eps, s1)
+        h2d = self.self_attn.forward_residual(x, h2d, B, Lq, s1)
+        x = Fn.LayerNormFn.apply(h2d, self.layer_norm2.weight, self.layer_norm2.bias, self.layer_norm2.eps, s2)
+        return self.mlp.forward_residual(x, h2d, s2)
 
 
 class SiglipEncoder(nn.Module):
@@ -108,7 +109,7 @@ class SiglipVisionTransformer(nn.Module):
         Lq = self.embeddings.num_patches
         for layer in self.encoder.layers:
             h = layer(h, B, Lq)
-        h = Fn.LayerNormFn.apply(h, self.post_layernorm.weight, self.post_layernorm.bias, self.post_layernorm.eps)
+        h = Fn.LayerNormFn.apply(h, self.post_layernorm.weight, self.post_layernorm.bias, self.post_layernorm.eps, None)
         return h.view(B, Lq, -1)
 
 

@@ -59,7 +59,7 @@ class Ego3DPositionEmbeddingMLP(nn.Module):
         """feat_padded [N, round8(F)] (zero tail) -> residual + head(feat)."""
         h0, ln, _, h3 = self.position_embedding_head
         x = Fn.LinearFn.apply(feat_padded, h0.weight, h0.bias, None, 1.0)
-        x = Fn.LayerNormFn.apply(x, ln.weight, ln.bias, ln.eps)
+        x = Fn.LayerNormFn.apply(x, ln.weight, ln.bias, ln.eps, None)
         x = Fn.ReLUFn.apply(x)
         return Fn.LinearFn.apply(x, h3.weight, h3.bias, residual2d, 1.0)
 

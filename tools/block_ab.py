@@ -1,0 +1,57 @@
+"""A/B one Gemma2DecoderLayer fwd+bwd (bench.py's gemma2_block workload) with and without ResidualSlot fusion,
+interleaved on one box.  usage: python tools/block_ab.py [reps]"""
+import os, sys, time
+import numpy as np
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from spatialvla_amd import SpatialVLAConfig, presets
+from spatialvla_amd import functional as Fn
+from spatialvla_amd.modeling_gemma2 import Gemma2DecoderLayer, KVMask
+
+dev = "cuda"
+cfg = SpatialVLAConfig(**presets.spatialvla_4b(False)).text_config
+with torch.device(dev):
+    layer = Gemma2DecoderLayer(cfg, 1).to(torch.bfloat16)
+with torch.no_grad():
+    for p in layer.parameters():
+        if p.dim() >= 2:
+            p.normal_(0, 0.02)
+B, L = 32, 312
+tt = torch.zeros(B, L, dtype=torch.long, device=dev); tt[:, L - 13:] = 1
+mask = KVMask.build(torch.ones(B, L, dtype=torch.long, device=dev), tt, True, B, L, dev)
+pos = torch.arange(1, L + 1, device=dev).unsqueeze(0).expand(B, L)
+rope = layer.self_attn.rotary_emb.tables(pos, torch.bfloat16)
+g = torch.Generator(device=dev).manual_seed(5)
+x = torch.randn(B, L, cfg.hidden_size, device=dev, generator=g).to(torch.bfloat16).requires_grad_(True)
+gy = torch.randn(B, L, cfg.hidden_size, device=dev, generator=g).to(torch.bfloat16)
+Slot = Fn.ResidualSlot
+
+
+def run(use_slot, iters=10):
+    Fn.ResidualSlot = Slot if use_slot else (lambda: None)
+    s = torch.cuda.current_stream()
+    out = []
+    for it in range(iters + 2):
+        for p in layer.parameters():
+            p.grad = None
+        x.grad = None
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record(s)
+        y = layer(x, mask, rope)
+        e1.record(s)
+        y.backward(gy)
+        e2.record(s)
+        e2.synchronize()
+        if it >= 2:
+            out.append((e0.elapsed_time(e1), e0.elapsed_time(e2)))
+    return np.mean(out, 0), x.grad.clone()
+
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+gs = {}
+for r in range(reps):
+    for mode in (0, 1):
+        (f, t), gx = run(bool(mode))
+        gs[mode] = gx
+        print(f"slot={mode} fwd {f:.3f} ms  fwd+bwd {t:.3f} ms", flush=True)
+print("x.grad bitwise equal:", torch.equal(gs[0], gs[1]))
