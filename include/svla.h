@@ -99,9 +99,10 @@ typedef struct {
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                    const svla_epilogue* epi, void* stream);
-/* Tuning knob (not a reference interface): main-loop variant for the 256x256 tile.
- * 0 = 8-phase ping-pong + stream-K (default), 1 = two-barrier schedule, 2 = 8-phase without
- * stream-K.  Returns 0. */
+/* Tuning knob (not a reference interface): GEMM dispatch variant.  0 = auto (default: plain TN stores via
+ * hipBLASLt, else the 4-wave or 8-phase 256x256 kernel + stream-K by shape), 1 = two-barrier schedule,
+ * 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel,
+ * 5 = auto without hipBLASLt (hand-written kernels only).  Returns 0. */
 int svla_gemm_set_variant(int variant);
 /* Stream-K workspace of the 256x256 GEMM (caller-owned, zero-filled once before first use, 256-B aligned,
  * at least svla_gemm_workspace_bytes() for the current device).  Without one (ws = NULL) every output tile

@@ -1343,9 +1343,10 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   return svla::check_launch("gemm");
 }
 
-// main-loop choice for the 256x256 tile (A/B tuning knob): 0 = auto (4-wave kernel for long-K GEMMs with more
-// than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
-// without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel
+// dispatch choice (A/B tuning knob): 0 = auto (plain TN stores via hipBLASLt; 4-wave kernel for long-K GEMMs
+// with more than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
+// without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = auto without
+// hipBLASLt
 int g_variant = 0;
 
 struct SKWorkspace {
@@ -1572,10 +1573,21 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   // paired per call) once the k-loop is long enough to amortise its tile prologue/epilogue, the grid has more
   // than a wave of tiles and the epilogue is light -- it runs the epilogue on half the waves, so GEGLU-backward
   // (+31%), softcap-CE (+9%) and RoPE (+2%) stay on the 8-wave kernel, as do short-K / sub-wave shapes
+  // plain TN store (both operands K-contiguous, no epilogue, no segments): hipBLASLt (blaslt.hip), in the auto
+  // variant only; 5 = hand-written kernels for everything
+  auto whole = [](const svla_operand* o, int64_t R, int64_t Kx) {
+    return o->nseg == 1 && (o->r_valid == 0 || o->r_valid >= R) && (o->k_valid == 0 || o->k_valid >= Kx);
+  };
+  if (g_variant == 0 && epi->kind == SVLA_EPI_STORE && !epi->accumulate && epi->alpha == 1.0f &&
+      A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && whole(A, M, K) && whole(B, N, K) && c_nseg == 1 &&
+      C.start[0] == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus()) &&
+      svla::blaslt_gemm_tn(M, N, K, A->ptr[0], A->ld, B->ptr[0], B->ld, C.ptr[0], ldc, g_ws.ptr,
+                           (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0)
+    return svla::check_launch("gemm (hipBLASLt)");
   const int64_t t256 = tiles(256, 256);
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (g_variant == 3 || (g_variant == 0 && light_epi && K >= 2048 && t256 >= num_cus() &&
+                    (g_variant == 3 || ((g_variant == 0 || g_variant == 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
                                         (t256 >= 512 || K >= 4096) &&
                                         (B->layout == SVLA_LAYOUT_KC || K >= 4096)));  // short-K x RC B: +4%
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile

@@ -5,6 +5,7 @@ kernel assumes (so a bad call raises on the host instead of faulting the device)
 torch's current HIP stream.  No function here has a non-HIP path.
 """
 import ctypes
+import os
 import math
 from typing import List, Optional, Sequence
 

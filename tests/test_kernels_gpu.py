@@ -40,13 +40,13 @@ def test_gemm_layouts(cuda, M, N, K, layouts):
 
 
 def _variants(fn):
-    """Run fn() under the 256x256 main-loop variants: 1 = 2-barrier, 2 = 8-phase, 0 = product dispatch
-    (twice), 3 = 4-wave kernel wherever both operands are KC (twice), 4 = 8-phase + stream-K.
-    Returns {variant: result}."""
+    """Run fn() under the GEMM dispatch variants: 1 = 2-barrier, 2 = 8-phase, 0 = product dispatch (twice;
+    plain TN stores go to hipBLASLt), 3 = 4-wave kernel wherever both operands are KC (twice), 4 = 8-phase +
+    stream-K, 5 = product dispatch with hand-written kernels only.  Returns {variant: result}."""
     from spatialvla_amd import _lib as L
     outs = {}
     try:
-        for v in (1, 2, 0, "0b", 3, "3b", 4):
+        for v in (1, 2, 0, "0b", 3, "3b", 4, 5):
             L.lib().svla_gemm_set_variant({"0b": 0, "3b": 3}.get(v, v))
             outs[v] = fn()
             torch.cuda.synchronize()
@@ -69,7 +69,7 @@ def _check_variants(outs, tol=2e-3):
         assert torch.equal(a, b)
     for a, b in zip(f(3), f("3b")):
         assert torch.equal(a, b)
-    for v in (0, 3, 4):
+    for v in (0, 3, 4, 5):
         assert rel_l2(_flat(outs[v]), _flat(outs[1])) < tol, v
 
 

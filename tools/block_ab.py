@@ -16,6 +16,18 @@ with torch.no_grad():
     for p in layer.parameters():
         if p.dim() >= 2:
             p.normal_(0, 0.02)
+# flat parameter / gradient buffers in the engine's layout (TrainEngine: q|k|v adjacent, dW written in place)
+from spatialvla_amd.engine import _group_params
+ps = _group_params(layer)
+offs, n = [], 0
+for p in ps:
+    offs.append(n); n += (p.numel() + 63) // 64 * 64
+flat_p = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+flat_g = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+with torch.no_grad():
+    for p, o in zip(ps, offs):
+        v = flat_p[o:o + p.numel()].view_as(p); v.copy_(p.data); p.data = v
+        p._svla_grad = flat_g[o:o + p.numel()].view_as(p); p._svla_accum = False
 B, L = 32, 312
 tt = torch.zeros(B, L, dtype=torch.long, device=dev); tt[:, L - 13:] = 1
 mask = KVMask.build(torch.ones(B, L, dtype=torch.long, device=dev), tt, True, B, L, dev)
@@ -48,6 +60,10 @@ def run(use_slot, iters=10):
 
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+if len(sys.argv) > 2:  # profile mode: one configuration only (for rocprofv3 --kernel-trace)
+    (f, t), _ = run(sys.argv[2] == "1", iters=int(sys.argv[3]) if len(sys.argv) > 3 else 10)
+    print(f"slot={sys.argv[2]} fwd {f:.3f} ms  fwd+bwd {t:.3f} ms", flush=True)
+    sys.exit(0)
 gs = {}
 for r in range(reps):
     for mode in (0, 1):
