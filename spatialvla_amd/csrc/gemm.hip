@@ -1343,6 +1343,36 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   return svla::check_launch("gemm");
 }
 
+// In-place rotate_half RoPE over the first rope_cols columns of a bf16 [M][ldc] matrix (heads of rope_D
+// columns), row m at position m % rope_L: the ROPE epilogue as a separate pass, for a GEMM that stored plain
+// bf16 (hipBLASLt).  Same rounding as the epilogue: out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)).
+// One thread owns 8 columns of the low half of a head and their partners D/2 away, so it reads both before
+// writing either.
+__global__ void rope_inplace_kernel(int64_t M, bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
+  const int hd = E.rope_D, half = hd >> 1, cph = half / 8;  // 8-column chunks per half head
+  const int64_t per_row = (int64_t)(E.rope_cols / hd) * cph;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * per_row) return;
+  const int64_t m = idx / per_row;
+  const int r = (int)(idx % per_row);
+  const int head = r / cph, dd = (r % cph) * 8;
+  bf16_t* lo = c + m * ldc + (int64_t)head * hd + dd;
+  bf16_t* hi = lo + half;
+  const int64_t pos = m % E.rope_L;
+  float xl[8], xh[8], cs[8], sn[8], ol[8], oh[8];
+  unpack8(*reinterpret_cast<const u32x4*>(lo), xl);
+  unpack8(*reinterpret_cast<const u32x4*>(hi), xh);
+  unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.rope_cos + pos * E.rope_ld + dd), cs);
+  unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.rope_sin + pos * E.rope_ld + dd), sn);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ol[j] = round_bf(xl[j] * cs[j]) + round_bf(-xh[j] * sn[j]);
+    oh[j] = round_bf(xh[j] * cs[j]) + round_bf(xl[j] * sn[j]);
+  }
+  *reinterpret_cast<u32x4*>(lo) = pack8(ol);
+  *reinterpret_cast<u32x4*>(hi) = pack8(oh);
+}
+
 // dispatch choice (A/B tuning knob): 0 = auto (plain TN stores via hipBLASLt; 4-wave kernel for long-K GEMMs
 // with more than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
 // without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = auto without
@@ -1578,12 +1608,21 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   auto whole = [](const svla_operand* o, int64_t R, int64_t Kx) {
     return o->nseg == 1 && (o->r_valid == 0 || o->r_valid >= R) && (o->k_valid == 0 || o->k_valid >= Kx);
   };
-  if (g_variant == 0 && epi->kind == SVLA_EPI_STORE && !epi->accumulate && epi->alpha == 1.0f &&
-      A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && whole(A, M, K) && whole(B, N, K) && c_nseg == 1 &&
-      C.start[0] == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus()) &&
+  // RoPE (the Gemma2 q|k|v projection) likewise: hipBLASLt store + the in-place rotate_half pass
+  const bool tn_plain = g_variant == 0 && !epi->accumulate && epi->alpha == 1.0f && A->layout == SVLA_LAYOUT_KC &&
+                        B->layout == SVLA_LAYOUT_KC && whole(A, M, K) && whole(B, N, K) && c_nseg == 1 &&
+                        C.start[0] == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  const bool rope_split = epi->kind == SVLA_EPI_ROPE && ldc % 8 == 0 && epi->rope_D % 16 == 0;
+  if (tn_plain && (epi->kind == SVLA_EPI_STORE || rope_split) &&
       svla::blaslt_gemm_tn(M, N, K, A->ptr[0], A->ld, B->ptr[0], B->ld, C.ptr[0], ldc, g_ws.ptr,
-                           (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0)
+                           (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0) {
+    if (epi->kind == SVLA_EPI_ROPE) {
+      const int64_t work = M * (epi->rope_cols / epi->rope_D) * (epi->rope_D / 16);
+      hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M,
+                         (bf16_t*)C.ptr[0], ldc, *epi);
+    }
     return svla::check_launch("gemm (hipBLASLt)");
+  }
   const int64_t t256 = tiles(256, 256);
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
   const bool use4 = !kseg && seg_ok(256, 256) &&

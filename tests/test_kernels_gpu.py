@@ -449,23 +449,21 @@ def test_gemm_rope_epilogue(cuda, D, Hq, Hkv, L):
     inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
     f = (torch.arange(L, device=cuda).float() + 1)[:, None] * inv[None]
     cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
-    plain = torch.empty(B * L, N, dtype=BF, device=cuda)
-    Kn.linear_fwd(x, [w], plain)
-    rot = torch.empty_like(plain)
     nrot = (Hq + Hkv) * D
-    Kn.linear_fwd(x, [w], rot, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
-    ref = plain.clone()
-    ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
-    assert torch.equal(rot, ref)
-    if D == 256:  # the same through the 4-wave kernel (same k order per output: bitwise equal)
+    # 0: hipBLASLt store + in-place RoPE pass; 5: hand-written kernel with the fused epilogue; 3: 4-wave kernel
+    for v in ((0, 5, 3) if D == 256 else (0, 5)):
         try:
-            L_.lib().svla_gemm_set_variant(3)
-            rot4 = torch.empty_like(plain)
-            Kn.linear_fwd(x, [w], rot4, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
+            L_.lib().svla_gemm_set_variant(v)
+            plain = torch.empty(B * L, N, dtype=BF, device=cuda)
+            Kn.linear_fwd(x, [w], plain)
+            rot = torch.empty_like(plain)
+            Kn.linear_fwd(x, [w], rot, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
             torch.cuda.synchronize()
         finally:
             L_.lib().svla_gemm_set_variant(0)
-        assert torch.equal(rot4, ref)
+        ref = plain.clone()
+        ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
+        assert torch.equal(rot, ref), v
 
 
 def test_gemma2_attention_plugin_signature(cuda):
