@@ -1373,6 +1373,29 @@ __global__ void rope_inplace_kernel(int64_t M, bf16_t* __restrict__ c, int64_t l
   *reinterpret_cast<u32x4*>(hi) = pack8(oh);
 }
 
+// The remaining epilogues of a bias GEMM that stored bf16(acc + bias) through hipBLASLt, as one elementwise
+// pass with the fused epilogues' rounding: BIAS_RESID c = bf16(c + in0); BIAS_GELU c = gelu(out1) (out1 holds
+// the stored pre-activation).  N % 8 == 0.
+__global__ void epi_pass_kernel(int kind, int64_t M, int64_t N, bf16_t* __restrict__ c, int64_t ldc,
+                                svla_epilogue E) {
+  const int64_t cpr = N / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * cpr) return;
+  const int64_t m = idx / cpr, n = (idx % cpr) * 8;
+  float v[8], r[8];
+  if (kind == SVLA_EPI_BIAS_RESID) {
+    unpack8(*reinterpret_cast<const u32x4*>(c + m * ldc + n), v);
+    unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.in0 + m * E.ld_in0 + n), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += r[j];
+  } else {
+    unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.out1 + m * E.ld_out1 + n), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(r[j]);
+  }
+  *reinterpret_cast<u32x4*>(c + m * ldc + n) = pack8(v);
+}
+
 // dispatch choice (A/B tuning knob): 0 = auto (plain TN stores via hipBLASLt; 4-wave kernel for long-K GEMMs
 // with more than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
 // without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = auto without
@@ -1612,16 +1635,28 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   const bool tn_plain = g_variant == 0 && !epi->accumulate && epi->alpha == 1.0f && A->layout == SVLA_LAYOUT_KC &&
                         B->layout == SVLA_LAYOUT_KC && whole(A, M, K) && whole(B, N, K) && c_nseg == 1 &&
                         C.start[0] == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
-  const bool rope_split = epi->kind == SVLA_EPI_ROPE && ldc % 8 == 0 && epi->rope_D % 16 == 0;
-  if (tn_plain && (epi->kind == SVLA_EPI_STORE || rope_split) &&
-      svla::blaslt_gemm_tn(M, N, K, A->ptr[0], A->ld, B->ptr[0], B->ld, C.ptr[0], ldc, g_ws.ptr,
-                           (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0) {
-    if (epi->kind == SVLA_EPI_ROPE) {
-      const int64_t work = M * (epi->rope_cols / epi->rope_D) * (epi->rope_D / 16);
-      hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M,
-                         (bf16_t*)C.ptr[0], ldc, *epi);
+  // and the SigLIP bias family: bias in hipBLASLt's epilogue, residual / GELU as one elementwise pass
+  const int ek = epi->kind;
+  const bool rope_split = ek == SVLA_EPI_ROPE && epi->rope_D % 16 == 0;
+  const bool bias_split = (ek == SVLA_EPI_BIAS || ek == SVLA_EPI_BIAS_GELU ||
+                           (ek == SVLA_EPI_BIAS_RESID && epi->in0 != C.ptr[0])) && N % 8 == 0;  // in0 read after C
+  if (tn_plain && (ek == SVLA_EPI_STORE || rope_split || bias_split)) {
+    const void* bias = (ek == SVLA_EPI_STORE || ek == SVLA_EPI_ROPE) ? nullptr : epi->bias;
+    void* dst = ek == SVLA_EPI_BIAS_GELU ? epi->out1 : C.ptr[0];
+    const int64_t ldd = ek == SVLA_EPI_BIAS_GELU ? epi->ld_out1 : ldc;
+    if (svla::blaslt_gemm_tn(M, N, K, A->ptr[0], A->ld, B->ptr[0], B->ld, bias, dst, ldd, g_ws.ptr,
+                             (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0) {
+      if (ek == SVLA_EPI_ROPE) {
+        const int64_t work = M * (epi->rope_cols / epi->rope_D) * (epi->rope_D / 16);
+        hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M,
+                           (bf16_t*)C.ptr[0], ldc, *epi);
+      } else if (ek == SVLA_EPI_BIAS_RESID || ek == SVLA_EPI_BIAS_GELU) {
+        const int64_t work = M * (N / 8);
+        hipLaunchKernelGGL(epi_pass_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, ek, M, N,
+                           (bf16_t*)C.ptr[0], ldc, *epi);
+      }
+      return svla::check_launch("gemm (hipBLASLt)");
     }
-    return svla::check_launch("gemm (hipBLASLt)");
   }
   const int64_t t256 = tiles(256, 256);
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;

@@ -102,8 +102,8 @@ namespace svla {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // blaslt.hip: plain TN GEMM through hipBLASLt; 0 = done, nonzero = no plan (run the hand-written kernel)
-int blaslt_gemm_tn(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
-                   int64_t ldc, void* ws, size_t ws_bytes, hipStream_t s);
+int blaslt_gemm_tn(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
+                   const void* bias, void* C, int64_t ldc, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace svla
 
 #define SVLA_CHECK_ARG(cond, ...)            \
