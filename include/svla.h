@@ -142,6 +142,28 @@ typedef struct {
 } svla_attn_args;
 
 int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);
+/* KV-cached decode attention.  Replaces the HybridCache decode step of
+ * SpatialVLAForConditionalGeneration.generate / predict_action (model/modeling_spatialvla.py:440-492) through
+ * eager_attention_forward (model/modeling_gemma2.py:169-195, cache update :387-395).
+ * Lq new queries per sequence sit at absolute positions Lk-Lq .. Lk-1 and attend to the first Lk cached keys:
+ *   q   (b, t, h, d) at q + (b*Lq + t)*ldq + h*D + d              (already rotated)
+ *   k/v (b, j, h, d) at k + b*bsk + j*ldk + h*D + d               (cache rows, keys already rotated)
+ *   out (b, t, h, d) at out + (b*Lq + t)*ldo + h*D + d
+ * kv_class[b*ldc + j] as svla_attn_fwd (0 prompt key, 1 causal, 2 never visible); sliding window as there.
+ * D in {64,128,192,256}; Hq/Hkv in {1,2,4}; (Hq/Hkv) * Lk * 4 bytes <= 128 KiB. */
+typedef struct {
+  int32_t B, Lq, Lk, Hq, Hkv, D;
+  int32_t sliding_window;
+  float scale;
+  float softcap;
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk; int64_t bsk;
+  const void* v; int64_t ldv; int64_t bsv;
+  const uint8_t* kv_class; int64_t ldc;
+} svla_attn_decode_args;
+
+int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, void* stream);
+
 /* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
  * workspace: B*Hq*L fp32 (row dot(dO, O)). */
 int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,

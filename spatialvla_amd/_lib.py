@@ -45,6 +45,13 @@ class AttnArgs(ctypes.Structure):
                 ("kv_class", c_vp), ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64)]
 
 
+
+class AttnDecodeArgs(ctypes.Structure):
+    _fields_ = [("B", c_i32), ("Lq", c_i32), ("Lk", c_i32), ("Hq", c_i32), ("Hkv", c_i32), ("D", c_i32),
+                ("sliding_window", c_i32), ("scale", c_f32), ("softcap", c_f32),
+                ("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("bsk", c_i64),
+                ("v", c_vp), ("ldv", c_i64), ("bsv", c_i64), ("kv_class", c_vp), ("ldc", c_i64)]
+
 # name -> (restype, argtypes); every entry point of include/svla.h
 SIGNATURES = {
     "svla_last_error": (ctypes.c_char_p, []),
@@ -58,6 +65,7 @@ SIGNATURES = {
     "svla_attn_fwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_vp]),
     "svla_attn_bwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, c_vp]),
+    "svla_attn_decode": (c_i32, [ctypes.POINTER(AttnDecodeArgs), c_vp, c_i64, c_vp]),
     "svla_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),
     "svla_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp]),
     "svla_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),

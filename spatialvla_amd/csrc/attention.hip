@@ -18,6 +18,8 @@
 //    accumulators before the store — no separate RoPE pass over HBM.
 //  * Backward is two deterministic kernels (dK/dV per key tile looping over the GQA query heads,
 //    dQ per query tile) — no float atomics.
+#include <atomic>
+
 #include "svla_common.h"
 
 namespace {
@@ -564,12 +566,17 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
   }
 }
 
+// The dynamic-LDS limit of a kernel must cover the largest launch so far: the class array (and the bwd
+// lse/delta slabs) grow with L, so the attribute is raised whenever a launch needs more than the last setting.
 template <auto KERN>
 void set_lds_once(int bytes) {
-  static bool done = false;  // one flag per kernel instantiation
-  if (!done) {
-    (void)hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    done = true;
+  static std::atomic<int> set_to{0};  // one high-water mark per kernel instantiation
+  int cur = set_to.load(std::memory_order_relaxed);
+  while (bytes > cur) {
+    if (set_to.compare_exchange_weak(cur, bytes)) {
+      (void)hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+      break;
+    }
   }
 }
 
@@ -590,6 +597,7 @@ int round16(int x) { return (x + 15) & ~15; }
 template <int D, int NH>
 int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
   const int lds = 4 * tile_bytes<D>(64) + round16(a.L);
+  SVLA_CHECK_ARG(lds <= 160 * 1024, "attn_fwd: L too large for the LDS-resident key classes");
   dim3 grid((a.L + 63) / 64, a.Hq / NH, a.B), block(256 * NH);
   set_lds_once<attn_fwd_kernel<D, NH>>(lds);
   hipLaunchKernelGGL((attn_fwd_kernel<D, NH>), grid, block, lds, s, a, out, ldo, lse);

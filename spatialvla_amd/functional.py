@@ -305,6 +305,36 @@ class GemmaAttentionFn(torch.autograd.Function):
         return (dx, *rets, ret_wo, None, None, None, None)
 
 
+@torch.no_grad()
+def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_class, p0, cfg: GemmaAttnCfg):
+    """Gemma2Attention.forward with a KV cache (modeling_gemma2.py:364-413, cache update :387-395), inference
+    only.  x holds the cfg.L new tokens of each of the cfg.B sequences, at absolute positions p0 .. p0+L-1;
+    their rotated k and v are written into rows p0.. of k_cache/v_cache ([B, capacity, Hkv*D]).  The prefill
+    (p0 == 0) runs the flash kernel of the uncached forward over the prompt, so it is bit-identical to it;
+    later steps run the decode kernel over the first p0+L cache rows."""
+    x = _c(x)
+    M, H = x.shape
+    B, Lq = cfg.B, cfg.L
+    qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
+    qkv = _empty(M, qd + 2 * kd, like=x)
+    K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, Lq, cfg.D, qd + kd))
+    k_cache[:, p0:p0 + Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
+    v_cache[:, p0:p0 + Lq].copy_(qkv[:, qd + kd:].view(B, Lq, kd))
+    attn = _empty(M, qd, like=x)
+    if p0 == 0:
+        lse = _empty(B, cfg.Hq, Lq, dtype=F32, like=x)
+        cls = kv_class[:, :Lq].contiguous()  # held until the launch: attn_args keeps only its pointer
+        a = K.attn_args(B, Lq, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
+                        qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, cls, cfg.window)
+        K.attn_fwd(a, attn, lse)
+    else:
+        K.attn_decode(qkv[:, :qd], Lq, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale, cfg.softcap,
+                      kv_class, cfg.window, attn)
+    out = _empty(M, wo.shape[0], like=x)
+    K.linear_fwd(attn, [wo], out)
+    return out
+
+
 class GemmaMLPFn(torch.autograd.Function):
     """Gemma2MLP.forward (modeling_gemma2.py:91-92): down(gelu_tanh(gate x) * up x) — gate/up as one
     GEMM with the GeGLU in its epilogue; backward: dH GEMM, then the GeGLU derivative in one elementwise pass."""

@@ -316,6 +316,28 @@ def attn_fwd(a: L.AttnArgs, out: torch.Tensor, lse: torch.Tensor):
     L.check(L.lib().svla_attn_fwd(ctypes.byref(a), out.data_ptr(), _ld(out), lse.data_ptr(), _stream()), "attn_fwd")
 
 
+def attn_decode(q, Lq, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_class, window, out):
+    """Lq new queries (rows b*Lq+t of q, rotated) against the first Lk rows of the [B, cap, Hkv*D] K/V cache."""
+    B = k_cache.shape[0]
+    _req(q.shape[0] == B * Lq and out.shape[0] == B * Lq, "attn_decode: q/out rows != B*Lq")
+    _req(k_cache.shape[1] >= Lk and v_cache.shape[1] >= Lk, "attn_decode: cache shorter than Lk")
+    _req(k_cache.stride(2) == 1 and v_cache.stride(2) == 1 and q.stride(1) == 1 and out.stride(1) == 1,
+         "attn_decode: rows must be contiguous")
+    _req(kv_class is None or (kv_class.dtype == torch.uint8 and kv_class.shape[0] == B and kv_class.stride(1) == 1),
+         "attn_decode: kv_class must be uint8 [B, >=Lk]")
+    for t, n in ((q, "q"), (k_cache, "k"), (v_cache, "v"), (out, "out")):
+        _chk_bf16(t, n)
+    a = L.AttnDecodeArgs()
+    a.B, a.Lq, a.Lk, a.Hq, a.Hkv, a.D = B, Lq, Lk, Hq, Hkv, D
+    a.sliding_window, a.scale, a.softcap = int(window or 0), float(scale), float(softcap or 0.0)
+    a.q, a.ldq = q.data_ptr(), q.stride(0)
+    a.k, a.ldk, a.bsk = k_cache.data_ptr(), k_cache.stride(1), k_cache.stride(0)
+    a.v, a.ldv, a.bsv = v_cache.data_ptr(), v_cache.stride(1), v_cache.stride(0)
+    a.kv_class = _ptr(kv_class)
+    a.ldc = kv_class.stride(0) if kv_class is not None else 0
+    L.check(L.lib().svla_attn_decode(ctypes.byref(a), out.data_ptr(), out.stride(0), _stream()), "attn_decode")
+
+
 def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):
     ws = torch.empty(a.B * a.Hq * a.L, dtype=torch.float32, device=out.device)
     L.check(L.lib().svla_attn_bwd(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),

@@ -47,6 +47,38 @@ class KVMask:
         return KVMask(cls.contiguous())
 
 
+class Gemma2KVCache:
+    """Key/value cache of greedy decoding: the reference's HybridCache (transformers cache_utils, built at
+    modeling_gemma2.py:712-720, updated at :387-395) for sequences shorter than the sliding window (4096) —
+    there every layer, sliding or global, keeps all keys, and the window is applied as a mask by the kernel.
+
+    Layout in HBM: key_cache / value_cache [layers, B, capacity, Hkv*D] bf16 (one row per token, heads
+    back to back, rotated keys); kv_class [B, capacity] uint8 per-key classes (KVMask: prompt keys 0 or 2,
+    generated keys 1)."""
+
+    def __init__(self, config, batch_size: int, capacity: int, device, dtype=torch.bfloat16):
+        kd = config.num_key_value_heads * config.head_dim
+        self.config = config
+        self.key_cache = torch.empty(config.num_hidden_layers, batch_size, capacity, kd, dtype=dtype, device=device)
+        self.value_cache = torch.empty_like(self.key_cache)
+        self.kv_class = torch.full((batch_size, capacity), 2, dtype=torch.uint8, device=device)
+        self.seen_tokens = 0
+
+    @property
+    def capacity(self) -> int:
+        return self.key_cache.shape[2]
+
+    def get_seq_length(self, layer_idx: int = 0) -> int:
+        return self.seen_tokens
+
+    def append_classes(self, cls: torch.Tensor):
+        """Classes of the next cls.shape[1] tokens (called once per forward, before the layers)."""
+        n = cls.shape[1]
+        if self.seen_tokens + n > self.capacity:
+            raise ValueError(f"KV cache full: {self.seen_tokens} + {n} tokens > capacity {self.capacity}")
+        self.kv_class[:, self.seen_tokens:self.seen_tokens + n] = cls
+
+
 class Gemma2RMSNorm(nn.Module):
     def __init__(self, dim: int, eps: float = 1e-6):
         super().__init__()
@@ -148,11 +180,17 @@ class Gemma2Attention(nn.Module):
         self.o_proj = nn.Linear(self.num_heads * self.head_dim, self.hidden_size, bias=False)
         self.rotary_emb = Gemma2RotaryEmbedding(self.head_dim, self.max_position_embeddings, self.rope_theta)
 
-    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple):
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None):
         B, Lq, H = hidden_states.shape
         cfg = Fn.GemmaAttnCfg(B, Lq, self.num_heads, self.num_key_value_heads, self.head_dim, self.scaling,
                               float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
         cos, sin = rope
+        if cache is not None:
+            i = self.layer_idx
+            out = Fn.gemma_attention_cached(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
+                                            self.v_proj.weight, self.o_proj.weight, cos, sin, cache.key_cache[i],
+                                            cache.value_cache[i], cache.kv_class, cache.seen_tokens, cfg)
+            return out.view(B, Lq, H)
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
                                         cfg)
@@ -181,13 +219,13 @@ class Gemma2DecoderLayer(nn.Module):
         self.post_feedforward_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.sliding_window = config.sliding_window
 
-    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple):
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None):
         # reference :475-496 (sandwich norms + residuals)
         # each residual-stream tensor has two consumers (pre-norm, residual add): a ResidualSlot sums their
         # gradients inside the pre-norm's backward kernel instead of an autograd add
         s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
         x = self.input_layernorm(hidden_states, s1)
-        a = self.self_attn(x, attention_mask, rope)
+        a = self.self_attn(x, attention_mask, rope, cache)
         h = self.post_attention_layernorm.add_forward(hidden_states, a, s1)
         x = self.pre_feedforward_layernorm(h, s2)
         m = self.mlp(x)
@@ -210,9 +248,15 @@ class Gemma2Model(nn.Module):
     def set_input_embeddings(self, value):
         self.embed_tokens = value
 
-    def forward(self, hidden_states, attention_mask: KVMask, position_ids, output_hidden_states=False):
+    def forward(self, hidden_states, attention_mask: KVMask, position_ids, output_hidden_states=False,
+                cache: Optional[Gemma2KVCache] = None):
         """hidden_states: inputs_embeds already multiplied by the bf16 normalizer (fused in the merge
-        kernel, reference :741-742)."""
+        kernel, reference :741-742).  With a cache, attention_mask holds the classes of the new tokens only
+        (they are appended to the cache's classes) and the cache advances by the new tokens."""
+        if cache is not None:
+            if torch.is_grad_enabled() and hidden_states.requires_grad:
+                raise ValueError("the KV cache is an inference path: run it under torch.no_grad()")
+            cache.append_classes(attention_mask.kv_class)
         rope = self.layers[0].self_attn.rotary_emb.tables(position_ids, hidden_states.dtype)
         all_h = () if output_hidden_states else None
         hook = getattr(self, "_svla_layer_grad_hook", None)
@@ -222,7 +266,9 @@ class Gemma2Model(nn.Module):
             if hook is not None and hidden_states.requires_grad:
                 # fires once d(layer input) is complete, i.e. after every weight grad of layers >= i
                 hidden_states.register_hook(lambda g, i=i: hook(i))
-            hidden_states = layer(hidden_states, attention_mask, rope)
+            hidden_states = layer(hidden_states, attention_mask, rope, cache)
+        if cache is not None:
+            cache.seen_tokens += hidden_states.shape[1]
         hidden_states = self.norm(hidden_states)
         if output_hidden_states:
             all_h += (hidden_states,)

@@ -23,7 +23,7 @@ from . import functional as Fn
 from . import zoe_fast
 from . import kernels as K
 from .configuration_spatialvla import SpatialVLAConfig
-from .modeling_gemma2 import Gemma2ForCausalLM, KVMask
+from .modeling_gemma2 import Gemma2ForCausalLM, Gemma2KVCache, KVMask
 from .modeling_siglip import SiglipVisionModel
 
 SIGLIP_MEAN, SIGLIP_STD = (0.5, 0.5, 0.5), (0.5, 0.5, 0.5)
@@ -289,9 +289,11 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         num_logits_to_keep: int = 0,
         kv_mask: Optional[KVMask] = None,
     ) -> Union[Tuple, SpatialVLACausalLMOutputWithPast]:
-        if past_key_values is not None or use_cache:
-            if past_key_values is not None:
-                raise NotImplementedError("KV-cached decoding is SURVEY §8(f)#2 (next); use predict_action()")
+        cache = past_key_values
+        if cache is not None and not isinstance(cache, Gemma2KVCache):
+            raise ValueError("past_key_values must be a Gemma2KVCache (see new_cache())")
+        if cache is None and use_cache and not torch.is_grad_enabled():
+            cache = self.new_cache(input_ids.shape[0], input_ids.shape[1] + 256)
         if inputs_embeds is not None:
             raise NotImplementedError("inputs_embeds input is not supported on the HIP path; pass input_ids")
         if output_attentions:
@@ -309,11 +311,23 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             labels = torch.where(input_ids == self.pad_token_id, -100, labels)
 
         hidden = self._merge_inputs(input_ids, image_features)
+        past = cache.seen_tokens if cache is not None else 0
         if position_ids is None:
-            start = 0 if cache_position is None else int(cache_position[0])
-            position_ids = (torch.arange(start, start + Lq, device=dev) + 1)[None]  # 1-indexed (:372)
-        mask = kv_mask or KVMask.build(attention_mask, token_type_ids, is_training, B, Lq, dev)
-        h, all_h = self.language_model.model(hidden, mask, position_ids, output_hidden_states=bool(output_hidden_states))
+            start = past if cache_position is None else int(cache_position[0])
+            position_ids = (torch.arange(start, start + Lq, device=dev) + 1)[None]  # 1-indexed (:372, :473-474)
+        if kv_mask is not None:
+            mask = kv_mask
+        elif past == 0:
+            mask = KVMask.build(attention_mask, token_type_ids, is_training, B, Lq, dev)
+        else:
+            # decode step: new tokens see the prompt and every earlier token (HybridCache path, :387-395);
+            # attention_mask (if given) spans past + new tokens as in HF generate
+            cls = torch.ones(B, Lq, dtype=torch.uint8, device=dev)
+            if attention_mask is not None:
+                cls = torch.where(attention_mask[:, -Lq:].to(dev) != 0, 1, 2).to(torch.uint8)
+            mask = KVMask(cls.contiguous())
+        h, all_h = self.language_model.model(hidden, mask, position_ids, output_hidden_states=bool(output_hidden_states),
+                                             cache=cache)
 
         target = self._targets(labels, attention_mask, B, Lq, dev)
         stash = {}
@@ -327,7 +341,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         if not return_dict:
             out = (logits,)
             return (loss,) + out if loss is not None else out
-        return SpatialVLACausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=None, hidden_states=all_h,
+        return SpatialVLACausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=cache, hidden_states=all_h,
                                                 attentions=None, image_hidden_states=image_features)
 
     def action_argmax(self):
@@ -336,40 +350,88 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         return self.last_stash.get("argmax")
 
     # ------------------------------------------------------------------ inference
-    @torch.no_grad()
-    def predict_action(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
-        """Greedy decode (reference :484-492).  Mathematically identical to the reference's
-        HybridCache decode: the prompt attends bidirectionally (:294) and every generated token attends to
-        the prompt and to earlier generated tokens only — realised as full re-forwards with per-key
-        classes (prompt keys class 0, generated keys class 1).  KV caching is §8(f)#2 (next)."""
-        ids = model_inputs["input_ids"]
+    def new_cache(self, batch_size: int, capacity: int) -> Gemma2KVCache:
+        """An empty KV cache for `capacity` tokens per sequence (prompt + generated)."""
+        w = self.language_model.lm_head.weight
+        return Gemma2KVCache(self.config.text_config, batch_size, capacity, w.device, w.dtype)
+
+    def _prompt_classes(self, am, B, P, dev):
+        if am is None:
+            return torch.zeros(B, P, dtype=torch.uint8, device=dev)
+        return torch.where(am.to(dev) != 0, 0, 2).to(torch.uint8).contiguous()
+
+    def _next_token(self, h, finished, eos):
+        """Greedy pick from the last position's logits (softcapped lm_head, argmax in its epilogue); sequences
+        that already emitted eos get pad, as HF generate does for finished sequences."""
+        B = h.shape[0]
+        stash = {}
+        tgt = torch.full((B,), -1, dtype=torch.int64, device=h.device)
+        self.language_model.head(h[:, -1:].contiguous(), tgt, stash)
+        nxt = stash["argmax"].view(B, 1)
+        if eos is not None:
+            nxt = torch.where(finished, torch.full_like(nxt, max(self.pad_token_id, 0)), nxt)
+            finished = finished | (nxt == eos)
+        return nxt, finished
+
+    def _predict_inputs(self, model_inputs):
         dev = self.language_model.lm_head.weight.device
-        ids = ids.to(dev)
+        ids = model_inputs["input_ids"].to(dev)
         pv = model_inputs.get("pixel_values")
         pv = pv.to(dev, torch.bfloat16) if pv is not None else None
         intr = model_inputs.get("intrinsic")
         intr = intr.to(dev, torch.bfloat16) if intr is not None else None
-        am = model_inputs.get("attention_mask")
+        return ids, pv, intr, model_inputs.get("attention_mask"), dev
+
+    @torch.no_grad()
+    def predict_action(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
+        """Greedy decode with a KV cache (reference :484-492 -> generate(max_new_tokens=256, do_sample=False)
+        with HybridCache).  Prefill: the prompt (image features merged, positions 1..P) attends bidirectionally
+        (:294) and fills the cache; decode: one token per step at position P+i+1 (:473-474), no pixel values
+        after step 0 (:475-476), attending to the prompt and every earlier generated token.  Stops when every
+        sequence has emitted eos or after max_new_tokens."""
+        ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         feats = self.get_image_features(pv, intr) if pv is not None else None
+        cache = self.new_cache(B, P + max_new_tokens)
+        lm = self.language_model.model
+        pos = (torch.arange(P, device=dev) + 1)[None]
+        h, _ = lm(self._merge_inputs(ids, feats), KVMask(self._prompt_classes(am, B, P, dev)), pos, cache=cache)
+        finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
+        nxt, finished = self._next_token(h, finished, eos)
+        out = [nxt]
+        step_cls = KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev))
+        for _ in range(max_new_tokens - 1):
+            if eos is not None and bool(finished.all()):
+                break
+            pos = torch.full((1, 1), cache.seen_tokens + 1, dtype=torch.int64, device=dev)
+            h, _ = lm(self._merge_inputs(nxt, None), step_cls, pos, cache=cache)
+            nxt, finished = self._next_token(h, finished, eos)
+            out.append(nxt)
+        return torch.cat(out, 1)
+
+    @torch.no_grad()
+    def predict_action_uncached(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
+        """The same greedy decode as full re-forwards over prompt + generated tokens (no cache): prompt keys
+        class 0, generated keys class 1.  Kept as the parity reference of the cached path."""
+        ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
+        eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
+        B, P = ids.shape
+        feats = self.get_image_features(pv, intr) if pv is not None else None
+        finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
         out = []
         cur = ids
         for _ in range(max_new_tokens):
+            if eos is not None and out and bool(finished.all()):
+                break
             Lc = cur.shape[1]
             cls = torch.ones(B, Lc, dtype=torch.uint8, device=dev)
-            cls[:, :P] = 0 if am is None else torch.where(am.to(dev) != 0, 0, 2).to(torch.uint8)
-            hidden = self._merge_inputs(cur, feats)
+            cls[:, :P] = self._prompt_classes(am, B, P, dev)
             pos = (torch.arange(Lc, device=dev) + 1)[None]
-            h, _ = self.language_model.model(hidden, KVMask(cls.contiguous()), pos)
-            stash = {}
-            tgt = torch.full((B * Lc,), -1, dtype=torch.int64, device=dev)
-            self.language_model.head(h, tgt, stash)
-            nxt = stash["argmax"].view(B, Lc)[:, -1:]
+            h, _ = self.language_model.model(self._merge_inputs(cur, feats), KVMask(cls.contiguous()), pos)
+            nxt, finished = self._next_token(h, finished, eos)
             out.append(nxt)
             cur = torch.cat([cur, nxt], 1)
-            if eos is not None and bool((nxt == eos).all()):
-                break
         return torch.cat(out, 1)
 
     @classmethod
