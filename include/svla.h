@@ -150,7 +150,8 @@ int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, float* lse, v
  *   k/v (b, j, h, d) at k + b*bsk + j*ldk + h*D + d               (cache rows, keys already rotated)
  *   out (b, t, h, d) at out + (b*Lq + t)*ldo + h*D + d
  * kv_class[b*ldc + j] as svla_attn_fwd (0 prompt key, 1 causal, 2 never visible); sliding window as there.
- * D in {64,128,192,256}; Hq/Hkv in {1,2,4}; (Hq/Hkv) * Lk * 4 bytes <= 128 KiB. */
+ * D in {64,128,256}; Hq/Hkv in {1,2,4}; any Lk (keys are split into 64-key chunks across workgroups).
+ * workspace: >= svla_attn_decode_workspace_bytes(B, Lq, Hq, Lk, D) bytes (fp32 chunk partials). */
 typedef struct {
   int32_t B, Lq, Lk, Hq, Hkv, D;
   int32_t sliding_window;
@@ -162,7 +163,9 @@ typedef struct {
   const uint8_t* kv_class; int64_t ldc;
 } svla_attn_decode_args;
 
-int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, void* stream);
+size_t svla_attn_decode_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32_t Lk, int32_t D);
+int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, float* workspace, size_t ws_bytes,
+                     void* stream);
 
 /* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
  * workspace: B*Hq*L fp32 (row dot(dO, O)). */

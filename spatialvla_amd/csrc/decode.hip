@@ -8,12 +8,14 @@
 // product, one division by the fp32 row sum at the end), so a cached step reproduces the full re-forward.
 //
 // Shape of the work: Lq (usually 1) new queries per sequence against Lk cached keys — a GEMV over the
-// K/V cache, HBM-bound (Lk * Hkv * D * 2 * 2 bytes per sequence), far from MFMA territory.  One workgroup
-// per (kv head, query, sequence): the Hq/Hkv query heads of a GQA group share every K/V row read.
-//  * scores: wave w takes keys w, w+4, ...; a lane holds D/64 contiguous elements of the key row (8-byte
-//    coalesced loads for D = 256) and the dot products finish with one butterfly per query head;
-//  * softmax: scores live in LDS ([group][Lk] fp32), block-wide max / sum;
-//  * PV: thread t owns output column d = t and walks the keys (a V row is one 512-byte coalesced read).
+// K/V cache, HBM-bound (Lk * Hkv * D * 2 * 2 bytes per sequence), far from MFMA territory.  At B = 1 one
+// workgroup per head would leave the chip idle, so the keys are split ("flash decoding"):
+//  * attn_decode_split_kernel, grid (ceil(Lk/64), Hkv, B*Lq): one workgroup per 64-key chunk and kv head;
+//    the Hq/Hkv query heads of the GQA group share every K/V row it reads.  Scores: 4 lanes per key, each
+//    with D/4 contiguous elements (16-B loads), q from LDS, two butterfly steps.  Chunk softmax: wave g owns
+//    query head g (64 keys = 64 lanes).  PV: D/8 lanes cover a V row with 16-B loads, 256/(D/8) row groups
+//    reduce through LDS.  Writes the chunk's (max, sum, unnormalised O) to the fp32 workspace;
+//  * attn_decode_combine_kernel, grid (Hq, B*Lq): rescales the chunks to the global max and normalises.
 #include "svla_common.h"
 
 namespace {
@@ -21,6 +23,7 @@ namespace {
 constexpr float MASKVAL = -3.3895313892515355e38f;  // torch.finfo(bfloat16).min, as the reference mask
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int NT = 256;
+constexpr int CH = 64;  // keys per chunk
 constexpr int MAXG = 4;
 
 __device__ __forceinline__ bool visible(int c, int kj, int qi, int window) {
@@ -29,147 +32,189 @@ __device__ __forceinline__ bool visible(int c, int kj, int qi, int window) {
   return v;
 }
 
-template <int E, int G>
-__global__ __launch_bounds__(NT) void attn_decode_kernel(svla_attn_decode_args a, bf16_t* __restrict__ out,
-                                                         int64_t ldo) {
-  extern __shared__ float sc[];  // [G][Lk] scores, then bf16-rounded probabilities
-  __shared__ float red[2 * NT / 64 * G];
-  const int hk = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+// workspace per (sequence-query bq, query head h, chunk c): [D] O partial, then {max, sum}
+__host__ __device__ inline int64_t ws_index(int64_t bq, int h, int c, int Hq, int nch, int D) {
+  return (((int64_t)bq * Hq + h) * nch + c) * (D + 2);
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(NT) void attn_decode_split_kernel(svla_attn_decode_args a, float* __restrict__ ws) {
+  constexpr int QP = D / 4;       // elements per score lane
+  constexpr int CPR = D / 8;      // 16-B chunks per V row
+  constexpr int RG = NT / CPR;    // V row groups
+  __shared__ float qs[G][D];
+  __shared__ float sc[G][CH];
+  __shared__ float red[RG][G][D];
+  const int c = blockIdx.x, hk = blockIdx.y, bq = blockIdx.z;
+  const int b = bq / a.Lq, t = bq % a.Lq;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int Lk = a.Lk, D = a.D;
-  const int qi = Lk - a.Lq + t;  // absolute (0-based) position of this query
+  const int nch = gridDim.x;
+  const int Lk = a.Lk;
+  const int qi = Lk - a.Lq + t;
   const bf16_t* qrow = (const bf16_t*)a.q + ((int64_t)b * a.Lq + t) * a.ldq + (int64_t)hk * G * D;
   const bf16_t* kb = (const bf16_t*)a.k + (int64_t)b * a.bsk + (int64_t)hk * D;
   const bf16_t* vb = (const bf16_t*)a.v + (int64_t)b * a.bsv + (int64_t)hk * D;
   const uint8_t* cls = a.kv_class ? a.kv_class + (int64_t)b * a.ldc : nullptr;
+  for (int i = tid; i < G * D; i += NT) qs[i / D][i % D] = bf2f(qrow[(i / D) * D + i % D]);
+  __syncthreads();
 
-  float qf[G][E];
+  // scores: key jj = tid/4, quarter p = tid%4 of the head dim
+  {
+    const int jj = tid >> 2, p = tid & 3;
+    const int j = c * CH + jj;
+    const bool jv = j < Lk;
+    float s[G];
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) s[g] = 0.f;
+    if (jv) {
+      const bf16_t* kr = kb + (int64_t)j * a.ldk + p * QP;
 #pragma unroll
-    for (int e = 0; e < E; ++e) qf[g][e] = bf2f(qrow[g * D + lane * E + e]);
-
-  // scores
-  for (int j = w; j < Lk; j += NT / 64) {
-    const bf16_t* kr = kb + (int64_t)j * a.ldk + lane * E;
-    float kf[E];
+      for (int e = 0; e < QP; e += 8) {
+        float kf[8];
+        unpack8(*reinterpret_cast<const u32x4*>(kr + e), kf);
 #pragma unroll
-    for (int e = 0; e < E; ++e) kf[e] = bf2f(kr[e]);
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s[g] = fmaf(qs[g][p * QP + e + i], kf[i], s[g]);
+      }
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      float s = 0.f;
+      s[g] += __shfl_xor(s[g], 1, 64);
+      s[g] += __shfl_xor(s[g], 2, 64);
+    }
+    if (p == 0) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) s = fmaf(qf[g][e], kf[e], s);
-      s = wave_sum(s);
-      if (lane == 0) {
-        float v = s * a.scale;
-        if (a.softcap > 0.f) v = a.softcap * fast_tanh(v / a.softcap);
-        if (!visible(cls ? cls[j] : 0, j, qi, a.sliding_window)) v = MASKVAL;
-        sc[g * Lk + j] = v;
+      for (int g = 0; g < G; ++g) {
+        float v = -INFINITY;
+        if (jv) {
+          v = s[g] * a.scale;
+          if (a.softcap > 0.f) v = a.softcap * fast_tanh(v / a.softcap);
+          if (!visible(cls ? cls[j] : 0, j, qi, a.sliding_window)) v = MASKVAL;
+        }
+        sc[g][jj] = v;
       }
     }
   }
   __syncthreads();
 
-  // softmax statistics per query head (block-wide)
-  float mx[G], inv[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float m = -INFINITY;
-    for (int j = tid; j < Lk; j += NT) m = fmaxf(m, sc[g * Lk + j]);
-    m = wave_max(m);
-    if (lane == 0) red[g * (NT / 64) + w] = m;
+  // chunk softmax: wave g <-> query head g
+  if (w < G) {
+    const float v = sc[w][lane];
+    const float m = wave_max(v);
+    const float pr = exp2f((v - m) * LOG2E);
+    const float l = wave_sum(pr);
+    sc[w][lane] = round_bf(pr);  // P enters the PV product as bf16 (the MFMA operand of svla_attn_fwd)
+    if (lane == 0) {
+      float* o = ws + ws_index(bq, hk * G + w, c, a.Hq, nch, D);
+      o[D] = m;
+      o[D + 1] = l;
+    }
   }
   __syncthreads();
+
+  // PV over the chunk
+  {
+    const int cc = tid % CPR, rg = tid / CPR;
+    float acc[G][8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float m = red[g * (NT / 64)];
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[g * (NT / 64) + i]);
-    mx[g] = m;
-    float l = 0.f;
-    for (int j = tid; j < Lk; j += NT) {
-      const float p = exp2f((sc[g * Lk + j] - m) * LOG2E);
-      l += p;
-      sc[g * Lk + j] = round_bf(p);  // P enters the PV product as bf16 (the MFMA operand of svla_attn_fwd)
+      for (int i = 0; i < 8; ++i) acc[g][i] = 0.f;
+    for (int jj = rg; jj < CH; jj += RG) {
+      const int j = c * CH + jj;
+      if (j >= Lk) break;
+      float vf[8];
+      unpack8(*reinterpret_cast<const u32x4*>(vb + (int64_t)j * a.ldv + cc * 8), vf);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pj = sc[g][jj];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[g][i] = fmaf(pj, vf[i], acc[g][i]);
+      }
     }
-    l = wave_sum(l);
-    if (lane == 0) red[(NT / 64) * G + g * (NT / 64) + w] = l;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[rg][g][cc * 8 + i] = acc[g][i];
   }
   __syncthreads();
+  for (int i = tid; i < G * D; i += NT) {
+    const int g = i / D, d = i % D;
+    float v = 0.f;
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float l = 0.f;
-#pragma unroll
-    for (int i = 0; i < NT / 64; ++i) l += red[(NT / 64) * G + g * (NT / 64) + i];
-    inv[g] = 1.0f / l;
+    for (int r = 0; r < RG; ++r) v += red[r][g][d];
+    ws[ws_index(bq, hk * G + g, c, a.Hq, nch, D) + d] = v;
   }
-
-  // O = P V, thread tid owns column d = tid
-  if (tid < D) {
-    float acc[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] = 0.f;
-    const bf16_t* vc = vb + tid;
-    for (int j = 0; j < Lk; ++j) {
-      const float vv = bf2f(vc[(int64_t)j * a.ldv]);
-#pragma unroll
-      for (int g = 0; g < G; ++g) acc[g] = fmaf(sc[g * Lk + j], vv, acc[g]);
-    }
-    bf16_t* orow = out + ((int64_t)b * a.Lq + t) * ldo + (int64_t)hk * G * D + tid;
-#pragma unroll
-    for (int g = 0; g < G; ++g) orow[g * D] = f2bf(acc[g] * inv[g]);
-  }
-  (void)mx;
 }
 
-template <int E, int G>
-int launch(const svla_attn_decode_args& a, bf16_t* out, int64_t ldo, hipStream_t s) {
-  const size_t lds = (size_t)G * a.Lk * sizeof(float);
-  if (lds > 48 * 1024) {
-    static bool done = false;  // one flag per instantiation
-    if (!done) {
-      (void)hipFuncSetAttribute((const void*)attn_decode_kernel<E, G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          128 * 1024);
-      done = true;
-    }
+template <int D>
+__global__ __launch_bounds__(D) void attn_decode_combine_kernel(int Hq, int nch, const float* __restrict__ ws,
+                                                                 bf16_t* __restrict__ out, int64_t ldo) {
+  const int h = blockIdx.x, bq = blockIdx.y, d = threadIdx.x;
+  float M = -INFINITY;
+  for (int c = 0; c < nch; ++c) M = fmaxf(M, ws[ws_index(bq, h, c, Hq, nch, D) + D]);
+  float l = 0.f, acc = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    const float* o = ws + ws_index(bq, h, c, Hq, nch, D);
+    const float f = __expf(o[D] - M);  // chunks whose keys are all masked (max = bf16 min) drop out
+    l = fmaf(o[D + 1], f, l);
+    acc = fmaf(o[d], f, acc);
   }
-  hipLaunchKernelGGL((attn_decode_kernel<E, G>), dim3(a.Hkv, a.Lq, a.B), dim3(NT), lds, s, a, out, ldo);
-  return svla::check_launch("attn_decode");
+  out[(int64_t)bq * ldo + (int64_t)h * D + d] = f2bf(acc / l);
 }
 
-template <int E>
-int launch_g(const svla_attn_decode_args& a, bf16_t* out, int64_t ldo, hipStream_t s) {
+template <int D, int G>
+int launch(const svla_attn_decode_args& a, bf16_t* out, int64_t ldo, float* ws, hipStream_t s) {
+  const int nch = (a.Lk + CH - 1) / CH;
+  hipLaunchKernelGGL((attn_decode_split_kernel<D, G>), dim3(nch, a.Hkv, a.B * a.Lq), dim3(NT), 0, s, a, ws);
+  if (int rc = svla::check_launch("attn_decode")) return rc;
+  hipLaunchKernelGGL((attn_decode_combine_kernel<D>), dim3(a.Hq, a.B * a.Lq), dim3(D), 0, s, a.Hq, nch, ws, out,
+                     ldo);
+  return svla::check_launch("attn_decode combine");
+}
+
+template <int D>
+int launch_g(const svla_attn_decode_args& a, bf16_t* out, int64_t ldo, float* ws, hipStream_t s) {
   switch (a.Hq / a.Hkv) {
-    case 1: return launch<E, 1>(a, out, ldo, s);
-    case 2: return launch<E, 2>(a, out, ldo, s);
-    default: return launch<E, 4>(a, out, ldo, s);
+    case 1: return launch<D, 1>(a, out, ldo, ws, s);
+    case 2: return launch<D, 2>(a, out, ldo, ws, s);
+    default: return launch<D, 4>(a, out, ldo, ws, s);
   }
 }
 
 }  // namespace
 
-extern "C" int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, void* stream) {
+extern "C" size_t svla_attn_decode_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32_t Lk, int32_t D) {
+  const int64_t nch = ((int64_t)Lk + CH - 1) / CH;
+  return (size_t)B * Lq * Hq * nch * (D + 2) * sizeof(float);
+}
+
+extern "C" int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, float* workspace,
+                                size_t ws_bytes, void* stream) {
   SVLA_CHECK_ARG(a && out, "attn_decode: NULL args/out");
   SVLA_CHECK_ARG(a->q && a->k && a->v, "attn_decode: NULL q/k/v");
   SVLA_CHECK_ARG(a->B > 0 && a->Lq > 0 && a->Lk >= a->Lq && a->Hkv > 0 && a->Hq % a->Hkv == 0,
                  "attn_decode: bad B/Lq/Lk/Hq/Hkv");
   const int G = a->Hq / a->Hkv;
   SVLA_CHECK_ARG(G == 1 || G == 2 || G == MAXG, "attn_decode: GQA group must be 1, 2 or 4");
-  SVLA_CHECK_ARG(a->D % 64 == 0 && a->D >= 64 && a->D <= 256, "attn_decode: head_dim must be 64/128/192/256");
-  SVLA_CHECK_ARG((int64_t)G * a->Lk * 4 <= 128 * 1024, "attn_decode: group * Lk too large for the LDS scores");
+  SVLA_CHECK_ARG(a->D == 64 || a->D == 128 || a->D == 256, "attn_decode: head_dim must be 64, 128 or 256");
+  SVLA_CHECK_ARG(a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0 && a->bsk % 8 == 0 && a->bsv % 8 == 0,
+                 "attn_decode: strides must be multiples of 8");
+  SVLA_CHECK_ARG(((uintptr_t)a->k & 15) == 0 && ((uintptr_t)a->v & 15) == 0, "attn_decode: k/v must be 16-B aligned");
   SVLA_CHECK_ARG(a->ldq >= (int64_t)a->Hq * a->D && a->ldk >= (int64_t)a->Hkv * a->D &&
                      a->ldv >= (int64_t)a->Hkv * a->D && ldo >= (int64_t)a->Hq * a->D,
                  "attn_decode: row strides smaller than the head block");
   SVLA_CHECK_ARG(a->B == 1 || (a->bsk >= (int64_t)a->Lk * a->ldk && a->bsv >= (int64_t)a->Lk * a->ldv),
                  "attn_decode: batch strides overlap the cached rows");
   SVLA_CHECK_ARG(!a->kv_class || a->ldc >= a->Lk, "attn_decode: kv_class row stride < Lk");
+  SVLA_CHECK_ARG(workspace && ws_bytes >= svla_attn_decode_workspace_bytes(a->B, a->Lq, a->Hq, a->Lk, a->D),
+                 "attn_decode: workspace smaller than svla_attn_decode_workspace_bytes()");
   hipStream_t s = (hipStream_t)stream;
   bf16_t* o = (bf16_t*)out;
-  switch (a->D / 64) {
-    case 1: return launch_g<1>(*a, o, ldo, s);
-    case 2: return launch_g<2>(*a, o, ldo, s);
-    case 3: return launch_g<3>(*a, o, ldo, s);
-    default: return launch_g<4>(*a, o, ldo, s);
+  switch (a->D) {
+    case 64: return launch_g<64>(*a, o, ldo, workspace, s);
+    case 128: return launch_g<128>(*a, o, ldo, workspace, s);
+    default: return launch_g<256>(*a, o, ldo, workspace, s);
   }
 }

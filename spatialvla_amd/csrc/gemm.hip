@@ -1396,6 +1396,88 @@ __global__ void epi_pass_kernel(int kind, int64_t M, int64_t N, bf16_t* __restri
   *reinterpret_cast<u32x4*>(c + m * ldc + n) = pack8(v);
 }
 
+// Small-M GEMM (M <= 8: the decode step of greedy generation, one or a few token rows): y = x W^T streams
+// every weight row once from HBM, so it is a GEMV — MFMA tiles of 256 rows would run at M/256 occupancy and
+// a 256x256 grid over N leaves most CUs idle.  One wave owns RW output rows (or RW gate/up row pairs for
+// GEGLU): each lane reads 16-B chunks of the weight rows (a 1 KiB coalesced sweep per row per step), the M
+// activation rows come through L1/L2 (a few KiB, shared by every wave), fp32 dot products finish with a
+// butterfly.  Epilogues: STORE, GEGLU (the fused epilogue's rounding: g, u, gelu(g) rounded to bf16), and
+// ROPE by the in-place pass after the store.
+constexpr int GEMV_MAXM = 8;
+
+template <int RW, bool GEGLU>
+__global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ x,
+                                                   int64_t ldx, const bf16_t* __restrict__ w0,
+                                                   const bf16_t* __restrict__ w1, int64_t ldw,
+                                                   bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
+  constexpr int NW = GEGLU ? 2 : 1;  // weight rows per output row
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = wave * RW;
+  if (r0 >= rows) return;
+  float acc[RW][NW][GEMV_MAXM];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) acc[r][q][m] = 0.f;
+  for (int64_t k = (int64_t)lane * 8; k < K; k += 512) {
+    float wf[RW][NW][8];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int64_t n = r0 + r < rows ? r0 + r : rows - 1;
+      unpack8(*reinterpret_cast<const u32x4*>(w0 + n * ldw + k), wf[r][0]);
+      if constexpr (GEGLU) unpack8(*reinterpret_cast<const u32x4*>(w1 + n * ldw + k), wf[r][NW - 1]);
+    }
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+      if (m < M) {
+        float xf[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+#pragma unroll
+          for (int q = 0; q < NW; ++q)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[r][q][m] = fmaf(wf[r][q][j], xf[j], acc[r][q][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) {
+    if (m < M) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        float v[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v[q] = wave_sum(acc[r][q][m]);
+        const int64_t n = r0 + r;
+        if (lane == 0 && n < rows) {
+          if constexpr (GEGLU) {
+            const float g = round_bf(v[0]), u = round_bf(v[1]);
+            c[m * ldc + n] = f2bf(round_bf(gelu_tanh(g)) * u);
+            ((bf16_t*)E.out1)[m * E.ld_out1 + n] = f2bf(g);
+            ((bf16_t*)E.out2)[m * E.ld_out2 + n] = f2bf(u);
+          } else {
+            c[m * ldc + n] = f2bf(v[0]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int RW, bool GEGLU>
+int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
+                int64_t ldc, const svla_epilogue& E, hipStream_t s) {
+  const int64_t waves = (rows + RW - 1) / RW;
+  hipLaunchKernelGGL((gemv_kernel<RW, GEGLU>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, M, rows, K,
+                     (const bf16_t*)A.ptr[0], A.ld, (const bf16_t*)B.ptr[0],
+                     (const bf16_t*)(GEGLU ? B.ptr[1] : B.ptr[0]), B.ld, c, ldc, E);
+  return 0;
+}
+
 // dispatch choice (A/B tuning knob): 0 = auto (plain TN stores via hipBLASLt; 4-wave kernel for long-K GEMMs
 // with more than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
 // without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = auto without
@@ -1628,6 +1710,35 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   // (+31%), softcap-CE (+9%) and RoPE (+2%) stay on the 8-wave kernel, as do short-K / sub-wave shapes
   // plain TN store (both operands K-contiguous, no epilogue, no segments): hipBLASLt (blaslt.hip), in the auto
   // variant only; 5 = hand-written kernels for everything
+  // decode-sized M: the GEMV path (STORE / GEGLU / ROPE, both operands K-contiguous, plain C)
+  {
+    const bool ek_ok = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_GEGLU ||
+                       (epi->kind == SVLA_EPI_ROPE && epi->rope_D % 16 == 0);
+    const bool b_ok = epi->kind == SVLA_EPI_GEGLU
+                          ? (B->nseg == 2 && B->seg_start[1] == N / 2 && aligned16(B->ptr[1]))
+                          : (B->nseg == 1);
+    if (M <= GEMV_MAXM && ek_ok && b_ok && g_variant != 5 && !epi->accumulate && epi->alpha == 1.0f &&
+        A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && A->nseg == 1 && K % 8 == 0 &&
+        A->ld % 8 == 0 && B->ld % 8 == 0 && (A->r_valid == 0 || A->r_valid >= M) &&
+        (A->k_valid == 0 || A->k_valid >= K) && (B->r_valid == 0 || B->r_valid >= N) &&
+        (B->k_valid == 0 || B->k_valid >= K) && c_nseg == 1 && C.start[0] == 0 && aligned16(A->ptr[0]) &&
+        aligned16(B->ptr[0])) {
+      bf16_t* c0 = C.ptr[0];
+      if (epi->kind == SVLA_EPI_GEGLU) {
+        launch_gemv<1, true>((int)M, N / 2, K, *A, *B, c0, ldc, *epi, s);
+      } else if (K > 4096 || N < 8192) {
+        launch_gemv<1, false>((int)M, N, K, *A, *B, c0, ldc, *epi, s);
+      } else {
+        launch_gemv<2, false>((int)M, N, K, *A, *B, c0, ldc, *epi, s);
+      }
+      if (epi->kind == SVLA_EPI_ROPE) {
+        const int64_t work = M * (epi->rope_cols / epi->rope_D) * (epi->rope_D / 16);
+        hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M, c0, ldc,
+                           *epi);
+      }
+      return svla::check_launch("gemm (small-M GEMV)");
+    }
+  }
   auto whole = [](const svla_operand* o, int64_t R, int64_t Kx) {
     return o->nseg == 1 && (o->r_valid == 0 || o->r_valid >= R) && (o->k_valid == 0 || o->k_valid >= Kx);
   };

@@ -335,7 +335,10 @@ def attn_decode(q, Lq, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_clas
     a.v, a.ldv, a.bsv = v_cache.data_ptr(), v_cache.stride(1), v_cache.stride(0)
     a.kv_class = _ptr(kv_class)
     a.ldc = kv_class.stride(0) if kv_class is not None else 0
-    L.check(L.lib().svla_attn_decode(ctypes.byref(a), out.data_ptr(), out.stride(0), _stream()), "attn_decode")
+    nb = L.lib().svla_attn_decode_workspace_bytes(B, Lq, Hq, Lk, D)
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=q.device)
+    L.check(L.lib().svla_attn_decode(ctypes.byref(a), out.data_ptr(), out.stride(0), ws.data_ptr(), nb, _stream()),
+            "attn_decode")
 
 
 def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):

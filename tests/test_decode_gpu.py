@@ -21,6 +21,7 @@ BF = torch.bfloat16
     (256, 8, 2, 1000, 2, 0, 50.0),    # GQA group of 4
     (128, 2, 2, 77, 1, 16, 0.0),      # sliding window masks the far keys
     (64, 2, 1, 129, 3, 0, 0.0),
+    (256, 8, 4, 9000, 1, 4096, 50.0),  # longer than the LDS-resident flash class array allows
     (256, 8, 4, 4500, 1, 4096, 50.0),  # past the Gemma2 sliding window
 ])
 def test_attn_decode_kernel(cuda, D, Hq, Hkv, Lk, Lq, window, cap):
@@ -42,7 +43,7 @@ def test_attn_decode_kernel(cuda, D, Hq, Hkv, Lk, Lq, window, cap):
     ref = _ref_attn(qfull.view(B, Lk, Hq, D), kc[:, :Lk].view(B, Lk, Hkv, D), vc[:, :Lk].view(B, Lk, Hkv, D),
                     1 / 16, cap, cls[:, :Lk], window)[:, Lk - Lq:]
     assert H.rel_l2(out.view(B, Lq, Hq, D), ref) < 1e-2
-    if D == 256 and Lk <= 8192:
+    if D == 256 and Lk <= 4608:
         # the same rows from the prefill flash kernel (what the uncached re-forward computes)
         qkv = torch.cat([qfull.view(B * Lk, -1), kc[:, :Lk].reshape(B * Lk, kd), vc[:, :Lk].reshape(B * Lk, kd)], 1)
         cls_l = cls[:, :Lk].contiguous()  # held: attn_args keeps only its pointer
@@ -115,3 +116,60 @@ def test_forward_past_key_values_matches_reforward(cuda):
     assert H.rel_l2(o2.logits, ref[:, P:P + 1]) < H.LOGITS_TOL
     assert H.rel_l2(o3.logits, ref[:, P + 1:P + 3]) < H.LOGITS_TOL
     assert torch.equal(o3.logits.float().argmax(-1), ref[:, P + 1:P + 3].float().argmax(-1))
+
+
+# ------------------------------------------------------------------ small-M GEMMs of the decode step (GEMV path)
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 2304), (3, 2304, 9216), (8, 4096, 2304), (2, 265347 // 64 * 64, 512)])
+def test_gemv_store(cuda, M, N, K):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(3)
+    x, w = _r(M, K), _r(N, K, scale=0.05)
+    out = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], out)
+    ref = x.float() @ w.float().t()
+    assert H.rel_l2(out, ref) < 1e-2
+    # the bf16 result matches the MFMA path on the same rows (equal up to fp32 summation order)
+    big = torch.empty(64, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(torch.cat([x, _r(64 - M, K)]), [w], big)
+    assert (out.float() - big[:M].float()).abs().max() <= 2 ** -6 * ref.abs().max()
+
+
+@pytest.mark.parametrize("M", [1, 2, 5])
+def test_gemv_geglu(cuda, M):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(4)
+    K, I = 2304, 1024
+    x, wg, wu = _r(M, K), _r(I, K, scale=0.05), _r(I, K, scale=0.05)
+    h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    Kn.linear_geglu_fwd(x, wg, wu, h, g, u)
+    g_ref = (x.float() @ wg.float().t()).to(BF)
+    u_ref = (x.float() @ wu.float().t()).to(BF)
+    h_ref = (torch.nn.functional.gelu(g_ref.float(), approximate="tanh").to(BF).float() * u_ref.float())
+    assert H.rel_l2(g, g_ref) < 1e-2 and H.rel_l2(u, u_ref) < 1e-2
+    assert H.rel_l2(h, h_ref) < 1e-2
+    # h is exactly the fused epilogue's rounding applied to the kernel's own g, u
+    h_own = (torch.nn.functional.gelu(g.float(), approximate="tanh").to(BF).float() * u.float()).to(BF)
+    assert (h.float() - h_own.float()).abs().max() <= 1e-2 * h_own.float().abs().max()
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_gemv_rope(cuda, M):
+    """The decode-step QKV projection: GEMV store + in-place RoPE pass, bitwise the reference bf16 RoPE applied
+    to the GEMV's own output."""
+    from spatialvla_amd import kernels as Kn, _lib as L_
+    from test_kernels_gpu import _rope_bf16
+    torch.manual_seed(5)
+    D, Hq, Hkv, K = 256, 8, 4, 2304
+    N = (Hq + 2 * Hkv) * D
+    nrot = (Hq + Hkv) * D
+    x, w = _r(M, K), _r(N, K, scale=0.05)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    f = (torch.arange(300, 300 + M, device=cuda).float() + 1)[:, None] * inv[None]
+    cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
+    plain = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], plain)
+    rot = torch.empty_like(plain)
+    Kn.linear_fwd(x, [w], rot, kind=L_.EPI_ROPE, rope=(cos, sin, M, D, nrot))
+    ref = plain.clone()
+    ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(1, M, Hq + Hkv, D), cos, sin).view(M, nrot)
+    assert torch.equal(rot, ref)
