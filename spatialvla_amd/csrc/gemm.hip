@@ -1405,11 +1405,19 @@ __global__ void epi_pass_kernel(int kind, int64_t M, int64_t N, bf16_t* __restri
 // ROPE by the in-place pass after the store.
 constexpr int GEMV_MAXM = 8;
 
+// weight row n of a B operand with up to 4 SEG_OUTER segments (q|k|v or gate|up kept in separate tensors)
+__device__ __forceinline__ const bf16_t* gemv_row(const svla_operand& B, int64_t n) {
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < B.nseg && n >= B.seg_start[i]) s = i;
+  return (const bf16_t*)B.ptr[s] + (n - B.seg_start[s]) * B.ld;
+}
+
 template <int RW, bool GEGLU>
 __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ x,
-                                                   int64_t ldx, const bf16_t* __restrict__ w0,
-                                                   const bf16_t* __restrict__ w1, int64_t ldw,
-                                                   bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
+                                                   int64_t ldx, svla_operand B, bf16_t* __restrict__ c,
+                                                   int64_t ldc, svla_epilogue E) {
   constexpr int NW = GEGLU ? 2 : 1;  // weight rows per output row
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1427,8 +1435,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
       const int64_t n = r0 + r < rows ? r0 + r : rows - 1;
-      unpack8(*reinterpret_cast<const u32x4*>(w0 + n * ldw + k), wf[r][0]);
-      if constexpr (GEGLU) unpack8(*reinterpret_cast<const u32x4*>(w1 + n * ldw + k), wf[r][NW - 1]);
+      if constexpr (GEGLU) {  // gate row n in ptr[0], up row n in ptr[1]
+        unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[0] + n * B.ld + k), wf[r][0]);
+        unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[1] + n * B.ld + k), wf[r][NW - 1]);
+      } else {
+        unpack8(*reinterpret_cast<const u32x4*>(gemv_row(B, n) + k), wf[r][0]);
+      }
     }
 #pragma unroll
     for (int m = 0; m < GEMV_MAXM; ++m) {
@@ -1468,13 +1480,88 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
   }
 }
 
+// SOFTCAP_CE at small M (the lm_head of a decode step): one wave per 128-column tile of the vocab walks its
+// rows two at a time and keeps the tile's online-softmax partials {max, sumexp, argmax} per activation row in
+// registers — the row_stats layout of the MFMA epilogue (logits rounded to bf16, softcapped, rounded again).
+__global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int64_t K, const bf16_t* __restrict__ x,
+                                                           int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
+                                                           bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
+  constexpr int RW = 2;
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ntn = (N + 127) / 128;
+  if (tile >= ntn) return;
+  const float cap = E.cap, icap = 1.0f / E.cap;
+  float mx[GEMV_MAXM], se[GEMV_MAXM];
+  int am[GEMV_MAXM];
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) { mx[m] = -INFINITY; se[m] = 0.f; am[m] = 0x7fffffff; }
+  const int64_t nend = (tile + 1) * 128 < N ? (tile + 1) * 128 : N;
+  for (int64_t r0 = tile * 128; r0 < nend; r0 += RW) {
+    float acc[RW][GEMV_MAXM];
+#pragma unroll
+    for (int r = 0; r < RW; ++r)
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) acc[r][m] = 0.f;
+    for (int64_t k = (int64_t)lane * 8; k < K; k += 512) {
+      float wf[RW][8];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int64_t n = r0 + r < nend ? r0 + r : nend - 1;
+        unpack8(*reinterpret_cast<const u32x4*>(w + n * ldw + k), wf[r]);
+      }
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) {
+        if (m < M) {
+          float xf[8];
+          unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[r][m] = fmaf(wf[r][j], xf[j], acc[r][m]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+      if (m < M) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const int64_t n = r0 + r;
+          const float v = round_bf(cap * fast_tanh(round_bf(wave_sum(acc[r][m])) * icap));
+          if (n < nend) {
+            if (lane == 0) c[m * ldc + n] = f2bf(v);
+            if (v > mx[m]) {
+              se[m] = se[m] * __expf(mx[m] - v) + 1.0f;
+              mx[m] = v;
+              am[m] = (int)n;
+            } else {
+              se[m] += __expf(v - mx[m]);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+      if (m < M) {
+        float* rs = E.row_stats + (m * ntn + tile) * 3;
+        rs[0] = mx[m];
+        rs[1] = se[m];
+        rs[2] = __int_as_float(am[m]);
+      }
+    }
+  }
+}
+
 template <int RW, bool GEGLU>
 int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
                 int64_t ldc, const svla_epilogue& E, hipStream_t s) {
   const int64_t waves = (rows + RW - 1) / RW;
   hipLaunchKernelGGL((gemv_kernel<RW, GEGLU>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, M, rows, K,
-                     (const bf16_t*)A.ptr[0], A.ld, (const bf16_t*)B.ptr[0],
-                     (const bf16_t*)(GEGLU ? B.ptr[1] : B.ptr[0]), B.ld, c, ldc, E);
+                     (const bf16_t*)A.ptr[0], A.ld, B, c, ldc, E);
   return 0;
 }
 
@@ -1713,10 +1800,11 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   // decode-sized M: the GEMV path (STORE / GEGLU / ROPE, both operands K-contiguous, plain C)
   {
     const bool ek_ok = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_GEGLU ||
-                       (epi->kind == SVLA_EPI_ROPE && epi->rope_D % 16 == 0);
-    const bool b_ok = epi->kind == SVLA_EPI_GEGLU
-                          ? (B->nseg == 2 && B->seg_start[1] == N / 2 && aligned16(B->ptr[1]))
-                          : (B->nseg == 1);
+                       epi->kind == SVLA_EPI_SOFTCAP_CE || (epi->kind == SVLA_EPI_ROPE && epi->rope_D % 16 == 0);
+    bool b_ok = epi->kind == SVLA_EPI_GEGLU ? (B->nseg == 2 && B->seg_start[1] == N / 2)
+                                            : (B->nseg == 1 || (B->seg_dim == SVLA_SEG_OUTER &&
+                                                                epi->kind != SVLA_EPI_SOFTCAP_CE));
+    for (int i = 0; i < B->nseg; ++i) b_ok = b_ok && aligned16(B->ptr[i]);
     if (M <= GEMV_MAXM && ek_ok && b_ok && g_variant != 5 && !epi->accumulate && epi->alpha == 1.0f &&
         A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && A->nseg == 1 && K % 8 == 0 &&
         A->ld % 8 == 0 && B->ld % 8 == 0 && (A->r_valid == 0 || A->r_valid >= M) &&
@@ -1724,7 +1812,11 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
         (B->k_valid == 0 || B->k_valid >= K) && c_nseg == 1 && C.start[0] == 0 && aligned16(A->ptr[0]) &&
         aligned16(B->ptr[0])) {
       bf16_t* c0 = C.ptr[0];
-      if (epi->kind == SVLA_EPI_GEGLU) {
+      if (epi->kind == SVLA_EPI_SOFTCAP_CE) {
+        const int64_t ntn = (N + 127) / 128;
+        hipLaunchKernelGGL(gemv_softcap_kernel, dim3((unsigned)((ntn + 3) / 4)), dim3(256), 0, s, (int)M, N, K,
+                           (const bf16_t*)A->ptr[0], A->ld, (const bf16_t*)B->ptr[0], B->ld, c0, ldc, *epi);
+      } else if (epi->kind == SVLA_EPI_GEGLU) {
         launch_gemv<1, true>((int)M, N / 2, K, *A, *B, c0, ldc, *epi, s);
       } else if (K > 4096 || N < 8192) {
         launch_gemv<1, false>((int)M, N, K, *A, *B, c0, ldc, *epi, s);

@@ -10,6 +10,7 @@ SigLIP, Ego3D, projector, embedding merge, 26 Gemma2 layers, softcapped lm_head 
 The frozen ZoeDepth estimator (and its bicubic resampling) stays on stock PyTorch-ROCm ops under
 no_grad — it is not a north-star kernel target.
 """
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple, Union
 
@@ -136,6 +137,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         else:
             self.spatial_embed_tokens = None
         self.pad_token_id = config.pad_token_id if config.pad_token_id is not None else -1
+        # predict_action replays each decode step from a captured HIP graph (SVLA_DECODE_GRAPHS=0: eager launches)
+        self.decode_graphs = os.environ.get("SVLA_DECODE_GRAPHS", "1") != "0"
         self.strict_checks = True   # reference raises on an image-token count mismatch (needs a host sync)
         self.last_stash = {}
         self.post_init()
@@ -382,6 +385,52 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         intr = intr.to(dev, torch.bfloat16) if intr is not None else None
         return ids, pv, intr, model_inputs.get("attention_mask"), dev
 
+    def _decode_state(self, B: int, capacity: int, dev):
+        """Persistent decode state per (batch, capacity): the KV cache, the static token buffer the captured
+        graphs read, and the graphs themselves keyed by cache position.  Reused across predict_action calls, so
+        a control loop with a fixed prompt length replays the same graphs every call."""
+        states = self.__dict__.setdefault("_svla_decode_states", {})
+        key = (B, capacity, str(dev))
+        st = states.get(key)
+        if st is None:
+            st = {"cache": self.new_cache(B, capacity), "graphs": {},
+                  "tok": torch.zeros(B, 1, dtype=torch.int64, device=dev),
+                  "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev))}
+            states[key] = st
+        return st
+
+    def _decode_body(self, st, p0):
+        """One decode step at cache position p0: the token in st["tok"] -> argmax of its logits [B]."""
+        tok, cache = st["tok"], st["cache"]
+        pos = torch.full((1, 1), p0 + 1, dtype=torch.int64, device=tok.device)  # 1-indexed (:372, :473-474)
+        h, _ = self.language_model.model(self._merge_inputs(tok, None), st["cls"], pos, cache=cache)
+        stash = {}
+        tgt = torch.full((tok.shape[0],), -1, dtype=torch.int64, device=tok.device)
+        self.language_model.head(h[:, -1:].contiguous(), tgt, stash)
+        return stash["argmax"]
+
+    def _decode_step_graph(self, st, p0):
+        """The decode step as a HIP graph (torch.cuda.CUDAGraph on ROCm), captured once per cache position: a
+        B=1 step is ~300 small launches whose host-side cost exceeds their GPU time, and a graph replays them
+        as one submission.  Positions, cache rows and sequence lengths are baked into each graph."""
+        cache = st["cache"]
+        g = st["graphs"].get(p0)
+        if g is None:
+            side = torch.cuda.Stream(device=st["tok"].device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # eager warm-up (lazy kernel attributes); rewrites row p0 identically
+                self._decode_body(st, p0)
+            cache.seen_tokens = p0
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._decode_body(st, p0)
+            cache.seen_tokens = p0
+            g = st["graphs"][p0] = (graph, out)
+        g[0].replay()
+        cache.seen_tokens = p0 + 1
+        return g[1]
+
     @torch.no_grad()
     def predict_action(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
         """Greedy decode with a KV cache (reference :484-492 -> generate(max_new_tokens=256, do_sample=False)
@@ -393,20 +442,29 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         feats = self.get_image_features(pv, intr) if pv is not None else None
-        cache = self.new_cache(B, P + max_new_tokens)
+        graphs = self.decode_graphs and dev.type == "cuda"
+        st = self._decode_state(B, P + max_new_tokens, dev)
+        cache = st["cache"]
+        cache.seen_tokens = 0
         lm = self.language_model.model
         pos = (torch.arange(P, device=dev) + 1)[None]
         h, _ = lm(self._merge_inputs(ids, feats), KVMask(self._prompt_classes(am, B, P, dev)), pos, cache=cache)
         finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
         nxt, finished = self._next_token(h, finished, eos)
         out = [nxt]
-        step_cls = KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev))
+        pad = torch.full_like(nxt, max(self.pad_token_id, 0))
         for _ in range(max_new_tokens - 1):
             if eos is not None and bool(finished.all()):
                 break
-            pos = torch.full((1, 1), cache.seen_tokens + 1, dtype=torch.int64, device=dev)
-            h, _ = lm(self._merge_inputs(nxt, None), step_cls, pos, cache=cache)
-            nxt, finished = self._next_token(h, finished, eos)
+            st["tok"].copy_(nxt)
+            p0 = cache.seen_tokens
+            am_ = self._decode_step_graph(st, p0) if graphs else self._decode_body(st, p0)
+            if not graphs:
+                cache.seen_tokens = p0 + 1
+            nxt = am_.view(B, 1).clone()
+            if eos is not None:
+                nxt = torch.where(finished, pad, nxt)
+                finished = finished | (nxt == eos)
             out.append(nxt)
         return torch.cat(out, 1)
 

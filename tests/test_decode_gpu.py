@@ -75,10 +75,16 @@ def test_predict_action_cached_equals_uncached(cuda):
     model, g = _tiny_model(cuda)
     ids = g["in.input_ids"][:, :-13]  # prompt only (prefix)
     inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    model.decode_graphs = False
     cached = model.predict_action(inputs, max_new_tokens=8, eos_token_id=-1)
     full = model.predict_action_uncached(inputs, max_new_tokens=8, eos_token_id=-1)
     assert cached.shape == (2, 8)
     assert torch.equal(cached, full), (cached, full)
+    # the same steps replayed from captured HIP graphs: first call captures, second call replays
+    model.decode_graphs = True
+    g1 = model.predict_action(inputs, max_new_tokens=8, eos_token_id=-1)
+    g2 = model.predict_action(inputs, max_new_tokens=8, eos_token_id=-1)
+    assert torch.equal(g1, cached) and torch.equal(g2, cached)
 
 
 def test_predict_action_eos_pads_finished(cuda):
@@ -173,3 +179,8 @@ def test_gemv_rope(cuda, M):
     ref = plain.clone()
     ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(1, M, Hq + Hkv, D), cos, sin).view(M, nrot)
     assert torch.equal(rot, ref)
+    # q, k, v weights in three separate tensors (a B operand of 3 segments) give the same bits
+    wq, wk, wv = (t.clone() for t in torch.split(w, [Hq * D, Hkv * D, Hkv * D]))
+    seg = torch.empty_like(plain)
+    Kn.linear_fwd(x, [wq, wk, wv], seg, kind=L_.EPI_ROPE, rope=(cos, sin, M, D, nrot))
+    assert torch.equal(seg, ref)
