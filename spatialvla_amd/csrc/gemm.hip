@@ -1430,6 +1430,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
     for (int q = 0; q < NW; ++q)
 #pragma unroll
       for (int m = 0; m < GEMV_MAXM; ++m) acc[r][q][m] = 0.f;
+#pragma unroll 4
   for (int64_t k = (int64_t)lane * 8; k < K; k += 512) {
     float wf[RW][NW][8];
 #pragma unroll
@@ -1481,12 +1482,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
 }
 
 // SOFTCAP_CE at small M (the lm_head of a decode step): one wave per 128-column tile of the vocab walks its
-// rows two at a time and keeps the tile's online-softmax partials {max, sumexp, argmax} per activation row in
+// rows four at a time and keeps the tile's online-softmax partials {max, sumexp, argmax} per activation row in
 // registers — the row_stats layout of the MFMA epilogue (logits rounded to bf16, softcapped, rounded again).
 __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int64_t K, const bf16_t* __restrict__ x,
                                                            int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
                                                            bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
-  constexpr int RW = 2;
+  constexpr int RW = 4;
   const int lane = threadIdx.x & 63;
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t ntn = (N + 127) / 128;
@@ -1503,7 +1504,8 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
     for (int r = 0; r < RW; ++r)
 #pragma unroll
       for (int m = 0; m < GEMV_MAXM; ++m) acc[r][m] = 0.f;
-    for (int64_t k = (int64_t)lane * 8; k < K; k += 512) {
+  #pragma unroll 4
+  for (int64_t k = (int64_t)lane * 8; k < K; k += 512) {
       float wf[RW][8];
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
