@@ -11,6 +11,7 @@ The frozen ZoeDepth estimator (and its bicubic resampling) stays on stock PyTorc
 no_grad — it is not a north-star kernel target.
 """
 import os
+import warnings
 from dataclasses import dataclass
 from typing import List, Optional, Tuple, Union
 
@@ -65,13 +66,25 @@ class Ego3DPositionEmbeddingMLP(nn.Module):
         return Fn.LinearFn.apply(x, h3.weight, h3.bias, residual2d, 1.0)
 
 
+_ZOE_CONSTS = {}
+
+
+def _zoe_norm_consts(dtype, device):
+    """Zoe mean/std as device tensors, made once per (dtype, device): no host->device copy per call, so the
+    preprocessing can sit inside a captured HIP graph."""
+    key = (dtype, str(device))
+    if key not in _ZOE_CONSTS:
+        _ZOE_CONSTS[key] = (torch.tensor(ZOE_MEAN, dtype=dtype, device=device).view(1, -1, 1, 1),
+                            torch.tensor(ZOE_STD, dtype=dtype, device=device).view(1, -1, 1, 1))
+    return _ZOE_CONSTS[key]
+
+
 def process_zoe(pixel_values, pad_mode="reflect", output_size=(384, 512)):
     """Reference :99-110 (ZoeDepth preprocessing), stock torch ops."""
     ph, pw = 31, 31
     images = F.pad(pixel_values, (pw, pw, ph, ph), mode=pad_mode)
     images = F.interpolate(images, size=(384, 384), mode="bicubic", align_corners=True)
-    mean = torch.tensor(ZOE_MEAN, dtype=images.dtype, device=images.device).view(1, -1, 1, 1)
-    std = torch.tensor(ZOE_STD, dtype=images.dtype, device=images.device).view(1, -1, 1, 1)
+    mean, std = _zoe_norm_consts(images.dtype, images.device)
     images = (images - mean) / std
     return images, ph, pw
 
@@ -177,7 +190,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         return depth.contiguous()
 
     @torch.no_grad()
-    def ego3d_features(self, intrinsic, depth):
+    def ego3d_features(self, intrinsic, depth, kinv=None):
         """backproject_patch (:195-223) + frequency_encoding (:74-91) in one kernel -> [B*np, round8(F)]."""
         cfg = self.config
         B = depth.shape[0]
@@ -185,7 +198,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         nfeat = self.position_embedding_3d.freq_out_channels
         dt = self.multi_modal_projector.linear.weight.dtype
         feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=dt, device=depth.device)
-        kinv = torch.linalg.inv(intrinsic.float()).contiguous()
+        if kinv is None:
+            kinv = torch.linalg.inv(intrinsic.float()).contiguous()
         K.ego3d_encode(depth.float().contiguous(), kinv, self.uv_h.float().contiguous(),
                        cfg.vision_config.patch_size, cfg.ego3d_patch_reso, cfg.n_freqs, feat)
         return feat
@@ -201,7 +215,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                        self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
         return xyz
 
-    def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor):
+    def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor, kinv=None):
         """Reference :308-333 -> [B, np, H_text]."""
         dt = self.multi_modal_projector.linear.weight.dtype
         pv = pixel_values.to(dt).contiguous()
@@ -213,7 +227,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         sel = feats.reshape(-1, Hv)
         if self.config.use_vision_zoe:
             depth = self.predict_depth(pixel_values.to(dt))
-            enc = self.ego3d_features(intrinsic, depth)
+            enc = self.ego3d_features(intrinsic, depth, kinv)  # kinv: precomputed outside a graph capture
             sel = self.position_embedding_3d.forward_residual(enc, sel)
         lin = self.multi_modal_projector.linear
         img = Fn.LinearFn.apply(sel, lin.weight, lin.bias, None, 1.0 / (self.config.text_config.hidden_size ** 0.5))
@@ -393,11 +407,66 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         key = (B, capacity, str(dev))
         st = states.get(key)
         if st is None:
-            st = {"cache": self.new_cache(B, capacity), "graphs": {},
+            st = {"cache": self.new_cache(B, capacity), "graphs": {}, "prefill": {},
                   "tok": torch.zeros(B, 1, dtype=torch.int64, device=dev),
                   "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev))}
             states[key] = st
         return st
+
+    def _prefill_body(self, st, x):
+        """Vision tower + Ego3D/Zoe + Gemma2 prefill over the prompt (filling the cache) + the first greedy token."""
+        ids, cache = x["ids"], st["cache"]
+        feats = self.get_image_features(x["pv"], x["intr"], x["kinv"]) if x["pv"] is not None else None
+        pos = (torch.arange(ids.shape[1], device=ids.device) + 1)[None]
+        strict, self.strict_checks = self.strict_checks, False  # checked on the host by predict_action
+        try:
+            hidden = self._merge_inputs(ids, feats)
+        finally:
+            self.strict_checks = strict
+        h, _ = self.language_model.model(hidden, KVMask(x["cls"]), pos, cache=cache)
+        stash = {}
+        tgt = torch.full((ids.shape[0],), -1, dtype=torch.int64, device=ids.device)
+        self.language_model.head(h[:, -1:].contiguous(), tgt, stash)
+        return stash["argmax"]
+
+    def _prefill_graph(self, st, x):
+        """The prefill as one HIP graph per (prompt length, with/without image): ~2000 launches (SigLIP, the frozen
+        Zoe forward, 26 Gemma2 layers) whose host cost at B=1 rivals their GPU time.  Inputs are copied into the
+        graph's static buffers; shapes, the cache and the positions are baked in."""
+        cache = st["cache"]
+        key = (x["ids"].shape[1], x["pv"] is not None)
+        if key in st["prefill"] and st["prefill"][key] is None:
+            return self._prefill_body(st, x)
+        g = st["prefill"].get(key)
+        if g is None:
+            static = {k: (v.clone() if v is not None else None) for k, v in x.items()}
+            side = torch.cuda.Stream(device=x["ids"].device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # eager warm-up: lazy kernel attributes, hipBLASLt plans, Zoe caches
+                self._prefill_body(st, static)
+            cache.seen_tokens = 0
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    out = self._prefill_body(st, static)
+            except RuntimeError as e:  # an op of the prefill cannot be captured: run this shape eagerly from now on
+                cache.seen_tokens = 0
+                torch.cuda.synchronize()
+                st["prefill"][key] = None
+                import traceback
+                where = [f"{fr.filename.split('/')[-1]}:{fr.lineno} {fr.name}" for fr in traceback.extract_tb(e.__traceback__)]
+                warnings.warn(f"prefill graph capture failed at {' <- '.join(reversed(where[-6:]))}: "
+                              f"{str(e).splitlines()[0]}; prefill runs eagerly")
+                return self._prefill_body(st, x)
+            cache.seen_tokens = 0
+            g = st["prefill"][key] = (graph, static, out)
+        graph, static, out = g
+        for k, v in x.items():
+            if v is not None:
+                static[k].copy_(v)
+        graph.replay()
+        return out
 
     def _decode_body(self, st, p0):
         """One decode step at cache position p0: the token in st["tok"] -> argmax of its logits [B]."""
@@ -441,16 +510,27 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
-        feats = self.get_image_features(pv, intr) if pv is not None else None
         graphs = self.decode_graphs and dev.type == "cuda"
         st = self._decode_state(B, P + max_new_tokens, dev)
         cache = st["cache"]
         cache.seen_tokens = 0
-        lm = self.language_model.model
-        pos = (torch.arange(P, device=dev) + 1)[None]
-        h, _ = lm(self._merge_inputs(ids, feats), KVMask(self._prompt_classes(am, B, P, dev)), pos, cache=cache)
+        cls = self._prompt_classes(am, B, P, dev)
+        if pv is not None and self.strict_checks:  # reference :379-385, checked before any graph replay
+            vc = self.config.vision_config
+            n_img = B * (vc.image_size // vc.patch_size) ** 2
+            n_tok = int((model_inputs["input_ids"] == self.config.image_token_index).sum())
+            if n_tok != n_img:
+                raise ValueError("Number of images does not match number of special image tokens in the input text. "
+                                 f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
+        # inv(K) (reference :206) runs outside the graph: the batched LU inverse checks its info on the host
+        kinv = torch.linalg.inv(intr.float()).contiguous() if (pv is not None and intr is not None) else None
+        prefill = {"ids": ids, "pv": pv, "intr": intr, "cls": cls, "kinv": kinv}
+        first = self._prefill_graph(st, prefill) if graphs else self._prefill_body(st, prefill)
+        cache.seen_tokens = P
         finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
-        nxt, finished = self._next_token(h, finished, eos)
+        nxt = first.view(B, 1).clone()
+        if eos is not None:
+            finished = nxt == eos
         out = [nxt]
         pad = torch.full_like(nxt, max(self.pad_token_id, 0))
         for _ in range(max_new_tokens - 1):

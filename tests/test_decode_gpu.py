@@ -66,7 +66,8 @@ def test_attn_decode_rejects_bad_args(cuda):
 def _tiny_model(cuda):
     g = load_file(os.path.join(os.path.dirname(__file__), "golden", "tiny_train.safetensors"))
     model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
-    model.predict_depth = lambda p: g["out.depth"].to(cuda)
+    depth = g["out.depth"].to(cuda)  # a device tensor: the captured prefill graph may not copy from the host
+    model.predict_depth = lambda p: depth
     return model, g
 
 
@@ -85,6 +86,22 @@ def test_predict_action_cached_equals_uncached(cuda):
     g1 = model.predict_action(inputs, max_new_tokens=8, eos_token_id=-1)
     g2 = model.predict_action(inputs, max_new_tokens=8, eos_token_id=-1)
     assert torch.equal(g1, cached) and torch.equal(g2, cached)
+    # new inputs of the same shape go through the same (replayed) prefill and decode graphs
+    inputs2 = dict(inputs, pixel_values=inputs["pixel_values"].flip(-1))
+    model.decode_graphs = False
+    e3 = model.predict_action(inputs2, max_new_tokens=8, eos_token_id=-1)
+    model.decode_graphs = True
+    g3 = model.predict_action(inputs2, max_new_tokens=8, eos_token_id=-1)
+    assert torch.equal(g3, e3)
+
+
+def test_predict_action_image_token_mismatch_raises(cuda):
+    model, g = _tiny_model(cuda)
+    ids = g["in.input_ids"][:, :-13].clone()
+    ids[0, 0] = 2  # one image token fewer than image features
+    with pytest.raises(ValueError):
+        model.predict_action({"input_ids": ids, "pixel_values": g["in.pixel_values"],
+                              "intrinsic": g["in.intrinsic"]}, max_new_tokens=2, eos_token_id=-1)
 
 
 def test_predict_action_eos_pads_finished(cuda):

@@ -56,6 +56,10 @@ def main():
         tn, toks = timed(lambda: pa(n_new), args.reps)
         tl, _ = timed(lambda: pa(n_long), max(3, args.reps // 2))
         per_tok = (tl - t1) / (n_long - 1)
+        graphs_on = model.decode_graphs
+        model.decode_graphs = False
+        toks_eager = pa(n_new)
+        model.decode_graphs = graphs_on
         res_unc = None
         if not args.no_uncached:
             tu, toks_u = timed(lambda: model.predict_action_uncached(inputs, max_new_tokens=n_new, eos_token_id=-1),
@@ -71,7 +75,7 @@ def main():
         "metric": "SpatialVLA-4B greedy decode latency (BASELINE configs[1])", "unit": "ms", "batch": args.batch,
         "prompt_tokens": P, "new_tokens": n_new, "ms_total": round(tn, 2), "ms_prefill_plus_first": round(t1, 2),
         "ms_per_decode_token": round(per_tok, 3), "tokens_per_s_decode": round(1000.0 * args.batch / per_tok, 1),
-        "uncached": res_unc, "decode_graphs": graphs,
+        "uncached": res_unc, "decode_graphs": graphs, "graph_tokens_equal_eager": bool(torch.equal(toks, toks_eager)),
         "decode_roofline": {"bound": "hbm", "algorithmic_bytes_per_token_step": wbytes, "achieved": round(gbs, 1),
                             "peak": 8000.0, "unit": "GB/s", "frac": round(gbs / 8000.0, 4)},
         "dtype": "bf16", "data": "synthetic OXE-shaped prompt, random-init weights"}), flush=True)
