@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", default="spatialvla_4b", choices=["spatialvla_4b", "tiny"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the B=1 decode-latency leg")
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--seed", type=int, default=1234)
     return ap.parse_args()
@@ -156,6 +157,40 @@ def gemma2_block_roofline(model, B, L, device, iters=20):
             "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
             "ms_fwd_bwd": round(ms, 3), "ms_fwd": round(float(np.median(fwd_ms)), 3), "iters": iters,
             "algorithmic_flops": flops, "target_frac": 0.40}
+
+
+def decode_latency(model, cfgd, device, n_new=4, n_long=40):
+    """BASELINE configs[1] beside the training line (after the timed region, same weights): B=1 greedy decode
+    through predict_action -- prefill (vision + Zoe + Gemma2 over the 299-token prompt + first token) and the
+    KV-cached decode steps, both replayed from HIP graphs -- timed with HIP events, median of 5."""
+    b = make_batch(cfgd, 1, 4321, device)
+    P = int((b["token_type_ids"][0] == 0).sum())
+    inputs = {"input_ids": b["input_ids"][:, :P], "pixel_values": b["pixel_values"], "intrinsic": b["intrinsic"]}
+    model.eval()
+
+    def med(n):
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            model.predict_action(inputs, max_new_tokens=n, eos_token_id=-1)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts)[2]
+
+    with torch.no_grad():
+        model.predict_action(inputs, max_new_tokens=n_long, eos_token_id=-1)  # captures every graph once
+        t1, tn, tl = med(1), med(n_new), med(n_long)
+    per_tok = (tl - t1) / (n_long - 1)
+    lm = model.language_model
+    wbytes = sum(p.numel() * p.element_size() for p in lm.model.layers.parameters()) + \
+        lm.lm_head.weight.numel() * lm.lm_head.weight.element_size()
+    return {"what": "B=1 predict_action: 1 image + 299-token prompt -> 4 tokens (BASELINE configs[1])",
+            "ms_total": round(tn, 2), "ms_prefill_plus_first": round(t1, 2), "ms_per_decode_token": round(per_tok, 3),
+            "decode_roofline": {"bound": "hbm", "achieved": round(wbytes / (per_tok * 1e-3) / 1e9, 1),
+                                "peak": 8000.0, "unit": "GB/s", "algorithmic_bytes_per_token": wbytes}}
 
 
 def cpu_baseline(cfgd, iters):
@@ -273,6 +308,8 @@ def main():
             del batches, engine
             torch.cuda.empty_cache()
             result["cpu_baseline"] = cpu_baseline(cfgd, args.cpu_iters)
+        if world == 1 and args.config == "spatialvla_4b" and not args.no_decode:
+            result["decode"] = decode_latency(model, cfgd, device)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

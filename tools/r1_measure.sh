@@ -6,11 +6,11 @@ TAG=${TAG:-r1}
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-decode > $O/bench_prof.json 2> $O/bench_prof.err && \
 python tools/summarize_profile.py trace /tmp/prof_$TAG $O/$TAG > $O/trace_summary.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d /tmp/pmc_fetch -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.json 2> $O/pmc_fetch.err && \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d /tmp/pmc_fetch -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode > $O/pmc_fetch.json 2> $O/pmc_fetch.err && \
 python tools/summarize_profile.py pmc /tmp/pmc_fetch $O/${TAG}_pmc_fetch > $O/pmc_fetch_summary.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d /tmp/pmc_write -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_write.json 2> $O/pmc_write.err && \
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d /tmp/pmc_write -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode > $O/pmc_write.json 2> $O/pmc_write.err && \
 python tools/summarize_profile.py pmc /tmp/pmc_write $O/${TAG}_pmc_write > $O/pmc_write_summary.log 2>&1
 rc=$?
 ls -la $O
