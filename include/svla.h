@@ -167,6 +167,13 @@ size_t svla_attn_decode_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32
 int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, float* workspace, size_t ws_bytes,
                      void* stream);
 
+/* Decode-step q|k|v epilogue: rotate_half RoPE on q in place (rows b*Lq+t of qkv, position table row t) and on
+ * k, rotated k and plain v written to cache rows p0+t (k/v cache element (b, j, h, d) at base + b*bs + j*ld + h*D + d).
+ * Replaces apply_rotary_pos_emb + the HybridCache update (model/modeling_gemma2.py:123-154, :387-395). */
+int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                         const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache, int64_t ldk,
+                         int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0, void* stream);
+
 /* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
  * workspace: B*Hq*L fp32 (row dot(dO, O)). */
 int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,

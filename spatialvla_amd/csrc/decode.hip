@@ -183,6 +183,54 @@ int launch_g(const svla_attn_decode_args& a, bf16_t* out, int64_t ldo, float* ws
   }
 }
 
+// Decode-step epilogue of the q|k|v projection (one launch instead of RoPE pass + two cache copies): rotate_half
+// RoPE on q (in place) and k, k written rotated and v copied into cache rows p0 + t.  Same rounding as the
+// GEMM's ROPE epilogue: out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)) (modeling_gemma2.py:123-154).
+// One thread owns 8 columns of the low half of a head and their partners D/2 away (q/k), or 16 v columns.
+__global__ void qkv_rope_append_kernel(int B, int Lq, int Hq, int Hkv, int D, bf16_t* __restrict__ qkv, int64_t ld,
+                                       const bf16_t* __restrict__ cos_t, const bf16_t* __restrict__ sin_t,
+                                       int64_t rope_ld, bf16_t* __restrict__ kc, int64_t ldk, int64_t bsk,
+                                       bf16_t* __restrict__ vc, int64_t ldv, int64_t bsv, int p0) {
+  const int half = D >> 1, cph = half / 8;
+  const int64_t rot_per_row = (int64_t)(Hq + Hkv) * cph, v_per_row = (int64_t)Hkv * D / 16;
+  const int64_t per_row = rot_per_row + v_per_row;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * Lq * per_row) return;
+  const int64_t m = idx / per_row;
+  const int r = (int)(idx % per_row);
+  const int b = (int)(m / Lq), t = (int)(m % Lq);
+  bf16_t* row = qkv + m * ld;
+  if (r < rot_per_row) {
+    const int head = r / cph, dd = (r % cph) * 8;
+    bf16_t* lo = row + (int64_t)head * D + dd;
+    bf16_t* hi = lo + half;
+    float xl[8], xh[8], cs[8], sn[8], ol[8], oh[8];
+    unpack8(*reinterpret_cast<const u32x4*>(lo), xl);
+    unpack8(*reinterpret_cast<const u32x4*>(hi), xh);
+    unpack8(*reinterpret_cast<const u32x4*>(cos_t + (int64_t)t * rope_ld + dd), cs);
+    unpack8(*reinterpret_cast<const u32x4*>(sin_t + (int64_t)t * rope_ld + dd), sn);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ol[j] = round_bf(xl[j] * cs[j]) + round_bf(-xh[j] * sn[j]);
+      oh[j] = round_bf(xh[j] * cs[j]) + round_bf(xl[j] * sn[j]);
+    }
+    if (head < Hq) {  // q stays in the projection output for the attention kernel
+      *reinterpret_cast<u32x4*>(lo) = pack8(ol);
+      *reinterpret_cast<u32x4*>(hi) = pack8(oh);
+    } else {
+      bf16_t* kr = kc + (int64_t)b * bsk + (int64_t)(p0 + t) * ldk + (int64_t)(head - Hq) * D + dd;
+      *reinterpret_cast<u32x4*>(kr) = pack8(ol);
+      *reinterpret_cast<u32x4*>(kr + half) = pack8(oh);
+    }
+  } else {
+    const int c = (r - (int)rot_per_row) * 16;
+    const bf16_t* src = row + (int64_t)(Hq + Hkv) * D + c;
+    bf16_t* dst = vc + (int64_t)b * bsv + (int64_t)(p0 + t) * ldv + c;
+    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+    *reinterpret_cast<u32x4*>(dst + 8) = *reinterpret_cast<const u32x4*>(src + 8);
+  }
+}
+
 }  // namespace
 
 extern "C" size_t svla_attn_decode_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32_t Lk, int32_t D) {
@@ -217,4 +265,24 @@ extern "C" int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64
     case 128: return launch_g<128>(*a, o, ldo, workspace, s);
     default: return launch_g<256>(*a, o, ldo, workspace, s);
   }
+}
+
+extern "C" int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                                    const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache,
+                                    int64_t ldk, int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0,
+                                    void* stream) {
+  SVLA_CHECK_ARG(qkv && rope_cos && rope_sin && k_cache && v_cache, "qkv_rope_append: NULL pointer");
+  SVLA_CHECK_ARG(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && p0 >= 0, "qkv_rope_append: bad sizes");
+  SVLA_CHECK_ARG(D % 16 == 0 && D <= 256, "qkv_rope_append: head_dim must be a multiple of 16, <= 256");
+  SVLA_CHECK_ARG(ld % 8 == 0 && rope_ld % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && bsk % 8 == 0 && bsv % 8 == 0 &&
+                     ld >= (int64_t)(Hq + 2 * Hkv) * D && ldk >= (int64_t)Hkv * D && ldv >= (int64_t)Hkv * D,
+                 "qkv_rope_append: strides");
+  SVLA_CHECK_ARG((((uintptr_t)qkv | (uintptr_t)k_cache | (uintptr_t)v_cache | (uintptr_t)rope_cos |
+                   (uintptr_t)rope_sin) & 15) == 0, "qkv_rope_append: pointers must be 16-B aligned");
+  const int64_t per_row = (int64_t)(Hq + Hkv) * (D / 16) + (int64_t)Hkv * D / 16;
+  const int64_t work = (int64_t)B * Lq * per_row;
+  hipLaunchKernelGGL(qkv_rope_append_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     B, Lq, Hq, Hkv, D, (bf16_t*)qkv, ld, (const bf16_t*)rope_cos, (const bf16_t*)rope_sin, rope_ld,
+                     (bf16_t*)k_cache, ldk, bsk, (bf16_t*)v_cache, ldv, bsv, p0);
+  return svla::check_launch("qkv_rope_append");
 }

@@ -317,10 +317,15 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     B, Lq = cfg.B, cfg.L
     qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
     qkv = _empty(M, qd + 2 * kd, like=x)
-    K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, Lq, cfg.D, qd + kd))
-    k_cache[:, p0:p0 + Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
-    v_cache[:, p0:p0 + Lq].copy_(qkv[:, qd + kd:].view(B, Lq, kd))
     attn = _empty(M, qd, like=x)
+    if p0 > 0:
+        # decode step: plain projection, then one pass rotates q in place and appends rotated k / v to the cache
+        K.linear_fwd(x, [wq, wk, wv], qkv)
+        K.qkv_rope_append(qkv, B, Lq, cfg.Hq, cfg.Hkv, cfg.D, cos, sin, k_cache, v_cache, p0)
+    else:
+        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, Lq, cfg.D, qd + kd))
+        k_cache[:, :Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
+        v_cache[:, :Lq].copy_(qkv[:, qd + kd:].view(B, Lq, kd))
     if p0 == 0:
         lse = _empty(B, cfg.Hq, Lq, dtype=F32, like=x)
         cls = kv_class[:, :Lq].contiguous()  # held until the launch: attn_args keeps only its pointer

@@ -341,6 +341,19 @@ def attn_decode(q, Lq, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_clas
             "attn_decode")
 
 
+def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
+    """RoPE q in place, rotated k and v into cache rows p0.. (the decode step's q|k|v epilogue)."""
+    _req(qkv.shape[0] == B * Lq and qkv.stride(1) == 1, "qkv_rope_append: qkv rows")
+    _req(cos.shape[0] >= Lq and cos.shape == sin.shape and cos.stride(1) == 1, "qkv_rope_append: tables")
+    _req(k_cache.shape[1] >= p0 + Lq and v_cache.shape[1] >= p0 + Lq, "qkv_rope_append: cache too short")
+    for t, n in ((qkv, "qkv"), (cos, "cos"), (sin, "sin"), (k_cache, "k_cache"), (v_cache, "v_cache")):
+        _chk_bf16(t, n)
+    L.check(L.lib().svla_qkv_rope_append(B, Lq, Hq, Hkv, D, qkv.data_ptr(), qkv.stride(0), cos.data_ptr(),
+                                         sin.data_ptr(), cos.stride(0), k_cache.data_ptr(), k_cache.stride(1),
+                                         k_cache.stride(0), v_cache.data_ptr(), v_cache.stride(1), v_cache.stride(0),
+                                         int(p0), _stream()), "qkv_rope_append")
+
+
 def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):
     ws = torch.empty(a.B * a.Hq * a.L, dtype=torch.float32, device=out.device)
     L.check(L.lib().svla_attn_bwd(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),

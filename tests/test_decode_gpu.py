@@ -201,3 +201,27 @@ def test_gemv_rope(cuda, M):
     seg = torch.empty_like(plain)
     Kn.linear_fwd(x, [wq, wk, wv], seg, kind=L_.EPI_ROPE, rope=(cos, sin, M, D, nrot))
     assert torch.equal(seg, ref)
+
+
+@pytest.mark.parametrize("B,Lq,p0", [(1, 1, 299), (2, 3, 17)])
+def test_qkv_rope_append(cuda, B, Lq, p0):
+    """Decode-step q|k|v epilogue: bitwise the reference bf16 RoPE on q (in place) and k, k/v in cache rows p0.."""
+    from spatialvla_amd import kernels as Kn
+    from test_kernels_gpu import _rope_bf16
+    torch.manual_seed(8)
+    Hq, Hkv, D, cap = 8, 4, 256, p0 + Lq + 5
+    kd = Hkv * D
+    qkv = _r(B * Lq, (Hq + 2 * Hkv) * D)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    f = (torch.arange(p0, p0 + Lq, device=cuda).float() + 1)[:, None] * inv[None]
+    cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
+    kc = torch.zeros(B, cap, kd, dtype=BF, device=cuda)
+    vc = torch.zeros_like(kc)
+    ref = qkv.clone()
+    nrot = (Hq + Hkv) * D
+    ref[:, :nrot] = _rope_bf16(qkv[:, :nrot].view(B, Lq, Hq + Hkv, D), cos, sin).reshape(B * Lq, nrot)
+    Kn.qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, kc, vc, p0)
+    assert torch.equal(qkv[:, :Hq * D], ref[:, :Hq * D])
+    assert torch.equal(kc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, Hq * D:nrot])
+    assert torch.equal(vc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, nrot:])
+    assert kc[:, :p0].abs().sum() == 0 and kc[:, p0 + Lq:].abs().sum() == 0

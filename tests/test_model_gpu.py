@@ -209,7 +209,8 @@ def test_predict_action_decodes(cuda):
     g = _load("tiny_train.safetensors")
     gp = _load("tiny_prefill.safetensors")
     model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
-    model.predict_depth = lambda p: g["out.depth"].to(cuda)
+    depth = g["out.depth"].to(cuda)  # device tensor: no host copy inside the captured prefill graph
+    model.predict_depth = lambda p: depth
     ids = g["in.input_ids"][:, :-13]  # prompt only (prefix)
     inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
     out = model.predict_action(inputs, max_new_tokens=3, eos_token_id=-1)
