@@ -194,6 +194,10 @@ int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, cons
                      void* stream);
 int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w, float eps,
                          void* h, float* rstd, void* stream);
+/* h = res + rmsnorm(yin; w1), x = rmsnorm(h; w2) in one pass (inference; bitwise the two separate calls):
+ * Gemma2 post-attention + pre-feedforward norms, or post-feedforward + next input norm (modeling_gemma2.py:487-496). */
+int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1, const void* w2,
+                          float eps1, float eps2, void* h, void* x, void* stream);
 int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
                        void* y, float* mean, float* rstd, void* stream);
 int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* mean,

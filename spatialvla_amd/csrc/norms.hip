@@ -59,6 +59,64 @@ __global__ __launch_bounds__(NTH) void rms_fwd_kernel(int64_t N, const bf16_t* _
   }
 }
 
+// Two chained Gemma2 norms in one pass (inference: the decode step): h = bf16(res + bf16(rms(y; w1))) as
+// rms_fwd_kernel<true>, then x = bf16(rms(h; w2)) as rms_fwd_kernel<false> over the bf16 h -- the same chunk
+// mapping and summation order as the two separate launches, so both outputs are bitwise theirs.
+// post_attention_layernorm + pre_feedforward_layernorm, and post_feedforward_layernorm + the next layer's
+// input_layernorm (modeling_gemma2.py:487-496).
+__global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf16_t* __restrict__ y,
+                                                            const bf16_t* __restrict__ res,
+                                                            const bf16_t* __restrict__ w1,
+                                                            const bf16_t* __restrict__ w2, float eps1, float eps2,
+                                                            bf16_t* __restrict__ h, bf16_t* __restrict__ x) {
+  __shared__ float red[16];
+  const int64_t row = blockIdx.x;
+  const int nch = (int)(N >> 3);
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      ld8(y + row * N + ch * 8, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float rstd1 = rsqrtf(ss / (float)N + eps1);
+  float ss2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float wf[8], r[8];
+      ld8(w1 + ch * 8, wf);
+      ld8(res + row * N + ch * 8, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[c][j] = round_bf(r[j] + round_bf((v[c][j] * rstd1) * (1.0f + wf[j])));
+        ss2 += v[c][j] * v[c][j];
+      }
+      st8(h + row * N + ch * 8, v[c]);
+    }
+  }
+  __syncthreads();  // red[] is reused by the second reduction
+  ss2 = block_sum(ss2, red);
+  const float rstd2 = rsqrtf(ss2 / (float)N + eps2);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float wf[8], o[8];
+      ld8(w2 + ch * 8, wf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] * rstd2) * (1.0f + wf[j]);
+      st8(x + row * N + ch * 8, o);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ RMSNorm backward
 // dx = rstd*(g - xhat*mean(g*xhat)) + dres,  g = dy*(1+w), xhat = x*rstd;  dw += sum_rows dy*xhat
 __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
@@ -482,4 +540,15 @@ extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx
                      (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace, (bf16_t*)nullptr, 0);
   if (int rc = svla::check_launch("colsum_bf16")) return rc;
   return svla_colsum_f32(parts, N, workspace, out_bf16, accumulate, nullptr, stream);
+}
+
+extern "C" int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,
+                                     const void* w2, float eps1, float eps2, void* h, void* x, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "add_rmsnorm2: bad N");
+  SVLA_CHECK_ARG(res && yin && w1 && w2 && h && x && al16(res) && al16(yin) && al16(w1) && al16(w2) && al16(h) &&
+                     al16(x), "add_rmsnorm2: null/misaligned pointer");
+  hipLaunchKernelGGL(rms_add_norm2_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
+                     (bf16_t*)h, (bf16_t*)x);
+  return svla::check_launch("add_rmsnorm2_fwd");
 }

@@ -249,6 +249,17 @@ def add_rmsnorm_fwd(res, yin, w, eps, h, rstd):
 RPB = 16  # rows per block of the norm backward kernels (norms.hip)
 
 
+def add_rmsnorm2_fwd(res, yin, w1, w2, eps1, eps2, h, x):
+    rows, N = yin.shape
+    for t, n in ((res, "res"), (yin, "yin"), (w1, "w1"), (w2, "w2"), (h, "h"), (x, "x")):
+        _chk_bf16(t, n)
+    _req(res.shape == yin.shape == h.shape == x.shape and res.is_contiguous() and yin.is_contiguous(),
+         "add_rmsnorm2: shapes")
+    L.check(L.lib().svla_add_rmsnorm2_fwd(rows, N, res.data_ptr(), yin.data_ptr(), w1.data_ptr(), w2.data_ptr(),
+                                          float(eps1), float(eps2), h.data_ptr(), x.data_ptr(), _stream()),
+            "add_rmsnorm2_fwd")
+
+
 def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False):
     rows, N = x.shape
     nb = (rows + RPB - 1) // RPB

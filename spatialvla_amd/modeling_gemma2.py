@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from . import functional as Fn
+from . import kernels as Kn
 
 
 @dataclass
@@ -258,6 +259,8 @@ class Gemma2Model(nn.Module):
                 raise ValueError("the KV cache is an inference path: run it under torch.no_grad()")
             cache.append_classes(attention_mask.kv_class)
         rope = self.layers[0].self_attn.rotary_emb.tables(position_ids, hidden_states.dtype)
+        if cache is not None and not output_hidden_states:
+            return self._forward_cached(hidden_states, attention_mask, rope, cache), None
         all_h = () if output_hidden_states else None
         hook = getattr(self, "_svla_layer_grad_hook", None)
         for i, layer in enumerate(self.layers[: self.config.num_hidden_layers]):
@@ -273,6 +276,30 @@ class Gemma2Model(nn.Module):
         if output_hidden_states:
             all_h += (hidden_states,)
         return hidden_states, all_h
+
+
+    def _forward_cached(self, hidden, attention_mask, rope, cache):
+        """Inference layer loop (prefill into / decode from the cache): each residual add is fused with the norm
+        that consumes its result -- post_attention + pre_feedforward, post_feedforward + the next layer's
+        input_layernorm (or the final norm) -- bitwise the reference order (:475-496, :777), two norm launches per
+        layer instead of four."""
+        layers = self.layers[: self.config.num_hidden_layers]
+        shp = hidden.shape
+        H = shp[-1]
+        res = hidden.reshape(-1, H).contiguous()
+        x = layers[0].input_layernorm(res)
+        for i, layer in enumerate(layers):
+            a = layer.self_attn(x.view(shp), attention_mask, rope, cache).reshape(-1, H)
+            pa, pf = layer.post_attention_layernorm, layer.pre_feedforward_layernorm
+            h, x = torch.empty_like(res), torch.empty_like(res)
+            Kn.add_rmsnorm2_fwd(res, a, pa.weight, pf.weight, pa.eps, pf.eps, h, x)
+            m = layer.mlp(x).reshape(-1, H)
+            nxt = layers[i + 1].input_layernorm if i + 1 < len(layers) else self.norm
+            po = layer.post_feedforward_layernorm
+            res, x = torch.empty_like(res), torch.empty_like(res)
+            Kn.add_rmsnorm2_fwd(h, m, po.weight, nxt.weight, po.eps, nxt.eps, res, x)
+        cache.seen_tokens += shp[1]
+        return x.view(shp)
 
 
 class Gemma2ForCausalLM(nn.Module):

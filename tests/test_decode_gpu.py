@@ -225,3 +225,20 @@ def test_qkv_rope_append(cuda, B, Lq, p0):
     assert torch.equal(kc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, Hq * D:nrot])
     assert torch.equal(vc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, nrot:])
     assert kc[:, :p0].abs().sum() == 0 and kc[:, p0 + Lq:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("rows", [1, 3, 299])
+def test_add_rmsnorm2_bitwise(cuda, rows):
+    """The fused residual-add + two chained RMSNorms equals the two separate norm kernels bit for bit."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(9)
+    N = 2304
+    res, y = _r(rows, N), _r(rows, N, scale=3.0)
+    w1, w2 = _r(N, scale=0.3), _r(N, scale=0.3)
+    h_ref, x_ref = torch.empty_like(res), torch.empty_like(res)
+    rstd = torch.empty(rows, device=cuda)
+    Kn.add_rmsnorm_fwd(res, y, w1, 1e-6, h_ref, rstd)
+    Kn.rmsnorm_fwd(h_ref, w2, 1e-6, x_ref, rstd)
+    h, x = torch.empty_like(res), torch.empty_like(res)
+    Kn.add_rmsnorm2_fwd(res, y, w1, w2, 1e-6, 1e-6, h, x)
+    assert torch.equal(h, h_ref) and torch.equal(x, x_ref)
