@@ -1558,6 +1558,47 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
   }
 }
 
+// Long-K STORE GEMV (the down projection, K = 9216): the four waves of a workgroup split one row's K range, so
+// a row is streamed by 256 lanes instead of 64 (4x the loads in flight per row), and the partial dots are
+// summed through LDS in wave order (deterministic).
+__global__ __launch_bounds__(256) void gemv_splitk_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ x,
+                                                          int64_t ldx, svla_operand B, bf16_t* __restrict__ c,
+                                                          int64_t ldc) {
+  __shared__ float part[4][GEMV_MAXM];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = blockIdx.x;
+  const bf16_t* wr = gemv_row(B, n);
+  float acc[GEMV_MAXM];
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) acc[m] = 0.f;
+#pragma unroll 4
+  for (int64_t k = (int64_t)threadIdx.x * 8; k < K; k += 2048) {
+    float wf[8];
+    unpack8(*reinterpret_cast<const u32x4*>(wr + k), wf);
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+      if (m < M) {
+        float xf[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) {
+    if (m < M) {
+      const float v = wave_sum(acc[m]);
+      if (lane == 0) part[w][m] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < M) {
+    const int m = threadIdx.x;
+    c[m * ldc + n] = f2bf(((part[0][m] + part[1][m]) + part[2][m]) + part[3][m]);
+  }
+}
+
 template <int RW, bool GEGLU>
 int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
                 int64_t ldc, const svla_epilogue& E, hipStream_t s) {
@@ -1820,7 +1861,10 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
                            (const bf16_t*)A->ptr[0], A->ld, (const bf16_t*)B->ptr[0], B->ld, c0, ldc, *epi);
       } else if (epi->kind == SVLA_EPI_GEGLU) {
         launch_gemv<1, true>((int)M, N / 2, K, *A, *B, c0, ldc, *epi, s);
-      } else if (K > 4096 || N < 8192) {
+      } else if (K > 4096) {
+        hipLaunchKernelGGL(gemv_splitk_kernel, dim3((unsigned)N), dim3(256), 0, s, (int)M, N, K,
+                           (const bf16_t*)A->ptr[0], A->ld, *B, c0, ldc);
+      } else if (N < 8192) {
         launch_gemv<1, false>((int)M, N, K, *A, *B, c0, ldc, *epi, s);
       } else {
         launch_gemv<2, false>((int)M, N, K, *A, *B, c0, ldc, *epi, s);
