@@ -210,3 +210,22 @@ def test_product_fails_loudly_without_gpu():
     b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=1, seed=0), "cpu")
     with pytest.raises(Exception):
         m(**b)
+
+
+def test_kv_cache_layout_and_capacity():
+    """Gemma2KVCache (HybridCache stand-in): per-layer [B, capacity, Hkv*D] rows, classes appended per forward,
+    overflow raises (host logic only; the kernels are in tests/test_decode_gpu.py)."""
+    from spatialvla_amd import SpatialVLAConfig
+    from spatialvla_amd.modeling_gemma2 import Gemma2KVCache
+    cfg = SpatialVLAConfig(**H.cfg_dict("tiny")).text_config
+    c = Gemma2KVCache(cfg, batch_size=2, capacity=10, device="cpu")
+    kd = cfg.num_key_value_heads * cfg.head_dim
+    assert c.key_cache.shape == (cfg.num_hidden_layers, 2, 10, kd) and c.value_cache.shape == c.key_cache.shape
+    assert c.get_seq_length() == 0 and c.capacity == 10
+    c.append_classes(torch.zeros(2, 7, dtype=torch.uint8))
+    c.seen_tokens = 7
+    c.append_classes(torch.ones(2, 3, dtype=torch.uint8))
+    assert c.kv_class[:, :7].eq(0).all() and c.kv_class[:, 7:].eq(1).all()
+    c.seen_tokens = 10
+    with pytest.raises(ValueError):
+        c.append_classes(torch.ones(2, 1, dtype=torch.uint8))
