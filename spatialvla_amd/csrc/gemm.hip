@@ -1437,10 +1437,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
     for (int r = 0; r < RW; ++r) {
       const int64_t n = r0 + r < rows ? r0 + r : rows - 1;
       if constexpr (GEGLU) {  // gate row n in ptr[0], up row n in ptr[1]
-        unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[0] + n * B.ld + k), wf[r][0]);
-        unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[1] + n * B.ld + k), wf[r][NW - 1]);
+        unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[0] + n * B.ld + k)), wf[r][0]);
+        unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>((const bf16_t*)B.ptr[1] + n * B.ld + k)), wf[r][NW - 1]);
       } else {
-        unpack8(*reinterpret_cast<const u32x4*>(gemv_row(B, n) + k), wf[r][0]);
+        unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(gemv_row(B, n) + k)), wf[r][0]);
       }
     }
 #pragma unroll
@@ -1510,7 +1510,7 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         const int64_t n = r0 + r < nend ? r0 + r : nend - 1;
-        unpack8(*reinterpret_cast<const u32x4*>(w + n * ldw + k), wf[r]);
+        unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + n * ldw + k)), wf[r]);
       }
 #pragma unroll
       for (int m = 0; m < GEMV_MAXM; ++m) {
@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(256) void gemv_splitk_kernel(int M, int64_t rows, i
 #pragma unroll 4
   for (int64_t k = (int64_t)threadIdx.x * 8; k < K; k += 2048) {
     float wf[8];
-    unpack8(*reinterpret_cast<const u32x4*>(wr + k), wf);
+    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + k)), wf);
 #pragma unroll
     for (int m = 0; m < GEMV_MAXM; ++m) {
       if (m < M) {
