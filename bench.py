@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--config", default="spatialvla_4b", choices=["spatialvla_4b", "tiny"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the B=1 decode-latency leg")
-    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
     return ap.parse_args()
 
@@ -193,12 +193,35 @@ def decode_latency(model, cfgd, device, n_new=4, n_long=40):
                                 "peak": 8000.0, "unit": "GB/s", "algorithmic_bytes_per_token": wbytes}}
 
 
-def cpu_baseline(cfgd, iters):
-    """Reference eager restatement (oracle, test infrastructure) fwd+bwd at B=1 on the host cores."""
+def _usable_cpus():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                n = min(n, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def _cpu_isa():
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+    except (OSError, StopIteration):
+        return "unknown"
+    tags = [f for f in ("amx_bf16", "avx512_bf16", "avx512f", "avx2") if f in flags]
+    return "+".join(tags) or "baseline x86-64"
+
+
+def cpu_baseline(cfgd, iters, batches=(1, 2)):
+    """Reference eager restatement (oracle, test infrastructure) fwd+bwd on the host cores, per BASELINE.md §3:
+    every usable core, bf16, B=1 and B=2, 1 warm-up + `iters` timed iterations each, median."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import spatialvla_oracle as O
     from spatialvla_amd import presets
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    threads = _usable_cpus()
     torch.set_num_threads(threads)
     t_build = time.perf_counter()
     P = O.build_params_random(cfgd, seed=0)
@@ -206,35 +229,52 @@ def cpu_baseline(cfgd, iters):
     if cfgd.get("use_vision_zoe", True):
         from transformers import ZoeDepthConfig, ZoeDepthForDepthEstimation
         zoe = ZoeDepthForDepthEstimation(ZoeDepthConfig(**cfgd["vision_zoe_config"])).to(torch.bfloat16).eval()
-    log(f"[cpu_baseline] oracle built in {time.perf_counter() - t_build:.1f}s, {threads} threads")
-    b = presets.synthetic_batch(cfgd, batch=1, seed=99)
-    t = {k: torch.from_numpy(v) for k, v in b.items()}
-    t["pixel_values"] = t["pixel_values"].to(torch.bfloat16)
-    t["intrinsic"] = t["intrinsic"].to(torch.bfloat16)
-    times = []
-    for i in range(iters + 1):
-        for v in P.values():
-            v.grad = None
-        t0 = time.perf_counter()
-        loss, _ = O.forward(P, cfgd, t, zoe)
-        loss.backward()
-        dt = time.perf_counter() - t0
-        log(f"[cpu_baseline] iter {i}: {dt:.2f}s")
-        if i > 0:
-            times.append(dt)
-    med = float(np.median(times))
-    amx = False
-    try:
-        amx = "amx" in open("/proc/cpuinfo").read()
-    except OSError:
-        pass
-    return {"value": round(1.0 / med, 4), "unit": "episodes/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fwd+bwd, B=1 episode x {iters} timed iters (+1 warmup), median {med:.2f}s/episode, "
-                      f"bf16, {'AMX' if amx else 'no AMX'}"}
+    log(f"[cpu_baseline] oracle built in {time.perf_counter() - t_build:.1f}s, {threads} threads "
+        f"(os.cpu_count() {os.cpu_count()})")
+    per_b = {}
+    for B in batches:
+        b = presets.synthetic_batch(cfgd, batch=B, seed=99)
+        t = {k: torch.from_numpy(v) for k, v in b.items()}
+        t["pixel_values"] = t["pixel_values"].to(torch.bfloat16)
+        t["intrinsic"] = t["intrinsic"].to(torch.bfloat16)
+        times = []
+        for i in range(iters + 1):
+            for v in P.values():
+                v.grad = None
+            t0 = time.perf_counter()
+            loss, _ = O.forward(P, cfgd, t, zoe)
+            loss.backward()
+            dt = time.perf_counter() - t0
+            log(f"[cpu_baseline] B={B} iter {i}: {dt:.2f}s")
+            if i > 0:
+                times.append(dt)
+        per_b[B] = float(np.median(times))
+    eps = {B: B / t for B, t in per_b.items()}
+    best = max(eps, key=eps.get)
+    return {"value": round(eps[best], 4), "unit": "episodes/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "isa": _cpu_isa(),
+            "sample": "oracle fwd+bwd (bf16, torch CPU), 1 warm-up + %d timed iters per batch, median: %s; value = B=%d"
+                      % (iters, ", ".join(f"B={B} {per_b[B]:.2f}s/step = {eps[B]:.4f} ep/s" for B in batches), best)}
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run this script under torch.distributed.run with one rank
+    per GPU as a child process (nothing here has touched the GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] spawning {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

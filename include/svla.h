@@ -96,19 +96,20 @@ typedef struct {
  * Requirements: ld of every operand and of C a multiple of 8 elements; pointers 16-B aligned; the
  * reduction extent of a KC operand (k_valid, default K) a multiple of 8 (zero-pad: e.g. the lm_head
  * dlogits rows are zero beyond V up to their padded ld). */
+/* workspace: caller-owned stream-K workspace of the 256x256 kernels (256-B aligned, zero-filled once before its
+ * first use, at least svla_gemm_workspace_bytes() for the current device; the kernels leave it zeroed).  NULL =
+ * every output tile runs whole.  GEMMs that run concurrently (other streams, other threads) must use distinct
+ * workspaces; nothing else is shared between calls, so the entry point is re-entrant. */
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
-                   const svla_epilogue* epi, void* stream);
-/* Tuning knob (not a reference interface): GEMM dispatch variant.  0 = auto (default: plain TN stores via
- * hipBLASLt, else the 4-wave or 8-phase 256x256 kernel + stream-K by shape), 1 = two-barrier schedule,
- * 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel,
- * 5 = auto without hipBLASLt (hand-written kernels only).  Returns 0. */
-int svla_gemm_set_variant(int variant);
-/* Stream-K workspace of the 256x256 GEMM (caller-owned, zero-filled once before first use, 256-B aligned,
- * at least svla_gemm_workspace_bytes() for the current device).  Without one (ws = NULL) every output tile
- * runs whole.  GEMMs that use it must be ordered on one stream.  Returns 0 or SVLA_ERR_ARG. */
+                   const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream);
 size_t svla_gemm_workspace_bytes(void);
-int svla_gemm_set_workspace(void* ws, size_t bytes);
+/* svla_gemm_bf16 with an explicit kernel choice (tests / tuning tools, not a reference interface): 0 = auto (as
+ * svla_gemm_bf16), 1 = two-barrier tiles, 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case,
+ * 4 = never the 4-wave kernel, 5 = auto without the small-M GEMV path. */
+int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
+                      void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                      const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Attention.  Reference: eager_attention_forward (model/modeling_gemma2.py:169-195) selected via

@@ -58,10 +58,11 @@ SIGNATURES = {
     "svla_version": (ctypes.c_char_p, []),
     "svla_gemm_bf16": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), ctypes.POINTER(Operand),
                                ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64,
-                               ctypes.POINTER(Epilogue), c_vp]),
-    "svla_gemm_set_variant": (c_i32, [c_i32]),
+                               ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t, c_vp]),
     "svla_gemm_workspace_bytes": (ctypes.c_size_t, []),
-    "svla_gemm_set_workspace": (c_i32, [c_vp, ctypes.c_size_t]),
+    "svla_gemm_bf16_ex": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), ctypes.POINTER(Operand),
+                                  ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64,
+                                  ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t, c_i32, c_vp]),
     "svla_attn_fwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_vp]),
     "svla_attn_bwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, c_vp]),
@@ -126,9 +127,6 @@ def lib() -> ctypes.CDLL:
         with _lock:
             if _lib is None:
                 _lib = load()
-                v = os.environ.get("SVLA_GEMM_VARIANT")  # A/B knob of the 256x256 GEMM main loop (gemm.hip)
-                if v:
-                    _lib.svla_gemm_set_variant(int(v))
     return _lib
 
 

@@ -312,10 +312,10 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           // softcap, round to bf16, per-(row, 128-column group) online-softmax partials (16 lanes share one)
           float mx = -INFINITY, se = 0.f;
           int am = 0x7fffffff;
-          const float cap = E.cap, icap = 1.0f / E.cap;
+          const float cap = E.cap;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf(cap * fast_tanh(round_bf(v[j]) * icap));
+            v[j] = softcap_bf16(v[j], cap);
             if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
           }
 #pragma unroll
@@ -1344,8 +1344,7 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
 }
 
 // In-place rotate_half RoPE over the first rope_cols columns of a bf16 [M][ldc] matrix (heads of rope_D
-// columns), row m at position m % rope_L: the ROPE epilogue as a separate pass, for a GEMM that stored plain
-// bf16 (hipBLASLt).  Same rounding as the epilogue: out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)).
+// columns), row m at position m % rope_L: the ROPE epilogue as a separate pass, for the small-M GEMV path.  Same rounding as the epilogue: out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)).
 // One thread owns 8 columns of the low half of a head and their partners D/2 away, so it reads both before
 // writing either.
 __global__ void rope_inplace_kernel(int64_t M, bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
@@ -1371,29 +1370,6 @@ __global__ void rope_inplace_kernel(int64_t M, bf16_t* __restrict__ c, int64_t l
   }
   *reinterpret_cast<u32x4*>(lo) = pack8(ol);
   *reinterpret_cast<u32x4*>(hi) = pack8(oh);
-}
-
-// The remaining epilogues of a bias GEMM that stored bf16(acc + bias) through hipBLASLt, as one elementwise
-// pass with the fused epilogues' rounding: BIAS_RESID c = bf16(c + in0); BIAS_GELU c = gelu(out1) (out1 holds
-// the stored pre-activation).  N % 8 == 0.
-__global__ void epi_pass_kernel(int kind, int64_t M, int64_t N, bf16_t* __restrict__ c, int64_t ldc,
-                                svla_epilogue E) {
-  const int64_t cpr = N / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * cpr) return;
-  const int64_t m = idx / cpr, n = (idx % cpr) * 8;
-  float v[8], r[8];
-  if (kind == SVLA_EPI_BIAS_RESID) {
-    unpack8(*reinterpret_cast<const u32x4*>(c + m * ldc + n), v);
-    unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.in0 + m * E.ld_in0 + n), r);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] += r[j];
-  } else {
-    unpack8(*reinterpret_cast<const u32x4*>((const bf16_t*)E.out1 + m * E.ld_out1 + n), r);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(r[j]);
-  }
-  *reinterpret_cast<u32x4*>(c + m * ldc + n) = pack8(v);
 }
 
 // Small-M GEMM (M <= 8: the decode step of greedy generation, one or a few token rows): y = x W^T streams
@@ -1492,7 +1468,7 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
   const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t ntn = (N + 127) / 128;
   if (tile >= ntn) return;
-  const float cap = E.cap, icap = 1.0f / E.cap;
+  const float cap = E.cap;
   float mx[GEMV_MAXM], se[GEMV_MAXM];
   int am[GEMV_MAXM];
 #pragma unroll
@@ -1530,7 +1506,7 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
           const int64_t n = r0 + r;
-          const float v = round_bf(cap * fast_tanh(round_bf(wave_sum(acc[r][m])) * icap));
+          const float v = softcap_bf16(wave_sum(acc[r][m]), cap);
           if (n < nend) {
             if (lane == 0) c[m * ldc + n] = f2bf(v);
             if (v > mx[m]) {
@@ -1608,17 +1584,15 @@ int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svl
   return 0;
 }
 
-// dispatch choice (A/B tuning knob): 0 = auto (plain TN stores via hipBLASLt; 4-wave kernel for long-K GEMMs
-// with more than a wave of tiles, else 8-phase + stream-K), 1 = 2-barrier kernel, 2 = 8-phase
-// without stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = auto without
-// hipBLASLt
-int g_variant = 0;
-
-struct SKWorkspace {
-  void* ptr = nullptr;
-  size_t bytes = 0;
+// Per-call dispatch context (no process state: the library is re-entrant across threads and streams).
+// variant (tests / tools only, svla_gemm_bf16_ex): 0 = auto (the 4-wave kernel for long-K GEMMs with more than a
+// wave of tiles, else 8-phase + stream-K, else the 2-barrier tiles), 1 = 2-barrier kernel, 2 = 8-phase without
+// stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = no small-M GEMV path.
+struct GemmCtx {
+  void* ws;          // caller-owned stream-K workspace (slabs + arrival counters), NULL = no stream-K
+  size_t ws_bytes;
+  int variant;
 };
-SKWorkspace g_ws;
 
 int num_cus() {
   static int cus[64] = {0};
@@ -1637,7 +1611,7 @@ int num_cus() {
 size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }
 
 int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
-            const svla_epilogue& E, hipStream_t s) {
+            const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   SKArgs sk;
   memset(&sk, 0, sizeof(sk));
@@ -1652,13 +1626,13 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;  // last wave nearly full: nothing to balance
   const size_t need = sk_workspace_bytes(G);
-  if ((g_variant == 0 || g_variant >= 3) && g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
+  if (ctx.variant != 2 && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
       sk_tiles * sk.nk >= 8 * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
-    sk.slabs = reinterpret_cast<float*>(g_ws.ptr);
-    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(g_ws.ptr) + (size_t)2 * G * 32 * p8::NTH * 16);
+    sk.slabs = reinterpret_cast<float*>(ctx.ws);
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * G * 32 * p8::NTH * 16);
   }
   dim3 grid((unsigned)sk.grid), block(p8::NTH);
   const int la = A.layout, lb = B.layout;
@@ -1676,7 +1650,7 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
 }
 
 int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
-            const svla_epilogue& E, hipStream_t s) {
+            const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   SKArgs sk;
   memset(&sk, 0, sizeof(sk));
@@ -1689,12 +1663,12 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;
   const size_t need = sk_workspace_bytes(G);
-  if (g_ws.ptr && g_ws.bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G && sk_tiles * sk.nk >= 8 * G) {
+  if (ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G && sk_tiles * sk.nk >= 8 * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
-    sk.slabs = reinterpret_cast<float*>(g_ws.ptr);
-    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(g_ws.ptr) + (size_t)2 * G * 32 * p8::NTH * 16);
+    sk.slabs = reinterpret_cast<float*>(ctx.ws);
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * G * 32 * p8::NTH * 16);
   }
   dim3 grid((unsigned)sk.grid), block(p4::NTH);
 #define SVLA_LAUNCH4(LA_, LB_)                                                                       \
@@ -1752,23 +1726,38 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
 
 }  // namespace
 
-extern "C" int svla_gemm_set_variant(int v) {
-  g_variant = v;
-  return 0;
-}
-
 extern "C" size_t svla_gemm_workspace_bytes(void) { return sk_workspace_bytes(num_cus()); }
 
-extern "C" int svla_gemm_set_workspace(void* ws, size_t bytes) {
-  SVLA_CHECK_ARG(ws == nullptr || ((uintptr_t)ws & 255) == 0, "gemm workspace must be 256-B aligned");
-  g_ws.ptr = ws;
-  g_ws.bytes = ws ? bytes : 0;
-  return 0;
-}
+namespace {
+int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
+                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                  const svla_epilogue* epi, const GemmCtx& ctx, void* stream);
+}  // namespace
 
 extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                               void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
-                              const svla_epilogue* epi, void* stream) {
+                              const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream) {
+  return svla_gemm_bf16_ex(M, N, K, A, B, c_ptr, c_seg_start, c_nseg, ldc, epi, workspace, ws_bytes, 0, stream);
+}
+
+extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
+                                 void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                                 const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
+                                 void* stream) {
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 5, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
+  GemmCtx ctx;
+  ctx.ws = workspace;
+  ctx.ws_bytes = workspace ? ws_bytes : 0;
+  ctx.variant = variant;
+  return gemm_dispatch(M, N, K, A, B, c_ptr, c_seg_start, c_nseg, ldc, epi, ctx, stream);
+}
+
+namespace {
+int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
+                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                  const svla_epilogue* epi, const GemmCtx& ctx, void* stream) {
+  const int variant = ctx.variant;
   SVLA_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
                  (long long)K);
   SVLA_CHECK_ARG(epi != nullptr, "gemm: epilogue is NULL");
@@ -1833,13 +1822,11 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
   };
   const bool kseg = (A->nseg > 1 && A->seg_dim == SVLA_SEG_K) || (B->nseg > 1 && B->seg_dim == SVLA_SEG_K);
   const int64_t nk = (K + BK - 1) / BK;
-  const bool sk_ok = (g_variant == 0 || g_variant >= 3) && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
+  const bool sk_ok = variant != 2 && ctx.ws && ctx.ws_bytes >= sk_workspace_bytes(num_cus());
   // 4-wave kernel: ahead of the 8-phase one in the training step (tools/ab_prof.sh: kernel traces of bench.py
   // paired per call) once the k-loop is long enough to amortise its tile prologue/epilogue, the grid has more
   // than a wave of tiles and the epilogue is light -- it runs the epilogue on half the waves, so GEGLU-backward
   // (+31%), softcap-CE (+9%) and RoPE (+2%) stay on the 8-wave kernel, as do short-K / sub-wave shapes
-  // plain TN store (both operands K-contiguous, no epilogue, no segments): hipBLASLt (blaslt.hip), in the auto
-  // variant only; 5 = hand-written kernels for everything
   // decode-sized M: the GEMV path (STORE / GEGLU / ROPE, both operands K-contiguous, plain C)
   {
     const bool ek_ok = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_GEGLU ||
@@ -1848,7 +1835,7 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
                                             : (B->nseg == 1 || (B->seg_dim == SVLA_SEG_OUTER &&
                                                                 epi->kind != SVLA_EPI_SOFTCAP_CE));
     for (int i = 0; i < B->nseg; ++i) b_ok = b_ok && aligned16(B->ptr[i]);
-    if (M <= GEMV_MAXM && ek_ok && b_ok && g_variant != 5 && !epi->accumulate && epi->alpha == 1.0f &&
+    if (M <= GEMV_MAXM && ek_ok && b_ok && variant != 5 && !epi->accumulate && epi->alpha == 1.0f &&
         A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && A->nseg == 1 && K % 8 == 0 &&
         A->ld % 8 == 0 && B->ld % 8 == 0 && (A->r_valid == 0 || A->r_valid >= M) &&
         (A->k_valid == 0 || A->k_valid >= K) && (B->r_valid == 0 || B->r_valid >= N) &&
@@ -1877,54 +1864,26 @@ extern "C" int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operan
       return svla::check_launch("gemm (small-M GEMV)");
     }
   }
-  auto whole = [](const svla_operand* o, int64_t R, int64_t Kx) {
-    return o->nseg == 1 && (o->r_valid == 0 || o->r_valid >= R) && (o->k_valid == 0 || o->k_valid >= Kx);
-  };
-  // RoPE (the Gemma2 q|k|v projection) likewise: hipBLASLt store + the in-place rotate_half pass
-  const bool tn_plain = g_variant == 0 && !epi->accumulate && epi->alpha == 1.0f && A->layout == SVLA_LAYOUT_KC &&
-                        B->layout == SVLA_LAYOUT_KC && whole(A, M, K) && whole(B, N, K) && c_nseg == 1 &&
-                        C.start[0] == 0 && g_ws.ptr && g_ws.bytes >= sk_workspace_bytes(num_cus());
-  // and the SigLIP bias family: bias in hipBLASLt's epilogue, residual / GELU as one elementwise pass
-  const int ek = epi->kind;
-  const bool rope_split = ek == SVLA_EPI_ROPE && epi->rope_D % 16 == 0;
-  const bool bias_split = (ek == SVLA_EPI_BIAS || ek == SVLA_EPI_BIAS_GELU ||
-                           (ek == SVLA_EPI_BIAS_RESID && epi->in0 != C.ptr[0])) && N % 8 == 0;  // in0 read after C
-  if (tn_plain && (ek == SVLA_EPI_STORE || rope_split || bias_split)) {
-    const void* bias = (ek == SVLA_EPI_STORE || ek == SVLA_EPI_ROPE) ? nullptr : epi->bias;
-    void* dst = ek == SVLA_EPI_BIAS_GELU ? epi->out1 : C.ptr[0];
-    const int64_t ldd = ek == SVLA_EPI_BIAS_GELU ? epi->ld_out1 : ldc;
-    if (svla::blaslt_gemm_tn(M, N, K, A->ptr[0], A->ld, B->ptr[0], B->ld, bias, dst, ldd, g_ws.ptr,
-                             (size_t)2 * num_cus() * 32 * p8::NTH * 16, s) == 0) {
-      if (ek == SVLA_EPI_ROPE) {
-        const int64_t work = M * (epi->rope_cols / epi->rope_D) * (epi->rope_D / 16);
-        hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M,
-                           (bf16_t*)C.ptr[0], ldc, *epi);
-      } else if (ek == SVLA_EPI_BIAS_RESID || ek == SVLA_EPI_BIAS_GELU) {
-        const int64_t work = M * (N / 8);
-        hipLaunchKernelGGL(epi_pass_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, ek, M, N,
-                           (bf16_t*)C.ptr[0], ldc, *epi);
-      }
-      return svla::check_launch("gemm (hipBLASLt)");
-    }
-  }
   const int64_t t256 = tiles(256, 256);
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (g_variant == 3 || ((g_variant == 0 || g_variant == 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
+                    (variant == 3 || ((variant == 0 || variant == 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
                                         (t256 >= 512 || K >= 4096) &&
                                         (B->layout == SVLA_LAYOUT_KC || K >= 4096)));  // short-K x RC B: +4%
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
-    if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);
-    if (g_variant != 1 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, s);
+    if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);
+    if (variant != 1 && !kseg) return launch8(M, N, K, *A, *B, C, *epi, ctx, s);
     return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   }
-  if (use4) return launch4(M, N, K, *A, *B, C, *epi, s);
-  if (g_variant != 1 && !kseg && seg_ok(256, 256) &&
+  if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);
+  if (variant != 1 && !kseg && seg_ok(256, 256) &&
       (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
-    return launch8(M, N, K, *A, *B, C, *epi, s);
+    return launch8(M, N, K, *A, *B, C, *epi, ctx, s);
   if (tiles(256, 256) >= 512 && seg_ok(256, 256)) return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   if (tiles(256, 128) >= 256 && seg_ok(256, 128)) return launch<CfgMid>(M, N, K, *A, *B, C, *epi, s);
   SVLA_CHECK_ARG(seg_ok(128, 128), "gemm: segment starts must be multiples of 128");
   return launch<CfgSmall>(M, N, K, *A, *B, C, *epi, s);
 }
+
+}  // namespace

@@ -61,6 +61,12 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return ax < 0.55f ? small : copysignf(big, x);
 }
 // transformers "gelu_pytorch_tanh" == torch.nn.functional.gelu(approximate="tanh")
+// Gemma2 final logit softcap on a bf16 tensor, op by op as the reference (modeling_gemma2.py:994-997):
+// logits / cap, tanh, * cap, each rounded to bf16; true division and the accurate tanhf (argmax runs on these).
+__device__ __forceinline__ float softcap_bf16(float v, float cap) {
+  const float a = round_bf(round_bf(v) / cap);
+  return round_bf(round_bf(tanhf(a)) * cap);
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
@@ -101,9 +107,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 namespace svla {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
-// blaslt.hip: plain TN GEMM through hipBLASLt; 0 = done, nonzero = no plan (run the hand-written kernel)
-int blaslt_gemm_tn(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
-                   const void* bias, void* C, int64_t ldc, void* ws, size_t ws_bytes, hipStream_t s);
 }  // namespace svla
 
 #define SVLA_CHECK_ARG(cond, ...)            \

@@ -1,20 +1,32 @@
 """Data-parallel training step for SpatialVLA on MI355X (replaces the reference's HF Trainer + DeepSpeed
-ZeRO path: train/spatialvla_pretrain.py:383-399, scripts/zero1.json, train/dist_utils.py:29-99).
+ZeRO-1 path: train/spatialvla_pretrain.py:383-399, scripts/zero1.json, train/dist_utils.py:29-99).
 
 Design (one process per GPU, torch.distributed over RCCL/xGMI):
-  * All trainable parameters live in ONE flat bf16 buffer (params are views), their gradients in one
-    flat bf16 buffer: the HIP autograd Functions write dW straight into those views
-    (`param._svla_grad`), so there is no per-parameter grad allocation and no autograd accumulation.
-  * The flat order is the reverse of the forward order (lm_head, final norm, layers 25..0, merge,
-    projector, Ego3D, SigLIP), so buckets complete in backward order.  Buckets are all-reduced
-    (average) as soon as their last layer's backward has produced its gradients (layer hooks), on
-    RCCL's stream, overlapping the rest of the backward; the step waits once before the optimizer.
-  * Gradient clipping (max_grad_norm, Trainer default 1.0) and AdamW (scripts/zero1.json:23-34:
-    betas (0.9, 0.999), eps 1e-8) are two HIP kernels over the flat fp32 master / m / v buffers.
-  * LR schedule: linear warmup (warmup_ratio) then linear decay, as finetune_full.sh:74-77.
+  * All trainable parameters live in ONE flat bf16 buffer (params are views), their gradients in one flat bf16
+    buffer: the HIP autograd Functions write dW straight into those views (`param._svla_grad`), so there is no
+    per-parameter grad allocation and no autograd accumulation.
+  * The flat order is the reverse of the forward order (lm_head, final norm, Gemma2 layers 25..0, spatial
+    embeddings, projector, SigLIP post-LN and layers 26..0, patch embedding, Ego3D MLP), so the buffer fills from
+    the front during backward.  It is cut into buckets (~256 MB) at parameter boundaries.
+  * ZeRO stage 1 (scripts/zero1.json:2-10, "stage": 1, reduce_scatter, overlap_comm, allgather): every bucket is
+    padded to a multiple of world x 64 elements and split into `world` equal chunks; rank r owns chunk r of every
+    bucket -- its fp32 master weights and AdamW moments (the sharded optimizer state) hold just those chunks.
+      - backward: as soon as the layers of a bucket have written their gradients (layer hooks on the Gemma2 and
+        SigLIP layer inputs), the bucket is reduce-scattered (AVG) on RCCL's stream, overlapping the rest of the
+        backward; `finish_reduce()` launches the rest and waits.
+      - step: grad-norm clip (max_grad_norm, Trainer default 1.0) over the owned chunks + one scalar all-reduce,
+        then AdamW (betas 0.9/0.999, eps 1e-8, zero1.json:23-34) on the owned chunks only, then every bucket is
+        all-gathered back into the flat bf16 parameter buffer (async).
+      - forward: each layer waits for the all-gather of its bucket just before it runs (parameter wait points),
+        so the gathers overlap the optimizer of later buckets and the forward of earlier layers.
+    Volume per GPU per step: reduce-scatter + all-gather of the 3.07 B bf16 parameters, 2 x (N-1)/N x 6.14 GB --
+    the same bytes as an all-reduce -- while AdamW touches 1/N of the parameters (28 B/param -> 86 GB / N).
+  * world == 1: no collectives, one AdamW launch over the whole flat buffer.
+  * LR schedule: linear warmup (warmup_ratio) then linear decay, as finetune_full.sh:74-77 with the HF Trainer's
+    get_linear_schedule_with_warmup.
 """
 import math
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 import re
 
@@ -49,85 +61,125 @@ def _group_params(gmod) -> List[torch.nn.Parameter]:
     return out
 
 
-def _forward_order(model) -> List[torch.nn.Parameter]:
-    """Trainable parameters in backward-completion order (reverse of the forward pass)."""
-    seen, order = set(), []
+# Parameter wait points of the forward (ZeRO all-gather), in execution order: "pre" (start of forward:
+# embeddings, projector, Ego3D, spatial tokens), ("siglip", i), ("gemma", i), "head" (final norm + lm_head).
+def _param_groups(model):
+    """[(wait point, module)] in backward-completion order (the flat buffer order)."""
     lm = model.language_model
-    groups = [lm.lm_head, lm.model.norm] + list(reversed(list(lm.model.layers)))
+    nl = len(lm.model.layers)
+    groups = [("head", lm.lm_head), ("head", lm.model.norm)]
+    groups += [(("gemma", i), lm.model.layers[i]) for i in reversed(range(nl))]
     if getattr(model, "spatial_embed_tokens", None) is not None:
-        groups.append(model.spatial_embed_tokens)
-    groups.append(model.multi_modal_projector)
-    if getattr(model, "position_embedding_3d", None) is not None:
-        groups.append(model.position_embedding_3d)
+        groups.append(("pre", model.spatial_embed_tokens))
+    groups.append(("pre", model.multi_modal_projector))
     vt = model.vision_tower.vision_model
-    groups += [vt.post_layernorm] + list(reversed(list(vt.encoder.layers))) + [vt.embeddings]
-    for gmod in groups:
-        for p in _group_params(gmod):
-            if p.requires_grad and id(p) not in seen:
-                seen.add(id(p))
-                order.append(p)
-    for p in model.parameters():  # anything not covered above (kept last)
-        if p.requires_grad and id(p) not in seen:
-            seen.add(id(p))
-            order.append(p)
-    return order
+    ns = len(vt.encoder.layers)
+    groups.append(("pre", vt.post_layernorm))
+    groups += [(("siglip", i), vt.encoder.layers[i]) for i in reversed(range(ns))]
+    groups.append(("pre", vt.embeddings))
+    if getattr(model, "position_embedding_3d", None) is not None:
+        # not ordered by a data dependency against the SigLIP layer hooks: kept after every hooked group
+        groups.append(("pre", model.position_embedding_3d))
+    return groups
 
 
-class GradExchange:
-    """Bucketed, overlappable DP gradient averaging over a flat gradient buffer (RCCL all-reduce with
-    AVG on the nccl backend; SUM + divide on gloo, which has no AVG).  Buckets are cut at parameter
-    boundaries (`offsets`) once they reach `bucket_bytes`; `on_layer_grad(i)` launches every bucket whose
-    parameters all end before the end of layer i's last parameter in the flat order."""
+def _wait_rank(point, n_siglip):
+    if point == "pre":
+        return 0
+    if point == "head":
+        return 10 ** 6
+    kind, i = point
+    return 1 + i if kind == "siglip" else 1 + n_siglip + i
 
-    def __init__(self, flat_grad: torch.Tensor, offsets: List[int], bucket_bytes: int = 256 << 20,
-                 process_group=None):
-        self.flat = flat_grad
-        self.offsets = list(offsets)
-        self.numel = flat_grad.numel()
+
+class ZeroExchange:
+    """ZeRO-1 collectives over the flat gradient / parameter buffers (see the module docstring).  `buckets` are
+    (start, end) element ranges, each a multiple of world x 64 long; rank r owns [start + r*c, start + (r+1)*c),
+    c = (end - start) / world, of every bucket."""
+
+    def __init__(self, flat_param, flat_grad, buckets, process_group=None):
+        self.fp, self.fg = flat_param, flat_grad
+        self.buckets = buckets
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.buckets = []
-        start = 0
-        cap = max(1, bucket_bytes // flat_grad.element_size())
-        for i in range(len(self.offsets)):
-            end = self.offsets[i + 1] if i + 1 < len(self.offsets) else self.numel
-            if end - start >= cap or i + 1 == len(self.offsets):
-                self.buckets.append((start, end))
-                start = end
-        self.layer_ready: List[int] = []
-        self._pending = []
-        self._launched = set()
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.nccl = self.world > 1 and dist.get_backend(process_group) == "nccl"
+        self.chunk = [(e - s) // self.world for s, e in buckets]
+        self._rs = {}        # bucket -> pending reduce-scatter (work, out-of-place buffer or None)
+        self._ag = {}        # bucket -> pending all-gather (work, out-of-place buffer or None)
+        self.ready_end: Dict[object, int] = {}  # grad hook point -> flat index below which every grad is written
+        self.wait_buckets: Dict[object, List[int]] = {}  # parameter wait point -> buckets to wait for
 
-    def on_layer_grad(self, layer_idx: int):
-        last = self.layer_ready[layer_idx] if layer_idx < len(self.layer_ready) else -1
-        if last < 0:
+    def owned(self, b):
+        """(flat start, length) of this rank's chunk of bucket b."""
+        s, _ = self.buckets[b]
+        c = self.chunk[b]
+        return s + self.rank * c, c
+
+    # ---------------------------------------------------------------- backward: reduce-scatter
+    def on_grads_ready(self, point):
+        end = self.ready_end.get(point)
+        if end is None or self.world == 1:
             return
-        ready_end = self.offsets[last + 1] if last + 1 < len(self.offsets) else self.numel
-        for bi, (s, e) in enumerate(self.buckets):
-            if e <= ready_end and bi not in self._launched:
-                self._launch(bi)
+        for b, (s, e) in enumerate(self.buckets):
+            if e <= end and b not in self._rs:
+                self._reduce_scatter(b)
 
-    def _launch(self, bi):
-        s, e = self.buckets[bi]
-        self._launched.add(bi)
-        op = dist.ReduceOp.AVG if dist.get_backend(self.pg) == "nccl" else dist.ReduceOp.SUM
-        work = dist.all_reduce(self.flat[s:e], op=op, group=self.pg, async_op=True)
-        self._pending.append((bi, work, op))
+    def _reduce_scatter(self, b):
+        s, e = self.buckets[b]
+        o, c = self.owned(b)
+        src = self.fg[s:e]
+        if self.nccl:  # in place: the output is this rank's chunk of the input (NCCL's in-place form)
+            w = dist.reduce_scatter_tensor(self.fg[o:o + c], src, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
+            self._rs[b] = (w, None)
+        else:  # gloo (CPU tests, shared-GPU rehearsals): sum-all-reduce a copy, keep this rank's chunk
+            tmp = src.float()
+            w = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            self._rs[b] = (w, tmp)
 
-    def finish(self):
-        """Launch whatever is left and wait for every bucket (stream-ordered on nccl)."""
+    def finish_reduce(self):
+        """Launch the buckets no hook covered and wait for every reduce-scatter (stream-ordered on nccl)."""
         if self.world == 1:
             return
-        for bi in range(len(self.buckets)):
-            if bi not in self._launched:
-                self._launch(bi)
-        for bi, work, op in self._pending:
-            work.wait()
-            if op == dist.ReduceOp.SUM:
-                s, e = self.buckets[bi]
-                self.flat[s:e].div_(self.world)
-        self._pending.clear()
-        self._launched.clear()
+        for b in range(len(self.buckets)):
+            if b not in self._rs:
+                self._reduce_scatter(b)
+        for b, (w, out) in self._rs.items():
+            w.wait()
+            if out is not None:
+                o, c = self.owned(b)
+                r = o - self.buckets[b][0]
+                self.fg[o:o + c].copy_(out[r:r + c] / self.world)
+        self._rs.clear()
+
+    # ---------------------------------------------------------------- step: all-gather
+    def all_gather(self, b):
+        if self.world == 1:
+            return
+        s, e = self.buckets[b]
+        o, c = self.owned(b)
+        if self.nccl:  # in place: the input is this rank's chunk of the output
+            self._ag[b] = (dist.all_gather_into_tensor(self.fp[s:e], self.fp[o:o + c], group=self.pg, async_op=True),
+                           None)
+        else:
+            parts = [torch.empty(c, dtype=self.fp.dtype, device=self.fp.device) for _ in range(self.world)]
+            self._ag[b] = (dist.all_gather(parts, self.fp[o:o + c].clone(), group=self.pg, async_op=True), parts)
+
+    def _land(self, b):
+        w, parts = self._ag.pop(b)
+        w.wait()
+        if parts is not None:
+            s, e = self.buckets[b]
+            self.fp[s:e].copy_(torch.cat(parts))
+
+    def wait_params(self, point):
+        for b in self.wait_buckets.get(point, ()):
+            if b in self._ag:
+                self._land(b)
+
+    def wait_all_params(self):
+        for b in list(self._ag):
+            self._land(b)
 
 
 class TrainEngine:
@@ -135,8 +187,13 @@ class TrainEngine:
 
     def __init__(self, model, lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  max_grad_norm: float = 1.0, warmup_ratio: float = 0.005, total_steps: int = 1000,
-                 process_group=None, bucket_bytes: int = 256 << 20, overlap: bool = True):
+                 process_group=None, bucket_bytes: int = 256 << 20, overlap: bool = True, kernels=None):
+        """kernels: the optimizer kernel module (sumsq / clip_scale / adamw); the libsvla wrappers unless a test
+        injects a stand-in to exercise the exchange logic without a GPU."""
         self.model = model
+        self.K = kernels if kernels is not None else K
+        if hasattr(model, "clear_decode_cache"):  # captured decode graphs point at the storage rebound below
+            model.clear_decode_cache()
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.warmup_steps = max(1, int(math.ceil(warmup_ratio * total_steps)))
@@ -144,62 +201,156 @@ class TrainEngine:
         self.step_count = 0
         dev = next(model.parameters()).device
         self.device = dev
-        params = _forward_order(model)
-        self.params = params
-        offs, n = [], 0
-        for p in params:
+        world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = world
+
+        # ---- flat layout: parameters in backward order, buckets cut at parameter boundaries and padded to a
+        # multiple of world * ALIGN elements (the ZeRO chunks of every rank are equal and aligned)
+        seen, entries = set(), []   # (param, wait point, group index)
+        groups = _param_groups(model)
+        for gi, (point, gmod) in enumerate(groups):
+            for p in _group_params(gmod):
+                if p.requires_grad and id(p) not in seen:
+                    seen.add(id(p))
+                    entries.append((p, point, gi))
+        for p in model.parameters():  # anything not covered above (kept last, waited at the start of forward)
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                entries.append((p, "pre", len(groups)))
+        cap = max(1, bucket_bytes // 2)
+        quant = world * self.ALIGN
+        offs, buckets, n, bstart = [], [], 0, 0
+        for i, (p, _, _) in enumerate(entries):
             offs.append(n)
             n += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-        self.numel = n
+            if n - bstart >= cap or i + 1 == len(entries):
+                n = (n + quant - 1) // quant * quant
+                buckets.append((bstart, n))
+                bstart = n
+        self.params = [e[0] for e in entries]
         self.offsets = offs
+        self.numel = n
+        self.buckets = buckets
         self.flat_param = torch.zeros(n, dtype=BF16, device=dev)
         self.flat_grad = torch.zeros(n, dtype=BF16, device=dev)
-        self.master = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
         with torch.no_grad():
-            for p, o in zip(params, offs):
+            for p, o in zip(self.params, offs):
                 view = self.flat_param[o:o + p.numel()].view_as(p)
                 view.copy_(p.data.to(BF16))
                 p.data = view
                 p._svla_grad = self.flat_grad[o:o + p.numel()].view_as(p)
                 p._svla_accum = False
-                self.master[o:o + p.numel()].copy_(view.reshape(-1).float())
+        self.exchange = ZeroExchange(self.flat_param, self.flat_grad, buckets, process_group)
+        ex = self.exchange
+        # ---- sharded optimizer state: fp32 master / m / v of the owned chunk of every bucket, back to back
+        self.shard_offsets, sn = [], 0
+        for b in range(len(buckets)):
+            self.shard_offsets.append(sn)
+            sn += ex.owned(b)[1]
+        self.shard_numel = sn
+        self.master = torch.empty(sn, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(sn, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(sn, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for b in range(len(buckets)):
+                o, c = ex.owned(b)
+                so = self.shard_offsets[b]
+                self.master[so:so + c].copy_(self.flat_param[o:o + c].float())
+        self.sumsq_parts = torch.zeros(len(buckets), dtype=torch.float32, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.clip = torch.ones(1, dtype=torch.float32, device=dev)
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.exchange = GradExchange(self.flat_grad, offs, bucket_bytes, process_group)
-        self.buckets = self.exchange.buckets
-        if overlap and self.exchange.world > 1:
-            lm = self.model.language_model.model
-            pid = {id(p): i for i, p in enumerate(params)}
-            ready = []
-            for layer in lm.layers:
-                idx = [pid[id(p)] for p in layer.parameters() if id(p) in pid]
-                ready.append(max(idx) if idx else -1)
-            self.exchange.layer_ready = ready
-            lm._svla_layer_grad_hook = self.exchange.on_layer_grad
+
+        # ---- hook points: gradient readiness (backward) and parameter waits (forward)
+        ends: Dict[int, int] = {}
+        for (p, point, gi), o in zip(entries, offs):
+            ends[gi] = o + p.numel()
+        hookable = {}
+        for gi, (point, gmod) in enumerate(groups):
+            if isinstance(point, tuple) and gi in ends:
+                # the input grad of layer i is complete => every group before it in the flat order is written
+                hookable[point] = max(v for g, v in ends.items() if g <= gi)
+        ex.ready_end = hookable
+        ns = len(model.vision_tower.vision_model.encoder.layers)
+        first_wait = {}
+        for (p, point, gi), o in zip(entries, offs):
+            for b, (s, e) in enumerate(buckets):
+                if s <= o < e:
+                    r = _wait_rank(point, ns)
+                    if b not in first_wait or r < first_wait[b][0]:
+                        first_wait[b] = (r, point)
+        for b, (r, point) in first_wait.items():
+            ex.wait_buckets.setdefault(point, []).append(b)
+        self.gather_order = sorted(first_wait, key=lambda b: first_wait[b][0])
+        if world > 1:
+            lm = model.language_model.model
+            vt = model.vision_tower.vision_model
+            if overlap:
+                lm._svla_layer_grad_hook = lambda i: ex.on_grads_ready(("gemma", i))
+                vt._svla_layer_grad_hook = lambda i: ex.on_grads_ready(("siglip", i))
+            for mod in (model, model.language_model, lm, vt):  # wait points: "pre", ("siglip", i), ("gemma", i), "head"
+                mod._svla_param_wait = ex.wait_params
 
     # ------------------------------------------------------------------ optimizer
     def lr_at(self, step: int) -> float:
-        if step <= self.warmup_steps:
-            return self.lr * step / self.warmup_steps
+        """transformers get_linear_schedule_with_warmup's lr_lambda at scheduler step `step` (0-based): the HF
+        Trainer's optimizer step k runs at lr_lambda(k - 1) (LambdaLR steps after the optimizer), so the first
+        update of a warmup run has lr 0."""
+        if step < self.warmup_steps:
+            return self.lr * step / max(1, self.warmup_steps)
         return self.lr * max(0.0, (self.total_steps - step) / max(1, self.total_steps - self.warmup_steps))
 
     def optimizer_step(self):
+        """clip + AdamW on the owned chunks, then the parameter all-gathers (left in flight: the next forward's
+        layers wait for their own bucket)."""
         self.step_count += 1
-        K.sumsq(self.flat_grad, self.sumsq)
-        K.clip_scale(self.sumsq, self.max_grad_norm, self.clip, self.gnorm)
-        K.adamw(self.master, self.flat_param, self.flat_grad, self.m, self.v, self.lr_at(self.step_count),
-                self.betas[0], self.betas[1], self.eps, self.wd, self.step_count, self.clip)
+        lr = self.lr_at(self.step_count - 1)
+        ex = self.exchange
+        Kx = self.K
+        if self.world == 1:
+            Kx.sumsq(self.flat_grad, self.sumsq)
+        else:
+            for b in range(len(self.buckets)):
+                o, c = ex.owned(b)
+                Kx.sumsq(self.flat_grad[o:o + c], self.sumsq_parts[b:b + 1])
+            torch.sum(self.sumsq_parts, 0, keepdim=True, out=self.sumsq)
+            dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=ex.pg)
+        Kx.clip_scale(self.sumsq, self.max_grad_norm, self.clip, self.gnorm)
+        if self.world == 1:
+            Kx.adamw(self.master, self.flat_param, self.flat_grad, self.m, self.v, lr, self.betas[0], self.betas[1],
+                    self.eps, self.wd, self.step_count, self.clip)
+            return
+        for b in self.gather_order:
+            o, c = ex.owned(b)
+            so = self.shard_offsets[b]
+            Kx.adamw(self.master[so:so + c], self.flat_param[o:o + c], self.flat_grad[o:o + c], self.m[so:so + c],
+                    self.v[so:so + c], lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count, self.clip)
+            ex.all_gather(b)
 
     def train_step(self, batch: Dict[str, torch.Tensor]):
-        """forward + backward + DP all-reduce + clip + AdamW; returns the loss tensor (no host sync)."""
+        """forward + backward + ZeRO-1 exchange + clip + AdamW; returns the loss tensor (no host sync)."""
         out = self.model(**batch, return_dict=True)
         out.loss.backward()
-        self.exchange.finish()
+        self.exchange.finish_reduce()
         self.optimizer_step()
         return out.loss.detach()
+
+    def sync_params(self):
+        """Wait for every parameter all-gather still in flight (before evaluation or saving)."""
+        self.exchange.wait_all_params()
+
+    def full_master(self) -> torch.Tensor:
+        """The fp32 master weights in the flat layout (gathered across ranks; tests / checkpoints)."""
+        ex = self.exchange
+        if self.world == 1:
+            return self.master.clone()
+        out = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        for b, (s, e) in enumerate(self.buckets):
+            so, c = self.shard_offsets[b], ex.chunk[b]
+            parts = [torch.empty(c, dtype=torch.float32, device=self.device) for _ in range(self.world)]
+            dist.all_gather(parts, self.master[so:so + c].contiguous(), group=ex.pg)
+            out[s:e].copy_(torch.cat(parts))
+        return out
 
 
 def random_init_(model, seed: int = 0, std: float = 0.02):

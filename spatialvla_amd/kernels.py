@@ -87,30 +87,40 @@ def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=
 _gemm_ws: dict = {}
 
 
-def _ensure_gemm_workspace():
-    """Register the stream-K workspace of the 256x256 GEMM once per process (zero-filled, caller-owned)."""
-    dev = torch.cuda.current_device()
-    if dev not in _gemm_ws:
+def gemm_workspace(stream=None) -> torch.Tensor:
+    """The caller-owned stream-K workspace of svla_gemm_bf16 for one (device, stream): GEMMs on different streams
+    never share one (include/svla.h).  Zero-filled once; the kernels leave it zeroed."""
+    s = stream if stream is not None else torch.cuda.current_stream()
+    key = (s.device.index, s.cuda_stream)
+    buf = _gemm_ws.get(key)
+    if buf is None:
         n = int(L.lib().svla_gemm_workspace_bytes())
-        buf = torch.zeros(n, dtype=torch.uint8, device=f"cuda:{dev}")
-        L.check(L.lib().svla_gemm_set_workspace(buf.data_ptr(), n), "svla_gemm_set_workspace")
-        _gemm_ws[dev] = buf
+        buf = torch.zeros(n + 256, dtype=torch.uint8, device=s.device)
+        off = (-buf.data_ptr()) % 256
+        buf = buf[off:off + n]
+        _gemm_ws[key] = buf
+    return buf
 
 
 gemm_log: Optional[list] = None  # tools: when a list, every svla_gemm_bf16 call appends its shape/layouts/epilogue
+gemm_variant: int = int(os.environ.get("SVLA_GEMM_VARIANT", "0"))  # tests / tools: kernel choice (svla_gemm_bf16_ex)
 
 
 def gemm(M: int, N: int, K: int, A: L.Operand, B: L.Operand, c_mats: Sequence[Optional[torch.Tensor]],
-         c_starts: Sequence[int], ldc: int, epi: L.Epilogue):
-    if not _gemm_ws:
-        _ensure_gemm_workspace()
+         c_starts: Sequence[int], ldc: int, epi: L.Epilogue, variant: Optional[int] = None):
     if gemm_log is not None:
         gemm_log.append((M, N, K, int(A.layout), int(B.layout), int(epi.kind), int(epi.accumulate)))
     n = len(c_mats)
     cp = (ctypes.c_void_p * 4)(*([_ptr(c) for c in c_mats] + [None] * (4 - n)))
     cs = (ctypes.c_int64 * 5)(*([int(s) for s in c_starts] + [0] * (5 - n)))
-    rc = L.lib().svla_gemm_bf16(M, N, K, ctypes.byref(A), ctypes.byref(B), cp, cs, n, ldc, ctypes.byref(epi),
-                                _stream())
+    ws = gemm_workspace()
+    v = gemm_variant if variant is None else variant
+    if v:
+        rc = L.lib().svla_gemm_bf16_ex(M, N, K, ctypes.byref(A), ctypes.byref(B), cp, cs, n, ldc, ctypes.byref(epi),
+                                       ws.data_ptr(), ws.numel(), int(v), _stream())
+    else:
+        rc = L.lib().svla_gemm_bf16(M, N, K, ctypes.byref(A), ctypes.byref(B), cp, cs, n, ldc, ctypes.byref(epi),
+                                    ws.data_ptr(), ws.numel(), _stream())
     L.check(rc, "svla_gemm_bf16")
 
 

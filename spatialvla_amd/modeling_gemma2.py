@@ -263,15 +263,20 @@ class Gemma2Model(nn.Module):
             return self._forward_cached(hidden_states, attention_mask, rope, cache), None
         all_h = () if output_hidden_states else None
         hook = getattr(self, "_svla_layer_grad_hook", None)
+        pwait = getattr(self, "_svla_param_wait", None)  # ZeRO-1: parameters of layer i all-gathered (engine.py)
         for i, layer in enumerate(self.layers[: self.config.num_hidden_layers]):
             if output_hidden_states:
                 all_h += (hidden_states,)
             if hook is not None and hidden_states.requires_grad:
                 # fires once d(layer input) is complete, i.e. after every weight grad of layers >= i
                 hidden_states.register_hook(lambda g, i=i: hook(i))
+            if pwait is not None:
+                pwait(("gemma", i))
             hidden_states = layer(hidden_states, attention_mask, rope, cache)
         if cache is not None:
             cache.seen_tokens += hidden_states.shape[1]
+        if pwait is not None:
+            pwait("head")
         hidden_states = self.norm(hidden_states)
         if output_hidden_states:
             all_h += (hidden_states,)
@@ -284,6 +289,11 @@ class Gemma2Model(nn.Module):
         input_layernorm (or the final norm) -- bitwise the reference order (:475-496, :777), two norm launches per
         layer instead of four."""
         layers = self.layers[: self.config.num_hidden_layers]
+        pwait = getattr(self, "_svla_param_wait", None)
+        if pwait is not None:
+            for i in range(len(layers)):
+                pwait(("gemma", i))
+            pwait("head")
         shp = hidden.shape
         H = shp[-1]
         res = hidden.reshape(-1, H).contiguous()
@@ -332,6 +342,9 @@ class Gemma2ForCausalLM(nn.Module):
 
     def head(self, hidden_states, target, stash):
         """lm_head + softcap (reference :993-997) fused with the shifted CE; returns (logits2d, loss)."""
+        pwait = getattr(self, "_svla_param_wait", None)
+        if pwait is not None:
+            pwait("head")
         cap = float(self.config.final_logit_softcapping or 0.0)
         if cap <= 0:
             raise ValueError("final_logit_softcapping must be set for the fused softcap/CE head")

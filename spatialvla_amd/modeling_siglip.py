@@ -107,7 +107,13 @@ class SiglipVisionTransformer(nn.Module):
         B = pixel_values.shape[0]
         h = self.embeddings(pixel_values)
         Lq = self.embeddings.num_patches
-        for layer in self.encoder.layers:
+        hook = getattr(self, "_svla_layer_grad_hook", None)  # DP: gradients of layers >= i written (engine.py)
+        pwait = getattr(self, "_svla_param_wait", None)      # ZeRO-1: parameters of layer i all-gathered
+        for i, layer in enumerate(self.encoder.layers):
+            if hook is not None and h.requires_grad:
+                h.register_hook(lambda g, i=i: hook(i))
+            if pwait is not None:
+                pwait(("siglip", i))
             h = layer(h, B, Lq)
         h = Fn.LayerNormFn.apply(h, self.post_layernorm.weight, self.post_layernorm.bias, self.post_layernorm.eps, None)
         return h.view(B, Lq, -1)

@@ -215,8 +215,14 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                        self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
         return xyz
 
+    def _wait_params(self):
+        pwait = getattr(self, "_svla_param_wait", None)  # ZeRO-1: embeddings / projector / Ego3D all-gathered
+        if pwait is not None:
+            pwait("pre")
+
     def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor, kinv=None):
         """Reference :308-333 -> [B, np, H_text]."""
+        self._wait_params()
         dt = self.multi_modal_projector.linear.weight.dtype
         pv = pixel_values.to(dt).contiguous()
         sig_in = torch.empty_like(pv)
@@ -235,6 +241,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
 
     # ------------------------------------------------------------------ forward
     def _merge_inputs(self, input_ids, image_features):
+        self._wait_params()
         cfg = self.config
         B, Lq = input_ids.shape
         dev = input_ids.device
@@ -399,18 +406,51 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         intr = intr.to(dev, torch.bfloat16) if intr is not None else None
         return ids, pv, intr, model_inputs.get("attention_mask"), dev
 
+    DECODE_STATES_MAX = 2      # decode states (KV cache + captured graphs) kept per model, least recently used out
+    DECODE_CAPACITY_STEP = 64  # cache capacities are bucketed: prompts of nearby lengths share one state
+
+    def clear_decode_cache(self):
+        """Drop every persistent decode state (KV caches, captured prefill/decode graphs and their memory pool).
+        The graphs hold raw pointers to the weights they were captured with, so anything that rebinds parameter
+        storage (TrainEngine's flat buffers, load_state_dict with assign, .to()) must call this."""
+        self.__dict__["_svla_decode_states"] = {}
+
+    @staticmethod
+    def _reject_padding(am):
+        """Padded prompts are not supported by the HIP decode path: the reference's generate derives per-row
+        positions from attention_mask.cumsum(-1) - 1 (+1, modeling_gemma2.py:1039-1042,
+        modeling_spatialvla.py:473-474), while the fused RoPE here uses one position table for every row.
+        Raise instead of silently rotating padded rows with the wrong phases."""
+        if am is not None and bool((am == 0).any()):
+            raise ValueError("predict_action: padded prompts (attention_mask with zeros) are not supported on the "
+                             "HIP path; run equal-length prompts (one call per prompt length)")
+
     def _decode_state(self, B: int, capacity: int, dev):
-        """Persistent decode state per (batch, capacity): the KV cache, the static token buffer the captured
-        graphs read, and the graphs themselves keyed by cache position.  Reused across predict_action calls, so
-        a control loop with a fixed prompt length replays the same graphs every call."""
-        states = self.__dict__.setdefault("_svla_decode_states", {})
-        key = (B, capacity, str(dev))
+        """Persistent decode state per (batch, bucketed capacity): the KV cache, the static token buffer the captured
+        graphs read, the graphs themselves keyed by cache position (one private memory pool shared by all of a
+        state's graphs), and one side stream for their eager warm-ups.  Reused across predict_action calls, so a
+        control loop replays the same graphs every call; at most DECODE_STATES_MAX states are kept (LRU)."""
+        from collections import OrderedDict
+        states = self.__dict__.get("_svla_decode_states")
+        if not isinstance(states, OrderedDict):
+            states = self.__dict__["_svla_decode_states"] = OrderedDict()
+        cap = -(-capacity // self.DECODE_CAPACITY_STEP) * self.DECODE_CAPACITY_STEP
+        key = (B, cap, str(dev))
         st = states.get(key)
+        wptr = self.language_model.lm_head.weight.data_ptr()
+        if st is not None and st["wptr"] != wptr:  # weights were rebound since capture: the graphs are stale
+            states.pop(key)
+            st = None
         if st is None:
-            st = {"cache": self.new_cache(B, capacity), "graphs": {}, "prefill": {},
+            while len(states) >= self.DECODE_STATES_MAX:
+                states.popitem(last=False)
+            st = {"cache": self.new_cache(B, cap), "graphs": {}, "prefill": {}, "wptr": wptr,
                   "tok": torch.zeros(B, 1, dtype=torch.int64, device=dev),
-                  "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev))}
+                  "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev)),
+                  "pool": torch.cuda.graph_pool_handle() if dev.type == "cuda" else None,
+                  "side": torch.cuda.Stream(device=dev) if dev.type == "cuda" else None}
             states[key] = st
+        states.move_to_end(key)
         return st
 
     def _prefill_body(self, st, x):
@@ -440,15 +480,15 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         g = st["prefill"].get(key)
         if g is None:
             static = {k: (v.clone() if v is not None else None) for k, v in x.items()}
-            side = torch.cuda.Stream(device=x["ids"].device)
+            side = st["side"]
             side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):  # eager warm-up: lazy kernel attributes, hipBLASLt plans, Zoe caches
+            with torch.cuda.stream(side):  # eager warm-up: lazy kernel attributes, GEMM workspaces, Zoe caches
                 self._prefill_body(st, static)
             cache.seen_tokens = 0
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(graph):
+                with torch.cuda.graph(graph, pool=st["pool"]):
                     out = self._prefill_body(st, static)
             except RuntimeError as e:  # an op of the prefill cannot be captured: run this shape eagerly from now on
                 cache.seen_tokens = 0
@@ -485,14 +525,14 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         cache = st["cache"]
         g = st["graphs"].get(p0)
         if g is None:
-            side = torch.cuda.Stream(device=st["tok"].device)
+            side = st["side"]
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):  # eager warm-up (lazy kernel attributes); rewrites row p0 identically
                 self._decode_body(st, p0)
             cache.seen_tokens = p0
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with torch.cuda.graph(graph, pool=st["pool"]):
                 out = self._decode_body(st, p0)
             cache.seen_tokens = p0
             g = st["graphs"][p0] = (graph, out)
@@ -508,6 +548,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         after step 0 (:475-476), attending to the prompt and every earlier generated token.  Stops when every
         sequence has emitted eos or after max_new_tokens."""
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
+        self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         graphs = self.decode_graphs and dev.type == "cuda"
@@ -553,6 +594,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         """The same greedy decode as full re-forwards over prompt + generated tokens (no cache): prompt keys
         class 0, generated keys class 1.  Kept as the parity reference of the cached path."""
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
+        self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         feats = self.get_image_features(pv, intr) if pv is not None else None

@@ -1,0 +1,97 @@
+"""Data-parallel training on the HIP path: 2 ranks (gloo, both on cuda:0 -- the GPU box has one card) each run
+TrainEngine.train_step on half of a batch; the result must equal one process running train_step on the whole
+(concatenated) batch -- the ZeRO-1 exchange of scripts/zero1.json through spatialvla_amd.engine.
+
+Tolerances: per-rank losses average to the single-process loss (1e-3 relative); after 2 AdamW steps at lr 1e-3
+every bf16 parameter agrees to 2 bf16 ulps of its magnitude and the fp32 master weights to 2e-3 relative L2 per
+tensor (the gradients differ by the bf16 rounding of each rank's partial sum before the average)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 2
+B_TOTAL = 4
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(device):
+    from spatialvla_amd import presets
+    cfgd = H.cfg_dict("tiny")
+    return [H.batch_tensors(presets.synthetic_batch(cfgd, batch=B_TOTAL, seed=50 + s), device) for s in range(STEPS)]
+
+
+def _run(rank, world, device):
+    from spatialvla_amd.engine import TrainEngine
+    model = H.build_hip_model(H.cfg_dict("tiny"), device)
+    depth = torch.rand(B_TOTAL, 1, 224, 224, generator=torch.Generator().manual_seed(9)).mul(3).add(0.5).to(device)
+    per = B_TOTAL // world
+    model.predict_depth = lambda pv, _d=depth[rank * per:(rank + 1) * per]: _d
+    eng = TrainEngine(model, lr=1e-3, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0,
+                      bucket_bytes=1 << 16)
+    losses = []
+    for b in _batches(device):
+        part = {k: v[rank * per:(rank + 1) * per] for k, v in b.items()}
+        losses.append(float(eng.train_step(part).item()))
+    eng.sync_params()
+    full = eng.full_master().cpu()
+    names = {id(p): n for n, p in model.named_parameters()}
+    master = {names[id(p)]: full[o:o + p.numel()].numpy().copy() for p, o in zip(eng.params, eng.offsets)}
+    params = {n: p.detach().float().cpu().numpy().copy() for n, p in model.named_parameters() if p.requires_grad}
+    return losses, master, params, float(eng.gnorm.item()), len(eng.buckets)
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank,) + _run(rank, world, "cuda:0"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp2_train_step_equals_single_process(cuda):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    losses1, master1, params1, gnorm1, _ = _run(0, 1, "cuda:0")
+    nb = res[0][5]
+    assert nb > 3  # small buckets: the exchange really is bucketed
+    for s in range(STEPS):
+        mean = np.mean([r[1][s] for r in res])
+        assert abs(mean - losses1[s]) <= 1e-3 * abs(losses1[s]), (s, mean, losses1[s])
+    assert res[0][4] == pytest.approx(gnorm1, rel=1e-2)
+    for n, ref in params1.items():
+        for r in res:
+            got = r[3][n]
+            tol = 2 * 2.0 ** -7 * np.abs(ref).max() + 1e-6
+            assert np.abs(got - ref).max() <= tol, (n, r[0])
+            m_ref, m_got = master1[n], r[2][n]
+            assert np.linalg.norm(m_got - m_ref) <= 2e-3 * np.linalg.norm(m_ref) + 1e-6, (n, r[0])
+    for n in params1:  # ranks agree bitwise after the all-gather
+        assert np.array_equal(res[0][3][n], res[1][3][n]), n

@@ -40,18 +40,18 @@ def test_gemm_layouts(cuda, M, N, K, layouts):
 
 
 def _variants(fn):
-    """Run fn() under the GEMM dispatch variants: 1 = 2-barrier, 2 = 8-phase, 0 = product dispatch (twice;
-    plain TN stores go to hipBLASLt), 3 = 4-wave kernel wherever both operands are KC (twice), 4 = 8-phase +
-    stream-K, 5 = product dispatch with hand-written kernels only.  Returns {variant: result}."""
-    from spatialvla_amd import _lib as L
+    """Run fn() under the GEMM dispatch variants (svla_gemm_bf16_ex): 1 = 2-barrier, 2 = 8-phase, 0 = product
+    dispatch (twice), 3 = 4-wave kernel wherever both operands are KC (twice), 4 = 8-phase + stream-K, 5 = product
+    dispatch without the small-M GEMV path.  Returns {variant: result}."""
+    from spatialvla_amd import kernels as Kn
     outs = {}
     try:
         for v in (1, 2, 0, "0b", 3, "3b", 4, 5):
-            L.lib().svla_gemm_set_variant({"0b": 0, "3b": 3}.get(v, v))
+            Kn.gemm_variant = {"0b": 0, "3b": 3}.get(v, v)
             outs[v] = fn()
             torch.cuda.synchronize()
     finally:
-        L.lib().svla_gemm_set_variant(0)
+        Kn.gemm_variant = 0
     return outs
 
 
@@ -451,17 +451,17 @@ def test_gemm_rope_epilogue(cuda, D, Hq, Hkv, L):
     f = (torch.arange(L, device=cuda).float() + 1)[:, None] * inv[None]
     cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
     nrot = (Hq + Hkv) * D
-    # 0: hipBLASLt store + in-place RoPE pass; 5: hand-written kernel with the fused epilogue; 3: 4-wave kernel
-    for v in ((0, 5, 3) if D == 256 else (0, 5)):
+    # 0: product dispatch; 2: 8-phase kernel with the fused epilogue; 3: 4-wave kernel
+    for v in ((0, 2, 3) if D == 256 else (0, 2)):
         try:
-            L_.lib().svla_gemm_set_variant(v)
+            Kn.gemm_variant = v
             plain = torch.empty(B * L, N, dtype=BF, device=cuda)
             Kn.linear_fwd(x, [w], plain)
             rot = torch.empty_like(plain)
             Kn.linear_fwd(x, [w], rot, kind=L_.EPI_ROPE, rope=(cos, sin, L, D, nrot))
             torch.cuda.synchronize()
         finally:
-            L_.lib().svla_gemm_set_variant(0)
+            Kn.gemm_variant = 0
         ref = plain.clone()
         ref[:, :nrot] = _rope_bf16(plain[:, :nrot].view(B, L, Hq + Hkv, D), cos, sin).view(B * L, nrot)
         assert torch.equal(rot, ref), v
@@ -579,7 +579,7 @@ def test_geglu_bwd_kernel_matches_epilogue(cuda):
     g, u = _r(M, I), _r(M, I)
     wd, dout = _r(K, I, scale=0.1), _r(M, K)
     try:
-        L.lib().svla_gemm_set_variant(2)
+        Kn.gemm_variant = 2
         ref = torch.empty(M, 2 * I, dtype=BF, device=cuda)
         Kn.linear_dgrad(dout, [wd], ref[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=ref[:, :I], out2=ref[:, I:])
         new = torch.empty(M, 2 * I, dtype=BF, device=cuda)
@@ -587,7 +587,7 @@ def test_geglu_bwd_kernel_matches_epilogue(cuda):
         Kn.geglu_bwd(new[:, :I], g, u, new[:, :I], new[:, I:])
         torch.cuda.synchronize()
     finally:
-        L.lib().svla_gemm_set_variant(0)
+        Kn.gemm_variant = 0
     assert torch.equal(new, ref)
     dh = (dout.float() @ wd.float()).to(BF).float()
     gf, uf = g.float(), u.float()

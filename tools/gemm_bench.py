@@ -46,7 +46,7 @@ def run(name, m, n, k, lay, reps=10):
     for rnd in range(3):  # interleaved rounds in one process; report the best of 3 per arm
         for tag, v, fn in arms:
             if v is not None:
-                L.lib().svla_gemm_set_variant(v)
+                K.gemm_variant = v
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -57,10 +57,10 @@ def run(name, m, n, k, lay, reps=10):
     r = ref().float()
     errs = []
     for v in variants:
-        L.lib().svla_gemm_set_variant(v)
+        K.gemm_variant = v
         c.fill_(float("nan")); f(); torch.cuda.synchronize()
         errs.append(f"{((c.float() - r).norm() / r.norm()).item():.1e}")
-    L.lib().svla_gemm_set_variant(variants[0])
+    K.gemm_variant = 0
     cols = "  ".join(f"{t} {best[t]:7.3f} ms {2.0 * m * n * k / best[t] / 1e9:7.1f} TF" for t, _, _ in arms)
     print(f"{name:16s} M={m:6d} N={n:6d} K={k:6d} {cols}  relerr {'/'.join(errs)}", flush=True)
 
