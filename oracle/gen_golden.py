@@ -17,6 +17,15 @@ What is pinned (SURVEY.md §8(c) "Golden-vector plan"):
   (padded key columns un-masked in training).
 * layer4b_* — one Gemma2 decoder layer and one SigLIP encoder layer at SpatialVLA-4B
   widths (B=1, L=312 / 256): outputs and input-grads in full, param-grad norms.
+* full4b — the whole SpatialVLA-4B model (SigLIP-So400m + ZoeDepth BEiT-L + Ego3D + Gemma2-2B, V=265347) with
+  counter-hash weights (spatialvla_amd.detinit.hash_init_: bit-identical on CPU and GPU, so 8 GB of weights
+  never travel), one training forward+backward at B=1, L=312: loss, per-row argmax / top-2 margin / lse, the
+  logits of the 13 labelled rows over the action-token range, logits of all rows at 256 fixed columns, Zoe depth,
+  xyz, image features, every trainable gradient's norm and first-row slice.
+* decode_tiny / decode4b — greedy decode (predict_action, modeling_spatialvla.py:484-492) by the reference model
+  itself, restated without a cache (the HybridCache constructor does not run under transformers 5): each step
+  re-forwards prompt + generated tokens with the 4-D mask the cached path sees (prompt bidirectional,
+  :291-296; generated tokens causal, modeling_gemma2.py:387-395), next token = argmax of the last row.
 """
 import json
 import os
@@ -32,21 +41,24 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, HERE)
 
 from spatialvla_amd import presets  # noqa: E402
-from spatialvla_amd.detinit import deterministic_init_, det_tensor  # noqa: E402
+from spatialvla_amd.detinit import deterministic_init_, det_tensor, hash_init_  # noqa: E402
 import ref_shim  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
 SEED = 1234
 
 
-def build_reference_model(cfgdict):
+def build_reference_model(cfgdict, init="normal"):
     msv, csv = ref_shim.install()
     cfg = csv.SpatialVLAConfig(**json.loads(json.dumps(cfgdict)))
     ref_shim.configure_eager(cfg)
     torch.manual_seed(0)
     model = msv.SpatialVLAForConditionalGeneration(cfg)
     model = model.to(torch.bfloat16)
-    deterministic_init_(model, seed=SEED)
+    if init == "normal":
+        deterministic_init_(model, seed=SEED)
+    else:
+        hash_init_(model, seed=SEED)
     model.train()
     if cfg.use_vision_zoe:
         model.vision_zoe_model.eval()
@@ -190,16 +202,121 @@ def gen_layer4b():
     print("layer4b bytes", os.path.getsize(os.path.join(OUT, "layer4b.safetensors")))
 
 
+def decode_mask(prompt_len, L, B):
+    """additive [B,1,L,L]: prompt rows see the prompt (inference prefill, modeling_spatialvla.py:291-296),
+    generated row t sees the prompt and generated tokens <= t (cached decode, modeling_gemma2.py:387-395)."""
+    mn = torch.finfo(torch.bfloat16).min
+    m = torch.full((L, L), mn, dtype=torch.bfloat16)
+    m[:, :prompt_len] = 0.0
+    i = torch.arange(L)
+    gen = (i[:, None] >= prompt_len) & (i[None, :] >= prompt_len) & (i[None, :] <= i[:, None])
+    m = torch.where(gen, torch.zeros((), dtype=torch.bfloat16), m)
+    return m[None, None].expand(B, 1, L, L).contiguous()
+
+
+@torch.no_grad()
+def ref_greedy(model, ids, pv, intr, n_new, depth_cap=None):
+    """Greedy decode through the reference forward (4-D mask passthrough, :288-289), no cache."""
+    B, P = ids.shape
+    cur, toks, margins = ids, [], []
+    for step in range(n_new):
+        Lc = cur.shape[1]
+        out = model(input_ids=cur, pixel_values=pv, intrinsic=intr, attention_mask=decode_mask(P, Lc, B),
+                    use_cache=False, return_dict=True)
+        last = out.logits[:, -1].float()
+        top2 = last.topk(2, -1).values
+        nxt = last.argmax(-1, keepdim=True)
+        toks.append(nxt)
+        margins.append((top2[:, 0] - top2[:, 1])[:, None])
+        cur = torch.cat([cur, nxt], 1)
+        print(f"  decode step {step}: tokens {nxt.view(-1).tolist()} margins {margins[-1].view(-1).tolist()}",
+              flush=True)
+    return torch.cat(toks, 1), torch.cat(margins, 1)
+
+
+def gen_decode_tiny():
+    cfgd = presets.tiny()
+    model, cfg = build_reference_model(cfgd)
+    model.eval()
+    b = presets.synthetic_batch(cfgd, batch=2, seed=7)
+    t = batch_tensors(b)
+    P = int((t["token_type_ids"][0] == 0).sum())
+    ids = t["input_ids"][:, :P]
+    cap = {}
+    orig_bp = model.backproject_patch
+
+    def bp(K, depth, patch_size=14, reso=2):
+        cap.setdefault("depth", depth.detach().clone())
+        return orig_bp(K, depth, patch_size=patch_size, reso=reso)
+    model.backproject_patch = bp
+    toks, margins = ref_greedy(model, ids, t["pixel_values"], t["intrinsic"], 6)
+    save_file({"in.input_ids": ids.contiguous(), "in.pixel_values": t["pixel_values"].contiguous(),
+               "in.intrinsic": t["intrinsic"].contiguous(), "out.depth": cap["depth"].contiguous(),
+               "out.tokens": toks.contiguous(), "out.margins": margins.contiguous()},
+              os.path.join(OUT, "decode_tiny.safetensors"))
+    print("decode_tiny tokens", toks.tolist())
+
+
+def gen_full4b():
+    """The whole 4B model, hash-initialised, B=1 training step + greedy decode of 4 tokens."""
+    import time
+    cfgd = presets.spatialvla_4b()
+    t0 = time.time()
+    model, cfg = build_reference_model(cfgd, init="hash")
+    print(f"4B reference model built + hash-initialised in {time.time() - t0:.0f}s", flush=True)
+    b = presets.synthetic_batch(cfgd, batch=1, seed=4242)
+    t = batch_tensors(b)
+    t0 = time.time()
+    out, cap, grads = run_train(model, t)
+    print(f"4B train fwd+bwd {time.time() - t0:.0f}s loss {out.loss.item():.6f}", flush=True)
+    logits = out.logits.detach()                 # [1, L, V] bf16 (softcapped)
+    lf = logits[0, :-1].float()                  # shifted rows
+    top2 = lf.topk(2, -1).values
+    lse = torch.logsumexp(lf, -1)
+    labels = t["labels"][0, 1:]
+    rows = torch.nonzero(labels != -100).view(-1)
+    a0, na = cfg.action_token_begin_idx, cfg.spatial_token_num
+    g = torch.Generator().manual_seed(5)
+    cols = torch.randperm(logits.shape[-1], generator=g)[:256].sort().values
+    d = {f"in.{k}": v.contiguous() for k, v in t.items()}
+    d.update({"out.loss": out.loss.detach().float().reshape(1),
+              "out.argmax": lf.argmax(-1).contiguous(), "out.top2_margin": (top2[:, 0] - top2[:, 1]).contiguous(),
+              "out.lse": lse.contiguous(), "out.label_rows": rows.contiguous(),
+              "out.action_logits": logits[0, rows, a0:a0 + na].contiguous(),
+              "out.cols": cols.contiguous(), "out.col_logits": logits[0][:, cols].contiguous(),
+              "out.image_features": cap["image_features"].contiguous(),
+              "out.depth": cap["depth"].float().contiguous(), "out.xyz": cap["xyz"].float().contiguous()})
+    for n, gr in grads.items():
+        d[f"gradnorm.{n}"] = gr.float().norm().reshape(1)
+        d[f"gradrow.{n}"] = gr.reshape(gr.shape[0], -1)[0, :64].contiguous()
+    del grads, out
+    model.zero_grad(set_to_none=True)
+    model.eval()
+    P = int((t["token_type_ids"][0] == 0).sum())
+    ids = t["input_ids"][:, :P]
+    t0 = time.time()
+    toks, margins = ref_greedy(model, ids, t["pixel_values"], t["intrinsic"], 4)
+    print(f"4B greedy decode {time.time() - t0:.0f}s tokens {toks.tolist()}", flush=True)
+    d["decode.tokens"] = toks.contiguous()
+    d["decode.margins"] = margins.contiguous()
+    save_file(d, os.path.join(OUT, "full4b.safetensors"))
+    print("full4b bytes", os.path.getsize(os.path.join(OUT, "full4b.safetensors")))
+
+
 if __name__ == "__main__":
     if not ref_shim.reference_available():
         print("reference not present; nothing to do")
         sys.exit(0)
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(os.cpu_count())
-    which = sys.argv[1:] or ["tiny", "ragged", "layer4b"]
+    which = sys.argv[1:] or ["tiny", "ragged", "layer4b", "decode_tiny", "full4b"]
     if "tiny" in which:
         gen_tiny(False)
     if "ragged" in which:
         gen_tiny(True)
     if "layer4b" in which:
         gen_layer4b()
+    if "decode_tiny" in which:
+        gen_decode_tiny()
+    if "full4b" in which:
+        gen_full4b()

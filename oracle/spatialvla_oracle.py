@@ -182,9 +182,12 @@ def gemma_layer(P, tc, i, h, mask, cos, sin, prefix="language_model.model."):
 
 # ---------------------------------------------------------------------------------------- full model
 def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor], zoe_model=None,
-            is_training: Optional[bool] = None, depth: Optional[torch.Tensor] = None, cap: Optional[dict] = None):
+            is_training: Optional[bool] = None, depth: Optional[torch.Tensor] = None, cap: Optional[dict] = None,
+            mask4d: Optional[torch.Tensor] = None):
     """Returns (loss or None, logits bf16 [B, L, V]).  `P` maps reference parameter names -> tensors
-    (vision keys without the 4.47 `vision_model.` infix, as transformers 5 names them)."""
+    (vision keys without the 4.47 `vision_model.` infix, as transformers 5 names them).  mask4d: an explicit
+    additive [B, 1, L, L] mask, passed through as the reference passes a 4-D attention_mask
+    (modeling_spatialvla.py:288-289, modeling_gemma2.py:863-865)."""
     vc, tc = cfg["vision_config"], cfg["text_config"]
     dt = BF16
     ids = batch["input_ids"]
@@ -223,7 +226,8 @@ def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor
         labels = torch.where(ids == 0, -100, labels)
     if am is None:
         am = torch.ones_like(ids)
-    mask = prefix_mask(am, tt if tt is not None else torch.zeros_like(ids), is_training, L, dt)
+    mask = mask4d if mask4d is not None else prefix_mask(am, tt if tt is not None else torch.zeros_like(ids),
+                                                         is_training, L, dt)
     pos = (torch.arange(L) + 1)[None]
     cos, sin = rope_tables(pos, tc["head_dim"], dt, tc.get("rope_theta", 10000.0))
     h = emb * torch.tensor(tc["hidden_size"] ** 0.5, dtype=dt)
@@ -242,18 +246,57 @@ def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor
     return loss, logits
 
 
+def decode_mask(prompt_len: int, L: int, B: int, dtype=BF16):
+    """The attention a greedy decode sees, restated without a cache: prompt rows attend to the whole prompt
+    (inference prefill mask, modeling_spatialvla.py:291-296 with is_training False), generated token t attends to
+    the prompt and every generated token <= t (HybridCache decode steps, modeling_gemma2.py:387-395, 868-873).
+    Prompt rows never see generated keys, so their K/V equal the cached prefill's."""
+    mn = torch.finfo(dtype).min
+    m = torch.full((L, L), mn, dtype=dtype)
+    m[:, :prompt_len] = 0.0
+    i = torch.arange(L)
+    gen = (i[:, None] >= prompt_len) & (i[None, :] >= prompt_len) & (i[None, :] <= i[:, None])
+    m = torch.where(gen, torch.zeros((), dtype=dtype), m)
+    return m[None, None].expand(B, 1, L, L).contiguous()
+
+
+@torch.no_grad()
+def greedy_decode(P, cfg, batch, zoe_model=None, n_new: int = 4, depth=None):
+    """predict_action / generate(do_sample=False) (modeling_spatialvla.py:484-492) restated as full re-forwards:
+    positions 1..L (:367-372, :473-474), image features merged every step (same values the cached path reuses),
+    next token = argmax of the last position's softcapped bf16 logits.  Returns (tokens [B, n], top-1 minus
+    top-2 logit margin [B, n])."""
+    ids = batch["input_ids"]
+    B, Pl = ids.shape
+    toks, margins = [], []
+    cur = ids
+    for _ in range(n_new):
+        Lc = cur.shape[1]
+        b = {"input_ids": cur, "pixel_values": batch["pixel_values"], "intrinsic": batch["intrinsic"]}
+        _, logits = forward(P, cfg, b, zoe_model, is_training=False, depth=depth,
+                            mask4d=decode_mask(Pl, Lc, B))
+        last = logits[:, -1].float()
+        top2 = last.topk(2, -1).values
+        nxt = last.argmax(-1, keepdim=True)
+        toks.append(nxt)
+        margins.append((top2[:, 0] - top2[:, 1])[:, None])
+        cur = torch.cat([cur, nxt], 1)
+    return torch.cat(toks, 1), torch.cat(margins, 1)
+
+
 def params_from_model_state(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     """Rename product state-dict keys (4.47 `vision_tower.vision_model.` infix) to the oracle's names."""
     return {k.replace("vision_tower.vision_model.", "vision_tower."): v for k, v in sd.items()}
 
 
-def build_params(cfg: dict, seed: int, dtype=BF16, requires_grad=True, zoe_model_names=()):
-    """Deterministic parameters by name (spatialvla_amd.detinit rules) for every hot-path tensor."""
-    from spatialvla_amd.detinit import det_tensor
+def build_params(cfg: dict, seed: int, dtype=BF16, requires_grad=True, zoe_model_names=(), init="normal"):
+    """Deterministic parameters by name (spatialvla_amd.detinit rules) for every hot-path tensor; init "normal"
+    (det_tensor, the tiny fixtures) or "hash" (hash_tensor, the 4B fixtures)."""
+    from spatialvla_amd.detinit import det_tensor, hash_tensor
     shapes = param_shapes(cfg)
     P = {}
     for n, shp in shapes.items():
-        t = det_tensor(n, shp, seed).to(dtype)
+        t = det_tensor(n, shp, seed).to(dtype) if init == "normal" else hash_tensor(n, shp, seed, dtype=dtype)
         if requires_grad and n != "language_model.model.embed_tokens.weight":
             t.requires_grad_(True)
         P[n] = t

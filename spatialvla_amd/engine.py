@@ -196,7 +196,7 @@ class TrainEngine:
             model.clear_decode_cache()
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
-        self.warmup_steps = max(1, int(math.ceil(warmup_ratio * total_steps)))
+        self.warmup_steps = int(math.ceil(warmup_ratio * total_steps))
         self.total_steps = total_steps
         self.step_count = 0
         dev = next(model.parameters()).device

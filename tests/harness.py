@@ -1,9 +1,9 @@
 """Shared parity harness: the HIP model (spatialvla_amd) vs the CPU oracle (oracle/spatialvla_oracle.py)
 on the same deterministic weights and the same synthetic OXE-shaped batch.
 
-Tolerances: logits rel-L2 <= 1e-2; per-tensor grad rel-L2 <= 5e-2 (bf16 end-to-end
-through 2 + 2 layers; typical values are ~1e-2); action argmax identical wherever the oracle's top-1/top-2
-margin exceeds 0.05 (bf16 logits quantise at 1/32 near |30|).
+Tolerances: logits rel-L2 <= 1e-2; per-tensor grad rel-L2 <= 3e-2 (bf16 end-to-end; typical
+values are ~1e-2); action argmax identical wherever the oracle's top-1/top-2 margin exceeds 0.05 (bf16 logits
+quantise at 1/32 near |30|), and reported separately on the labelled (action-token) rows.
 """
 import json
 import os
@@ -18,7 +18,7 @@ for p in (REPO, os.path.join(REPO, "oracle")):
 
 SEED = 1234
 LOGITS_TOL = 1e-2
-GRAD_TOL = 5e-2
+GRAD_TOL = 3e-2
 MARGIN = 0.05
 
 
@@ -98,7 +98,7 @@ def run_oracle(P, zoe, cfgd, batch_cpu, depth=None):
     return loss.detach().float(), logits.detach().float(), grads, cap
 
 
-def compare(loss_h, logits_h, grads_h, argmax_h, loss_r, logits_r, grads_r):
+def compare(loss_h, logits_h, grads_h, argmax_h, loss_r, logits_r, grads_r, labels=None):
     B, L, V = logits_r.shape
     res = {"loss_hip": float(loss_h), "loss_ref": float(loss_r), "logits_rel": rel_l2(logits_h, logits_r)}
     rels = {}
@@ -123,7 +123,28 @@ def compare(loss_h, logits_h, grads_h, argmax_h, loss_r, logits_r, grads_r):
     conf = margin > MARGIN
     res["argmax_agree"] = float(agree.float().mean())
     res["argmax_agree_confident"] = float(agree[conf].float().mean()) if conf.any() else 1.0
+    if labels is not None:  # the action rows: positions whose next token is a label (the CE / accuracy rows)
+        act = labels[:, 1:].cpu() != -100
+        res["argmax_agree_action_rows"] = float(agree[act].float().mean()) if act.any() else 1.0
+        res["argmax_agree_action_rows_confident"] = float(agree[act & conf].float().mean()) if (act & conf).any() else 1.0
     return res
+
+
+def greedy_tokens_agree(got: torch.Tensor, ref: torch.Tensor, margins: torch.Tensor, tol: float = MARGIN):
+    """Greedy tokens vs the reference's: per sequence, every step must match until the first step whose
+    reference top-1/top-2 margin is <= tol (a near-tie that fp rounding may legitimately flip, after which the
+    sequences diverge).  Returns (#steps compared, #steps matched)."""
+    got, ref, margins = got.cpu(), ref.cpu(), margins.float().cpu()
+    n_cmp = n_ok = 0
+    for b in range(ref.shape[0]):
+        for s in range(ref.shape[1]):
+            n_cmp += 1
+            if int(got[b, s]) == int(ref[b, s]):
+                n_ok += 1
+                continue
+            assert float(margins[b, s]) <= tol, (b, s, int(got[b, s]), int(ref[b, s]), float(margins[b, s]))
+            break
+    return n_cmp, n_ok
 
 
 def tiny_parity_run(device="cuda:0", batch=2, seed=7, ragged=False):
@@ -139,4 +160,4 @@ def tiny_parity_run(device="cuda:0", batch=2, seed=7, ragged=False):
     model = build_hip_model(cfgd, device)
     bd = {k: v.to(device) for k, v in bc.items()}
     loss_h, logits_h, grads_h, am = run_hip(model, bd, depth=cap["depth"])
-    return compare(loss_h, logits_h, grads_h, am, loss_r, logits_r, grads_r)
+    return compare(loss_h, logits_h, grads_h, am, loss_r, logits_r, grads_r, labels=bc["labels"])

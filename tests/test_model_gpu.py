@@ -24,7 +24,7 @@ def test_tiny_train_vs_reference_golden(cuda):
     batch = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
     loss, logits, grads, am = H.run_hip(model, batch, depth=g["out.depth"])
     gr = {k[5:]: v.float() for k, v in g.items() if k.startswith("grad.")}
-    res = H.compare(loss, logits, grads, am, g["out.loss"][0], g["out.logits"].float(), gr)
+    res = H.compare(loss, logits, grads, am, g["out.loss"][0], g["out.logits"].float(), gr, labels=batch["labels"])
     worst = sorted(res["grad_rel"].items(), key=lambda kv: -kv[1])[:5]
     print(json.dumps({k: v for k, v in res.items() if k != "grad_rel"}, indent=1), worst)
     assert not res["grads_missing"], res["grads_missing"]
@@ -32,6 +32,7 @@ def test_tiny_train_vs_reference_golden(cuda):
     assert res["logits_rel"] < H.LOGITS_TOL
     assert res["grad_rel_max"] < H.GRAD_TOL, worst
     assert res["argmax_agree_confident"] == 1.0
+    assert res["argmax_agree_action_rows_confident"] == 1.0
 
 
 def test_tiny_image_features_and_ego3d(cuda):
@@ -215,3 +216,53 @@ def test_predict_action_decodes(cuda):
     inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
     out = model.predict_action(inputs, max_new_tokens=3, eos_token_id=-1)
     assert out.shape == (2, 3)
+
+
+@pytest.mark.parametrize("cached", [True, False])
+def test_predict_action_tokens_vs_reference_golden(cuda, cached):
+    """Greedy decode (KV cache + HIP graphs, and the uncached re-forward) against the tokens the reference model
+    itself generated (oracle/gen_golden.py gen_decode_tiny), margin-gated (harness.greedy_tokens_agree)."""
+    g = _load("decode_tiny.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    model.eval()
+    depth = g["out.depth"].to(cuda)
+    model.predict_depth = lambda p: depth
+    inputs = {"input_ids": g["in.input_ids"], "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    n = g["out.tokens"].shape[1]
+    fn = model.predict_action if cached else model.predict_action_uncached
+    out = fn(inputs, max_new_tokens=n, eos_token_id=-1)
+    n_cmp, n_ok = H.greedy_tokens_agree(out, g["out.tokens"], g["out.margins"])
+    print(f"decode tokens {out.tolist()} vs ref {g['out.tokens'].tolist()}: {n_ok}/{n_cmp}")
+    assert n_ok >= 2
+
+
+def test_predict_action_rejects_padding(cuda):
+    g = _load("decode_tiny.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    ids = g["in.input_ids"]
+    am = torch.ones_like(ids)
+    am[0, -1] = 0
+    with pytest.raises(ValueError, match="padded"):
+        model.predict_action({"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"],
+                              "attention_mask": am}, max_new_tokens=2)
+
+
+def test_decode_states_bounded_and_invalidated(cuda):
+    """decode states are bucketed by capacity, LRU-bounded, and dropped when the weights are rebound
+    (TrainEngine's flat buffers) -- a stale graph would read freed weights."""
+    from spatialvla_amd.engine import TrainEngine
+    g = _load("decode_tiny.safetensors")
+    model = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0")
+    model.eval()
+    depth = g["out.depth"].to(cuda)
+    model.predict_depth = lambda p: depth
+    base = {"pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    ids = g["in.input_ids"]
+    ref = model.predict_action(dict(base, input_ids=ids), max_new_tokens=3, eos_token_id=-1)
+    for extra in (1, 2, 70, 140):  # 1, 2: same capacity bucket; 70, 140: new buckets
+        model.predict_action(dict(base, input_ids=ids), max_new_tokens=3 + extra, eos_token_id=-1)
+    assert len(model._svla_decode_states) <= model.DECODE_STATES_MAX
+    TrainEngine(model, total_steps=10)   # rebinds every trainable parameter into the flat buffers
+    assert len(model._svla_decode_states) == 0
+    again = model.predict_action(dict(base, input_ids=ids), max_new_tokens=3, eos_token_id=-1)
+    assert torch.equal(again, ref)
