@@ -230,6 +230,9 @@ int svla_embed_merge_bwd(int64_t rows, int64_t H, const int64_t* ids, const int3
 int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* depth, const float* kinv, const float* uv_h,
                       int32_t patch, int32_t reso, int32_t n_freqs, void* feat, int64_t ldf, float* xyz_out,
                       void* stream);
+/* inv(K) of B row-major 3x3 fp32 matrices by the closed-form adjugate / determinant (camera intrinsics;
+ * replaces torch.linalg.inv(K.float()) of backproject_patch, model/modeling_spatialvla.py:221).  No host sync. */
+int svla_inv3x3_f32(int32_t B, const float* K, float* kinv, void* stream);
 /* SigLIP patchify (Conv2d k=s=patch): x [B,3,S,S] bf16 already normalised -> cols [B*(S/p)^2, ldc]
  * with column order (c, ky, kx) as the conv weight flattening; columns >= 3p^2 zeroed. */
 int svla_im2col_patch(int32_t B, int32_t S, int32_t patch, const void* x, void* cols, int64_t ldc,

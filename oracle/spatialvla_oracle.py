@@ -79,8 +79,8 @@ def backproject(K, depth, uv_h, patch_size=14, reso=2):
 
 
 def freq_encode(xyz, n_freqs, dtype):
-    freq = (2 ** torch.linspace(0, n_freqs - 1, n_freqs)).to(dtype)
-    center = torch.tensor([0.0, 0.0, 2.0]).repeat(xyz.shape[-1] // 3).to(dtype)
+    freq = (2 ** torch.linspace(0, n_freqs - 1, n_freqs)).to(dtype).to(xyz.device)
+    center = torch.tensor([0.0, 0.0, 2.0]).repeat(xyz.shape[-1] // 3).to(dtype).to(xyz.device)
     xn = ((xyz - center) / 2.0).to(freq.dtype)
     xf = xn.unsqueeze(-1) * freq
     return torch.cat([xn.unsqueeze(-1), torch.sin(xf), torch.cos(xf)], -1).reshape(*xyz.shape[:2], -1)
@@ -114,7 +114,7 @@ def rms(x, w, eps):
 
 
 def rope_tables(pos, dim, dtype, theta=10000.0):
-    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.int64).float() / dim))
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.int64, device=pos.device).float() / dim))
     # the inv_freq buffer is cast with the model (`model.to(bf16)` / DeepSpeed bf16), so the reference
     # runs RoPE on bf16-quantised frequencies, upcast at modeling_gemma2.py:109 (quirk Q11)
     inv = inv.to(dtype).float()
@@ -131,12 +131,13 @@ def rot_half(x):
 def prefix_mask(attn_mask, tt, is_training, L, dtype):
     """_update_causal_mask (modeling_spatialvla.py:258-306), eager branch."""
     mn = torch.finfo(dtype).min
-    cm = torch.full((L, L), mn, dtype=dtype)
+    dev = attn_mask.device
+    cm = torch.full((L, L), mn, dtype=dtype, device=dev)
     if is_training:
         cm = torch.triu(cm, 1)
     else:
         cm[:, :L] = 0.0
-    cm = cm * (torch.arange(L) > torch.arange(L).reshape(-1, 1))
+    cm = cm * (torch.arange(L, device=dev) > torch.arange(L, device=dev).reshape(-1, 1))
     B = attn_mask.shape[0]
     cm = cm[None, None].expand(B, 1, -1, -1).clone()
     pm = (cm + attn_mask[:, None, None, :].to(dtype)) == 0
@@ -203,7 +204,7 @@ def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor
     if cfg.get("use_vision_zoe", True):
         if depth is None:
             depth = zoe_depth(zoe_model, pv)
-        uv = uv_h_buffer(vc["image_size"], vc["patch_size"], cfg["ego3d_patch_reso"], dt)
+        uv = uv_h_buffer(vc["image_size"], vc["patch_size"], cfg["ego3d_patch_reso"], dt).to(ids.device)
         with torch.no_grad():
             xyz = backproject(batch["intrinsic"].to(dt), depth, uv, vc["patch_size"], cfg["ego3d_patch_reso"])
             enc = freq_encode(xyz, cfg["n_freqs"], dt)
@@ -228,7 +229,7 @@ def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor
         am = torch.ones_like(ids)
     mask = mask4d if mask4d is not None else prefix_mask(am, tt if tt is not None else torch.zeros_like(ids),
                                                          is_training, L, dt)
-    pos = (torch.arange(L) + 1)[None]
+    pos = (torch.arange(L, device=ids.device) + 1)[None]
     cos, sin = rope_tables(pos, tc["head_dim"], dt, tc.get("rope_theta", 10000.0))
     h = emb * torch.tensor(tc["hidden_size"] ** 0.5, dtype=dt)
     for i in range(tc["num_hidden_layers"]):
@@ -274,7 +275,7 @@ def greedy_decode(P, cfg, batch, zoe_model=None, n_new: int = 4, depth=None):
         Lc = cur.shape[1]
         b = {"input_ids": cur, "pixel_values": batch["pixel_values"], "intrinsic": batch["intrinsic"]}
         _, logits = forward(P, cfg, b, zoe_model, is_training=False, depth=depth,
-                            mask4d=decode_mask(Pl, Lc, B))
+                            mask4d=decode_mask(Pl, Lc, B).to(cur.device))
         last = logits[:, -1].float()
         top2 = last.topk(2, -1).values
         nxt = last.argmax(-1, keepdim=True)

@@ -83,6 +83,7 @@ SIGNATURES = {
     "svla_embed_merge_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp]),
     "svla_ego3d_encode": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp,
                                   c_vp]),
+    "svla_inv3x3_f32": (c_i32, [c_i32, c_vp, c_vp, c_vp]),
     "svla_im2col_patch": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp]),
     "svla_affine_bf16": (c_i32, [c_i64, c_vp, c_f32, c_f32, c_vp, c_vp]),
     "svla_relu_fwd": (c_i32, [c_i64, c_vp, c_vp, c_vp]),

