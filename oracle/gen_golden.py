@@ -21,7 +21,8 @@ What is pinned (SURVEY.md §8(c) "Golden-vector plan"):
   counter-hash weights (spatialvla_amd.detinit.hash_init_: bit-identical on CPU and GPU, so 8 GB of weights
   never travel), one training forward+backward at B=1, L=312: loss, per-row argmax / top-2 margin / lse, the
   logits of the 13 labelled rows over the action-token range, logits of all rows at 256 fixed columns, Zoe depth,
-  xyz, image features, every trainable gradient's norm and first-row slice.
+  xyz, image features, every trainable gradient's norm and a linear sketch of it (column sums of a matrix, a
+  1-D gradient in full).
 * decode_tiny / decode4b — greedy decode (predict_action, modeling_spatialvla.py:484-492) by the reference model
   itself, restated without a cache (the HybridCache constructor does not run under transformers 5): each step
   re-forwards prompt + generated tokens with the 4-D mask the cached path sees (prompt bidirectional,
@@ -288,7 +289,9 @@ def gen_full4b():
               "out.depth": cap["depth"].float().contiguous(), "out.xyz": cap["xyz"].float().contiguous()})
     for n, gr in grads.items():
         d[f"gradnorm.{n}"] = gr.float().norm().reshape(1)
-        d[f"gradrow.{n}"] = gr.reshape(gr.shape[0], -1)[0, :64].contiguous()
+        # a linear sketch of the whole gradient: the column sums of a matrix (sum over output rows), a 1-D
+        # gradient in full -- sums of many terms, so it is not dominated by any single noisy element
+        d[f"gradsum.{n}"] = (gr.float().reshape(gr.shape[0], -1).sum(0) if gr.dim() >= 2 else gr.float()).contiguous()
     del grads, out
     model.zero_grad(set_to_none=True)
     model.eval()

@@ -931,6 +931,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #ifndef G4_PRIO
 #define G4_PRIO 0
 #endif
+#ifndef G4_RS
+#define G4_RS 1  // fragment reads: one per G4_RS MFMAs
+#endif
 #ifndef G4_GROUP_M
 #define G4_GROUP_M GROUP_M
 #endif
@@ -940,8 +943,8 @@ constexpr int OPB = BM * BK * 2;  // bytes per operand image per buffer (32 KiB)
 constexpr int STAGE = 2 * OPB;    // A | B
 constexpr int LDS = 2 * STAGE;    // 128 KiB (the 66.5 KiB epilogue image reuses it)
 static_assert(64 * (BN + 4) * 4 <= LDS, "epilogue image must fit");
-static_assert(G4_RB1 >= 15 && G4_DA0 > G4_RB1 && G4_DB0 >= G4_DA0 + 8 * G4_DST && G4_RB2 >= G4_DB0 + 8 * G4_DST - 1 &&
-                  G4_RB2 + 16 < 128,
+static_assert(G4_RB1 >= 15 * G4_RS && G4_DA0 > G4_RB1 && G4_DB0 >= G4_DA0 + 8 * G4_DST &&
+                  G4_RB2 >= G4_DB0 + 8 * G4_DST - 1 && G4_RB2 + 1 + 15 * G4_RS < 128,
               "gemm4 schedule knobs out of order");
 }  // namespace p4
 
@@ -1150,8 +1153,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
         if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii].get(), f0b[jj].get());
         else agpr_mfma<ii * 8 + jj>(f1a[ii].get(), f1b[jj].get());
-        if constexpr (x < 8) frag4_load<LA>(f1a[x], cur, 128 * wr, x, 1, lane);
-        else if constexpr (x < 16) frag4_load<LB>(f1b[x - 8], cur + OPB, 128 * wc, x - 8, 1, lane);
+        if constexpr (x % G4_RS == 0 && x / G4_RS < 8) frag4_load<LA>(f1a[x / G4_RS], cur, 128 * wr, x / G4_RS, 1, lane);
+        else if constexpr (x % G4_RS == 0 && x / G4_RS < 16)
+          frag4_load<LB>(f1b[x / G4_RS - 8], cur + OPB, 128 * wc, x / G4_RS - 8, 1, lane);
         if constexpr (x == G4_RB1) {
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
           __builtin_amdgcn_s_barrier();
@@ -1168,7 +1172,8 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
           }
-          constexpr int r = x - G4_RB2 - 1;
+          constexpr int r0 = x - G4_RB2 - 1;
+          constexpr int r = (r0 >= 0 && r0 % G4_RS == 0) ? r0 / G4_RS : -1;
           if constexpr (r >= 0 && r < 8) frag4_load<LA>(f0a[r], nxt, 128 * wr, r, 0, lane);
           else if constexpr (r >= 8 && r < 16) frag4_load<LB>(f0b[r - 8], nxt + OPB, 128 * wc, r - 8, 0, lane);
         }

@@ -1,0 +1,50 @@
+"""Diagnostic: HIP vs oracle-on-GPU gradients of the whole 4B model (full tensors), per parameter."""
+import os, sys, json
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "oracle")]
+import torch
+import harness as H
+import spatialvla_oracle as O
+from safetensors.torch import load_file
+from spatialvla_amd import SpatialVLAConfig, presets
+from spatialvla_amd.detinit import hash_init_
+from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration
+
+cuda = torch.device("cuda:0")
+gold = load_file(os.path.join(REPO, "tests/golden/full4b.safetensors"))
+cfg = SpatialVLAConfig(**json.loads(json.dumps(presets.spatialvla_4b())))
+cfg.vision_zoe_config._attn_implementation = "eager"
+cfg.vision_zoe_config.backbone_config._attn_implementation = "eager"
+with torch.device(cuda):
+    m = SpatialVLAForConditionalGeneration(cfg)
+m = m.to(torch.bfloat16)
+hash_init_(m, seed=H.SEED)
+m.language_model.model.embed_tokens.weight.requires_grad_(False)
+m.vision_zoe_model.eval()
+for p in m.vision_zoe_model.parameters():
+    p.requires_grad_(False)
+batch = {k[3:]: v.to(cuda) for k, v in gold.items() if k.startswith("in.")}
+loss, logits, grads, _ = H.run_hip(m, batch, depth=gold["out.depth"])
+P = O.params_from_model_state({n: p.detach().clone().requires_grad_(p.requires_grad)
+                               for n, p in m.named_parameters() if not n.startswith("vision_zoe_model.")})
+cap = {}
+oloss, ologits = O.forward(P, H.cfg_dict("spatialvla_4b"), batch, None, depth=gold["out.depth"].to(cuda), cap=cap)
+oloss.backward()
+rows = []
+for n, t in P.items():
+    if t.grad is None or n not in grads:
+        continue
+    r = H.rel_l2(grads[n], t.grad.float())
+    rows.append((r, n, float(t.grad.float().norm())))
+rows.sort(reverse=True)
+for r, n, nrm in rows[:40]:
+    print(f"{r:9.3e}  {n}  |g|={nrm:.3e}")
+print("median", sorted(r for r, _, _ in rows)[len(rows) // 2])
+# per layer summary
+import re, collections
+agg = collections.defaultdict(list)
+for r, n, _ in rows:
+    mm = re.match(r"(vision_tower\.encoder\.layers\.\d+|language_model\.model\.layers\.\d+)", n)
+    agg[mm.group(1) if mm else n].append(r)
+for k in sorted(agg, key=lambda s: (s.split('.')[0], int(s.split('.')[-1]) if s.split('.')[-1].isdigit() else -1)):
+    print(f"{k:45s} max {max(agg[k]):.3e}")

@@ -13,12 +13,8 @@ sel = args[args.index("--") + 1:] if "--" in args else []
 libs = []
 for path in paths:
     cd = L.load(os.path.abspath(path))
-    n = int(cd.svla_gemm_workspace_bytes())
-    ws = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    L.check(cd.svla_gemm_set_workspace(ws.data_ptr(), n), "ws")
-    cd.svla_gemm_set_variant(variant)
-    libs.append((os.path.basename(path).replace("libsvla_", "").replace(".so", ""), cd, ws))
-K._gemm_ws[torch.cuda.current_device()] = libs[0][2]
+    libs.append((os.path.basename(path).replace("libsvla_", "").replace(".so", ""), cd, None))
+K.gemm_variant = variant
 for name, m, n, k, lay in SHAPES:
     if sel and not any(x in name for x in sel):
         continue
@@ -47,5 +43,5 @@ for name, m, n, k, lay in SHAPES:
             best[tag] = min(best.get(tag, 1e9), e0.elapsed_time(e1) / 10)
             if cd is not None and rnd == 0:
                 errs[tag] = ((c.float() - ref).norm() / ref.norm()).item()
-    print(f"{name:14s} " + " ".join(f"{t}:{2e-9 * m * n * k / best[t]:6.0f}" for t, _ in arms)
+    print(f"{name:16s} " + " ".join(f"{t}:{2e-9 * m * n * k / best[t]:6.0f}" for t, _ in arms)
           + "  maxerr %.1e" % max(errs.values()), flush=True)
