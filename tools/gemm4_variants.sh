@@ -9,7 +9,7 @@ done
 wait
 for spec in "$@"; do
   name=${spec%%:*}
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 ../../build/obj/runtime.o ../../build/var/gemm_$name.o ../../build/obj/attention.o \
-    ../../build/obj/norms.o ../../build/obj/misc.o ../../build/obj/zoe.o -o ../../build/var/libsvla_$name.so
+  others=$(ls ../../build/obj/*.o | grep -v '/gemm\.o$')
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 ../../build/var/gemm_$name.o $others -o ../../build/var/libsvla_$name.so
   echo "built build/var/libsvla_$name.so"
 done
