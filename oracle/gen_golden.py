@@ -21,8 +21,8 @@ What is pinned (SURVEY.md §8(c) "Golden-vector plan"):
   counter-hash weights (spatialvla_amd.detinit.hash_init_: bit-identical on CPU and GPU, so 8 GB of weights
   never travel), one training forward+backward at B=1, L=312: loss, per-row argmax / top-2 margin / lse, the
   logits of the 13 labelled rows over the action-token range, logits of all rows at 256 fixed columns, Zoe depth,
-  xyz, image features, every trainable gradient's norm and a linear sketch of it (column sums of a matrix, a
-  1-D gradient in full).
+  xyz, image features, every trainable gradient's norm and a linear sketch of it (a hash-signed +-1 sum of the
+  rows of a matrix, a 1-D gradient in full).
 * decode_tiny / decode4b — greedy decode (predict_action, modeling_spatialvla.py:484-492) by the reference model
   itself, restated without a cache (the HybridCache constructor does not run under transformers 5): each step
   re-forwards prompt + generated tokens with the 4-D mask the cached path sees (prompt bidirectional,
@@ -203,6 +203,15 @@ def gen_layer4b():
     print("layer4b bytes", os.path.getsize(os.path.join(OUT, "layer4b.safetensors")))
 
 
+def sketch(name, g):
+    from spatialvla_amd.detinit import hash_tensor
+    g = g.float()
+    if g.dim() < 2:
+        return g
+    r = hash_tensor(name + "#sketch", (g.shape[0],), 0, device=g.device, dtype=torch.float32).sign()
+    return r @ g.reshape(g.shape[0], -1)
+
+
 def decode_mask(prompt_len, L, B):
     """additive [B,1,L,L]: prompt rows see the prompt (inference prefill, modeling_spatialvla.py:291-296),
     generated row t sees the prompt and generated tokens <= t (cached decode, modeling_gemma2.py:387-395)."""
@@ -289,9 +298,10 @@ def gen_full4b():
               "out.depth": cap["depth"].float().contiguous(), "out.xyz": cap["xyz"].float().contiguous()})
     for n, gr in grads.items():
         d[f"gradnorm.{n}"] = gr.float().norm().reshape(1)
-        # a linear sketch of the whole gradient: the column sums of a matrix (sum over output rows), a 1-D
-        # gradient in full -- sums of many terms, so it is not dominated by any single noisy element
-        d[f"gradsum.{n}"] = (gr.float().reshape(gr.shape[0], -1).sum(0) if gr.dim() >= 2 else gr.float()).contiguous()
+        # a linear sketch of the whole gradient: a +-1 combination of the rows of a matrix (signs from the counter
+        # hash, so the GPU test regenerates them), a 1-D gradient in full.  Plain column sums are a poor sketch:
+        # softmax / norm backward make many gradients' row sums cancel to rounding noise.
+        d[f"gradsum.{n}"] = sketch(n, gr).contiguous()
     del grads, out
     model.zero_grad(set_to_none=True)
     model.eval()

@@ -48,3 +48,29 @@ for r, n, _ in rows:
     agg[mm.group(1) if mm else n].append(r)
 for k in sorted(agg, key=lambda s: (s.split('.')[0], int(s.split('.')[-1]) if s.split('.')[-1].isdigit() else -1)):
     print(f"{k:45s} max {max(agg[k]):.3e}")
+
+# ---- sketches vs the reference golden, HIP and oracle-on-GPU
+def sk(x):
+    x = x.float()
+    return x.reshape(x.shape[0], -1).sum(0) if x.dim() >= 2 else x
+print("\nsketch rel-L2 vs golden (hip, oracle):")
+out = []
+for k, v in gold.items():
+    if not k.startswith("gradsum."):
+        continue
+    n = k[len("gradsum."):]
+    if n.endswith("k_proj.bias") or n not in grads:
+        continue
+    h = H.rel_l2(sk(grads[n]), v.float()); o = H.rel_l2(sk(P[n].grad), v.float())
+    out.append((h / max(o, 1e-3), n, h, o))
+out.sort(reverse=True)
+for r, n, h, o in out[:30]:
+    print(f"{r:7.2f} hip {h:.3e} ora {o:.3e} {n}")
+# bias of the HIP gradient relative to the oracle for a few SigLIP tensors
+for n in ["vision_tower.encoder.layers.26.mlp.fc1.weight", "vision_tower.encoder.layers.26.mlp.fc1.bias",
+          "vision_tower.encoder.layers.26.mlp.fc2.weight", "vision_tower.encoder.layers.17.mlp.fc1.weight",
+          "vision_tower.encoder.layers.2.self_attn.q_proj.weight", "language_model.model.layers.10.mlp.up_proj.weight"]:
+    h, o = grads[n].float(), P[n].grad.float()
+    d = h - o
+    print(f"{n}: rel {H.rel_l2(h, o):.3e} mean(d)/rms(o) {float(d.mean() / o.pow(2).mean().sqrt()):.3e} "
+          f"mean(o)/rms(o) {float(o.mean() / o.pow(2).mean().sqrt()):.3e} colsum rel {H.rel_l2(sk(h), sk(o)):.3e}")
