@@ -934,6 +934,12 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #ifndef G4_RS
 #define G4_RS 1  // fragment reads: one per G4_RS MFMAs
 #endif
+#ifndef G4_STAMPS
+#define G4_STAMPS 0  // diagnostic build: per-wave cycles spent in each wait of the k-loop (tools/gemm_stamps.py)
+#endif
+#if G4_STAMPS
+__device__ unsigned long long g4_stamps[16384][4][4];  // [block][wave][top lgkm, RB1, RB2, whole k-loop]
+#endif
 #ifndef G4_GROUP_M
 #define G4_GROUP_M GROUP_M
 #endif
@@ -1096,6 +1102,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   };
 
   const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
+#if G4_STAMPS
+  unsigned long long st[4] = {0, 0, 0, 0};
+#endif
 
   auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
     agpr_zero();
@@ -1145,7 +1154,13 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       const int64_t k2 = (int64_t)(kt + 2) * BK;
       const char* const rsa = abase + k2 * ksa;
       const char* const rsb = bbase + k2 * ksb;
+#if G4_STAMPS
+      unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if G4_STAMPS
+      st[0] += __builtin_amdgcn_s_memtime() - t0;
+#endif
       __builtin_amdgcn_sched_barrier(0);
       if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
       static_for<0, 128>([&](auto XC) {
@@ -1157,8 +1172,14 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         else if constexpr (x % G4_RS == 0 && x / G4_RS < 16)
           frag4_load<LB>(f1b[x / G4_RS - 8], cur + OPB, 128 * wc, x / G4_RS - 8, 1, lane);
         if constexpr (x == G4_RB1) {
+#if G4_STAMPS
+          unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
           __builtin_amdgcn_s_barrier();
+#if G4_STAMPS
+          st[1] += __builtin_amdgcn_s_memtime() - t1;
+#endif
         }
         if constexpr (decltype(DMA)::value) {
           if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0)
@@ -1168,9 +1189,16 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         }
         if constexpr (decltype(NEXT)::value) {
           if constexpr (x == G4_RB2) {
+#if G4_STAMPS
+            unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
             if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
+#if G4_STAMPS
+            st[2] += __builtin_amdgcn_s_memtime() - t2;
+#endif
           }
           constexpr int r0 = x - G4_RB2 - 1;
           constexpr int r = (r0 >= 0 && r0 % G4_RS == 0) ? r0 / G4_RS : -1;
@@ -1184,6 +1212,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     using T = std::true_type;
     using F = std::false_type;
     int kt = kb;
+#if G4_STAMPS
+    const unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
     for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{});
     if (kt + 1 < ke) {
@@ -1191,6 +1222,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       ++kt;
     }
     ktile(kt, F{}, F{});
+#if G4_STAMPS
+    st[3] += __builtin_amdgcn_s_memtime() - tl;
+#endif
     agpr_fence();  // MFMA results -> epilogue / slab readers
     __syncthreads();
   };
@@ -1307,6 +1341,10 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     }
     epilogue(m0, n0, t);
   }
+#if G4_STAMPS
+  if ((t_in & 63) == 0)
+    for (int i = 0; i < 4; ++i) g4_stamps[blockIdx.x % 16384][w][i] = st[i];
+#endif
 }
 
 #define SVLA_GEMM4_KERNEL(LA_, LB_)                                                                      \
@@ -1732,6 +1770,13 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
 }  // namespace
 
 extern "C" size_t svla_gemm_workspace_bytes(void) { return sk_workspace_bytes(num_cus()); }
+
+#if G4_STAMPS
+extern "C" int svla_diag_g4_stamps(void* host, size_t bytes) {  // diagnostic builds only (not in svla.h)
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g4_stamps), bytes < sizeof(g4_stamps) ? bytes : sizeof(g4_stamps)) ==
+                 hipSuccess ? 0 : 2;
+}
+#endif
 
 namespace {
 int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,

@@ -1,0 +1,28 @@
+"""Per-wave wait cycles of the gemm4 k-loop (diagnostic build -DG4_STAMPS=1): python tools/gemm_stamps.py lib.so M N K"""
+import ctypes, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from spatialvla_amd import kernels as K, _lib as L
+
+lib = L.load(os.path.abspath(sys.argv[1]))
+L._lib = lib
+M, N, Kd = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+a = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
+b = torch.randn(N, Kd, device="cuda").to(torch.bfloat16)
+c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+A, B = K._operand([a], L.LAYOUT_KC), K._operand([b], L.LAYOUT_KC)
+K.gemm_variant = 3
+for _ in range(5):
+    K.gemm(M, N, Kd, A, B, [c], [0], N, K._epi())
+torch.cuda.synchronize()
+buf = np.zeros((16384, 4, 4), dtype=np.uint64)
+fn = lib.svla_diag_g4_stamps
+fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+assert fn(buf.ctypes.data, buf.nbytes) == 0
+tiles = ((M + 255) // 256) * ((N + 255) // 256)
+s = buf[:min(tiles, 16384)].astype(np.float64)
+tot = s[..., 3].mean()
+print(f"{M}x{N}x{Kd}: k-loop mean {tot:.0f} ticks/wave; share waiting at top-lgkm {s[..., 0].mean() / tot:.3f}, "
+      f"RB1 {s[..., 1].mean() / tot:.3f}, RB2 {s[..., 2].mean() / tot:.3f}; per wave (RB1, RB2): "
+      f"{[(round(s[:, w, 1].mean() / tot, 3), round(s[:, w, 2].mean() / tot, 3)) for w in range(4)]}")
