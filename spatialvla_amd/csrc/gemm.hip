@@ -1042,11 +1042,82 @@ __device__ __forceinline__ void frag4_load(Frag<LAYOUT>& f, const char* img, int
 // The 64 accumulator quads of a wave live in fixed AGPRs (quad q = 8 * A-fragment + B-fragment in a[4q:4q+3]) and
 // are touched only by the inline asm below (agpr.h): with compiler-allocated accumulators hipcc renames them between
 // the MFMAs of a k-tile and pays ~250 v_accvgpr moves per k-tile at the loop back edge.
+// Each MFMA statement names exactly the four AGPRs it writes (a[4Q:4Q+3]) as clobbers: with the whole file listed,
+// the hazard recognizer pads every MFMA -> MFMA issue with an s_nop (it sees a write of every AGPR followed by a
+// read of every AGPR), 77 nops per k-tile; with the exact quad it sees independent accumulators, as they are.
 template <int Q>
-__device__ __forceinline__ void agpr_mfma(const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(4 * Q), "i"(4 * Q + 3)
-               : SVLA_AGPR_CLOBBERS);
-}
+__device__ __forceinline__ void agpr_mfma(const bf16x8& a, const bf16x8& b);
+#define SVLA_AGPR_MFMA_Q(Q, A0, A1, A2, A3)                                                                     \
+  template <>                                                                                                   \
+  __device__ __forceinline__ void agpr_mfma<Q>(const bf16x8& a, const bf16x8& b) {                              \
+    asm volatile("v_mfma_f32_16x16x32_bf16 a[" #A0 ":" #A3 "], %0, %1, a[" #A0 ":" #A3 "]" ::"v"(a), "v"(b)     \
+                 : "a" #A0, "a" #A1, "a" #A2, "a" #A3);                                                         \
+  }
+SVLA_AGPR_MFMA_Q(0, 0, 1, 2, 3)
+SVLA_AGPR_MFMA_Q(1, 4, 5, 6, 7)
+SVLA_AGPR_MFMA_Q(2, 8, 9, 10, 11)
+SVLA_AGPR_MFMA_Q(3, 12, 13, 14, 15)
+SVLA_AGPR_MFMA_Q(4, 16, 17, 18, 19)
+SVLA_AGPR_MFMA_Q(5, 20, 21, 22, 23)
+SVLA_AGPR_MFMA_Q(6, 24, 25, 26, 27)
+SVLA_AGPR_MFMA_Q(7, 28, 29, 30, 31)
+SVLA_AGPR_MFMA_Q(8, 32, 33, 34, 35)
+SVLA_AGPR_MFMA_Q(9, 36, 37, 38, 39)
+SVLA_AGPR_MFMA_Q(10, 40, 41, 42, 43)
+SVLA_AGPR_MFMA_Q(11, 44, 45, 46, 47)
+SVLA_AGPR_MFMA_Q(12, 48, 49, 50, 51)
+SVLA_AGPR_MFMA_Q(13, 52, 53, 54, 55)
+SVLA_AGPR_MFMA_Q(14, 56, 57, 58, 59)
+SVLA_AGPR_MFMA_Q(15, 60, 61, 62, 63)
+SVLA_AGPR_MFMA_Q(16, 64, 65, 66, 67)
+SVLA_AGPR_MFMA_Q(17, 68, 69, 70, 71)
+SVLA_AGPR_MFMA_Q(18, 72, 73, 74, 75)
+SVLA_AGPR_MFMA_Q(19, 76, 77, 78, 79)
+SVLA_AGPR_MFMA_Q(20, 80, 81, 82, 83)
+SVLA_AGPR_MFMA_Q(21, 84, 85, 86, 87)
+SVLA_AGPR_MFMA_Q(22, 88, 89, 90, 91)
+SVLA_AGPR_MFMA_Q(23, 92, 93, 94, 95)
+SVLA_AGPR_MFMA_Q(24, 96, 97, 98, 99)
+SVLA_AGPR_MFMA_Q(25, 100, 101, 102, 103)
+SVLA_AGPR_MFMA_Q(26, 104, 105, 106, 107)
+SVLA_AGPR_MFMA_Q(27, 108, 109, 110, 111)
+SVLA_AGPR_MFMA_Q(28, 112, 113, 114, 115)
+SVLA_AGPR_MFMA_Q(29, 116, 117, 118, 119)
+SVLA_AGPR_MFMA_Q(30, 120, 121, 122, 123)
+SVLA_AGPR_MFMA_Q(31, 124, 125, 126, 127)
+SVLA_AGPR_MFMA_Q(32, 128, 129, 130, 131)
+SVLA_AGPR_MFMA_Q(33, 132, 133, 134, 135)
+SVLA_AGPR_MFMA_Q(34, 136, 137, 138, 139)
+SVLA_AGPR_MFMA_Q(35, 140, 141, 142, 143)
+SVLA_AGPR_MFMA_Q(36, 144, 145, 146, 147)
+SVLA_AGPR_MFMA_Q(37, 148, 149, 150, 151)
+SVLA_AGPR_MFMA_Q(38, 152, 153, 154, 155)
+SVLA_AGPR_MFMA_Q(39, 156, 157, 158, 159)
+SVLA_AGPR_MFMA_Q(40, 160, 161, 162, 163)
+SVLA_AGPR_MFMA_Q(41, 164, 165, 166, 167)
+SVLA_AGPR_MFMA_Q(42, 168, 169, 170, 171)
+SVLA_AGPR_MFMA_Q(43, 172, 173, 174, 175)
+SVLA_AGPR_MFMA_Q(44, 176, 177, 178, 179)
+SVLA_AGPR_MFMA_Q(45, 180, 181, 182, 183)
+SVLA_AGPR_MFMA_Q(46, 184, 185, 186, 187)
+SVLA_AGPR_MFMA_Q(47, 188, 189, 190, 191)
+SVLA_AGPR_MFMA_Q(48, 192, 193, 194, 195)
+SVLA_AGPR_MFMA_Q(49, 196, 197, 198, 199)
+SVLA_AGPR_MFMA_Q(50, 200, 201, 202, 203)
+SVLA_AGPR_MFMA_Q(51, 204, 205, 206, 207)
+SVLA_AGPR_MFMA_Q(52, 208, 209, 210, 211)
+SVLA_AGPR_MFMA_Q(53, 212, 213, 214, 215)
+SVLA_AGPR_MFMA_Q(54, 216, 217, 218, 219)
+SVLA_AGPR_MFMA_Q(55, 220, 221, 222, 223)
+SVLA_AGPR_MFMA_Q(56, 224, 225, 226, 227)
+SVLA_AGPR_MFMA_Q(57, 228, 229, 230, 231)
+SVLA_AGPR_MFMA_Q(58, 232, 233, 234, 235)
+SVLA_AGPR_MFMA_Q(59, 236, 237, 238, 239)
+SVLA_AGPR_MFMA_Q(60, 240, 241, 242, 243)
+SVLA_AGPR_MFMA_Q(61, 244, 245, 246, 247)
+SVLA_AGPR_MFMA_Q(62, 248, 249, 250, 251)
+SVLA_AGPR_MFMA_Q(63, 252, 253, 254, 255)
+#undef SVLA_AGPR_MFMA_Q
 __device__ __forceinline__ void agpr_zero() { asm volatile(SVLA_AGPR_ZERO_ASM ::: SVLA_AGPR_CLOBBERS); }
 // MFMA results -> v_accvgpr_read: 12 wait states (8-pass XDL)
 __device__ __forceinline__ void agpr_fence() { asm volatile("s_nop 7\n\ts_nop 4" ::: SVLA_AGPR_CLOBBERS); }
@@ -1119,6 +1190,16 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     // host too, where the address-space cast would be a substitution failure and the kernel stub would vanish)
     auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w); };
     auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
+    // voffsets of every piece for a k-tile that lies wholly inside both reduction extents (all but the last when
+    // K % 64 != 0): the per-piece range selects (v_cmp / s_and / v_cndmask per piece) leave the main loop
+    uint32_t vfa[8], vfb[8];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      vfa[n] = op4_voff(sa, n, (int64_t)1 << 40);
+      vfb[n] = op4_voff(sb, n, (int64_t)1 << 40);
+    }
+    auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w); };
+    auto pieceB_full = [&](const char* kb_, int n, char* img) { op4_piece(kb_, vfb[n], n * sb.rs, n, img, w); };
     auto issue_all = [&](int kt, char* stage) {
       const int64_t k0 = (int64_t)kt * BK;
       const char* const ka = abase + k0 * ksa;
@@ -1148,7 +1229,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     // RC fragments come from asm transpose reads (hipcc would drain every LDS-DMA before a builtin one), which
     // the waitcnt pass cannot see: the fragments of a set are combined into MFMA operands only after an
     // explicit lgkmcnt(0) (set 0: at the top of the k-tile, set 1: at RB1).
-    auto ktile = [&](int kt, auto DMA, auto NEXT) {
+    auto ktile = [&](int kt, auto DMA, auto NEXT, auto FULLK) {
       char* const cur = smem + ((kt - kb) & 1) * STAGE;
       char* const nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
       const int64_t k2 = (int64_t)(kt + 2) * BK;
@@ -1182,10 +1263,14 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #endif
         }
         if constexpr (decltype(DMA)::value) {
-          if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0)
-            pieceA(rsa, kvA - k2, (x - G4_DA0) / G4_DST, cur);
-          if constexpr (x >= G4_DB0 && x < G4_DB0 + 8 * G4_DST && (x - G4_DB0) % G4_DST == 0)
-            pieceB(rsb, kvB - k2, (x - G4_DB0) / G4_DST, cur + OPB);
+          if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0) {
+            if constexpr (decltype(FULLK)::value) pieceA_full(rsa, (x - G4_DA0) / G4_DST, cur);
+            else pieceA(rsa, kvA - k2, (x - G4_DA0) / G4_DST, cur);
+          }
+          if constexpr (x >= G4_DB0 && x < G4_DB0 + 8 * G4_DST && (x - G4_DB0) % G4_DST == 0) {
+            if constexpr (decltype(FULLK)::value) pieceB_full(rsb, (x - G4_DB0) / G4_DST, cur + OPB);
+            else pieceB(rsb, kvB - k2, (x - G4_DB0) / G4_DST, cur + OPB);
+          }
         }
         if constexpr (decltype(NEXT)::value) {
           if constexpr (x == G4_RB2) {
@@ -1215,13 +1300,16 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #if G4_STAMPS
     const unsigned long long tl = __builtin_amdgcn_s_memtime();
 #endif
+    const int kfull = (int)(min(kvA, kvB) / BK);  // k-tiles [0, kfull) lie wholly inside both extents
 #pragma unroll 1
-    for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{});
+    for (; kt + 2 < ke && kt + 3 <= kfull; ++kt) ktile(kt, T{}, T{}, T{});
+#pragma unroll 1
+    for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{}, F{});
     if (kt + 1 < ke) {
-      ktile(kt, F{}, T{});
+      ktile(kt, F{}, T{}, F{});
       ++kt;
     }
-    ktile(kt, F{}, F{});
+    ktile(kt, F{}, F{}, F{});
 #if G4_STAMPS
     st[3] += __builtin_amdgcn_s_memtime() - tl;
 #endif
