@@ -1016,9 +1016,12 @@ __device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_RC>& st, int 
 }
 
 // piece n of the wave for the k-tile whose half-tile base address is kbase
+#ifndef G4_AUX
+#define G4_AUX 0  // cache-policy bits of the operand LDS-DMA (1 sc0, 2 nt, 16 sc1)
+#endif
 __device__ __forceinline__ void op4_piece(const char* kbase, uint32_t voff, uint32_t soff, int n, char* img, int w) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(kbase), (LDS_AS void*)(img + (8 * w + n) * 1024), 16, voff, soff,
-                                           0, 0);
+                                           0, G4_AUX);
 }
 
 // base address of the wave's 128-outer half of the operand tile at k = 0 (GEGLU: half 0 = gate, 1 = up tensor)
