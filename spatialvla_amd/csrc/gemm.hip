@@ -1016,6 +1016,9 @@ __device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_RC>& st, int 
 }
 
 // piece n of the wave for the k-tile whose half-tile base address is kbase
+#ifndef G4_ABL
+#define G4_ABL 0  // timing ablations (wrong results): 1 no k-loop LDS-DMA, 2 no k-loop fragment reads, 4 no k-loop barriers
+#endif
 #ifndef G4_AUX
 #define G4_AUX 0  // cache-policy bits of the operand LDS-DMA (1 sc0, 2 nt, 16 sc1)
 #endif
@@ -1252,7 +1255,8 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
         if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii].get(), f0b[jj].get());
         else agpr_mfma<ii * 8 + jj>(f1a[ii].get(), f1b[jj].get());
-        if constexpr (x % G4_RS == 0 && x / G4_RS < 8) frag4_load<LA>(f1a[x / G4_RS], cur, 128 * wr, x / G4_RS, 1, lane);
+        if constexpr (G4_ABL & 2) {
+        } else if constexpr (x % G4_RS == 0 && x / G4_RS < 8) frag4_load<LA>(f1a[x / G4_RS], cur, 128 * wr, x / G4_RS, 1, lane);
         else if constexpr (x % G4_RS == 0 && x / G4_RS < 16)
           frag4_load<LB>(f1b[x / G4_RS - 8], cur + OPB, 128 * wc, x / G4_RS - 8, 1, lane);
         if constexpr (x == G4_RB1) {
@@ -1260,12 +1264,12 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
-          __builtin_amdgcn_s_barrier();
+          if constexpr (!(G4_ABL & 4)) __builtin_amdgcn_s_barrier();
 #if G4_STAMPS
           st[1] += __builtin_amdgcn_s_memtime() - t1;
 #endif
         }
-        if constexpr (decltype(DMA)::value) {
+        if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) {
           if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0) {
             if constexpr (decltype(FULLK)::value) pieceA_full(rsa, (x - G4_DA0) / G4_DST, cur);
             else pieceA(rsa, kvA - k2, (x - G4_DA0) / G4_DST, cur);
@@ -1281,15 +1285,15 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
             unsigned long long t2 = __builtin_amdgcn_s_memtime();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
-            if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            if constexpr (!(G4_ABL & 4)) __builtin_amdgcn_s_barrier();
 #if G4_STAMPS
             st[2] += __builtin_amdgcn_s_memtime() - t2;
 #endif
           }
           constexpr int r0 = x - G4_RB2 - 1;
-          constexpr int r = (r0 >= 0 && r0 % G4_RS == 0) ? r0 / G4_RS : -1;
+          constexpr int r = (r0 >= 0 && r0 % G4_RS == 0 && !(G4_ABL & 2)) ? r0 / G4_RS : -1;
           if constexpr (r >= 0 && r < 8) frag4_load<LA>(f0a[r], nxt, 128 * wr, r, 0, lane);
           else if constexpr (r >= 8 && r < 16) frag4_load<LB>(f0b[r - 8], nxt + OPB, 128 * wc, r - 8, 0, lane);
         }
