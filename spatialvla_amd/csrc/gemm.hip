@@ -938,7 +938,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #define G4_STAMPS 0  // diagnostic build: per-wave cycles spent in each wait of the k-loop (tools/gemm_stamps.py)
 #endif
 #if G4_STAMPS
-__device__ unsigned long long g4_stamps[16384][4][4];  // [block][wave][top lgkm, RB1, RB2, whole k-loop]
+__device__ unsigned long long g4_stamps[16384][4][8];  // [block][wave][top lgkm, RB1, RB2, k-loop, prologue, epilogue, tiles, total]
 #endif
 #ifndef G4_GROUP_M
 #define G4_GROUP_M GROUP_M
@@ -1180,10 +1180,14 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 
   const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
 #if G4_STAMPS
-  unsigned long long st[4] = {0, 0, 0, 0};
+  unsigned long long stmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
 #endif
 
   auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
+#if G4_STAMPS
+    const unsigned long long tm0 = __builtin_amdgcn_s_memtime();
+#endif
     agpr_zero();
     Op4<LA> sa;
     Op4<LB> sb;
@@ -1246,7 +1250,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #endif
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #if G4_STAMPS
-      st[0] += __builtin_amdgcn_s_memtime() - t0;
+      stmp[0] += __builtin_amdgcn_s_memtime() - t0;
 #endif
       __builtin_amdgcn_sched_barrier(0);
       if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
@@ -1266,7 +1270,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to the waitcnt pass
           if constexpr (!(G4_ABL & 4)) __builtin_amdgcn_s_barrier();
 #if G4_STAMPS
-          st[1] += __builtin_amdgcn_s_memtime() - t1;
+          stmp[1] += __builtin_amdgcn_s_memtime() - t1;
 #endif
         }
         if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) {
@@ -1289,7 +1293,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if constexpr (!(G4_ABL & 4)) __builtin_amdgcn_s_barrier();
 #if G4_STAMPS
-            st[2] += __builtin_amdgcn_s_memtime() - t2;
+            stmp[2] += __builtin_amdgcn_s_memtime() - t2;
 #endif
           }
           constexpr int r0 = x - G4_RB2 - 1;
@@ -1318,7 +1322,8 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     }
     ktile(kt, F{}, F{}, F{});
 #if G4_STAMPS
-    st[3] += __builtin_amdgcn_s_memtime() - tl;
+    stmp[3] += __builtin_amdgcn_s_memtime() - tl;
+    stmp[4] += tl - tm0;
 #endif
     agpr_fence();  // MFMA results -> epilogue / slab readers
     __syncthreads();
@@ -1434,11 +1439,19 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         });
       }
     }
+#if G4_STAMPS
+    const unsigned long long te0 = __builtin_amdgcn_s_memtime();
+#endif
     epilogue(m0, n0, t);
+#if G4_STAMPS
+    stmp[5] += __builtin_amdgcn_s_memtime() - te0;
+    stmp[6] += 1;
+#endif
   }
 #if G4_STAMPS
+  stmp[7] = __builtin_amdgcn_s_memtime() - tk0;
   if ((t_in & 63) == 0)
-    for (int i = 0; i < 4; ++i) g4_stamps[blockIdx.x % 16384][w][i] = st[i];
+    for (int i = 0; i < 8; ++i) g4_stamps[blockIdx.x % 16384][w][i] = stmp[i];
 #endif
 }
 
