@@ -252,6 +252,15 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
 
 // ---------------- epilogue: 64-row passes through an fp32 LDS image [64][BN+4]; write_pass(pass, Ei) stores
 // the accumulators of rows [64*pass, 64*pass+64) into the image
+// Workgroup barrier for the epilogue's LDS image only: waits for this wave's LDS accesses (lgkmcnt), not for its
+// global stores -- __syncthreads() would drain vmcnt(0) as well, exposing every pass's output-store latency (the
+// 4-wave kernel spent ~40k cycles per 256x256 tile in its epilogue, ~30 % of a K = 2304 tile; stamps, r2).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int BM, int BN, int NTH, typename WritePass>
 __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, int64_t n0, const CDesc& Cd,
                                               const svla_epilogue& E, char* smem, int t, WritePass write_pass) {
@@ -270,7 +279,7 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
 #pragma unroll 1
   for (int pass = 0; pass < BM / 64; ++pass) {
     write_pass(pass, Ei);
-    __syncthreads();
+    lds_barrier();
     if (kind == SVLA_EPI_GEGLU) {
       // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
       constexpr int HC = CPR / 2;
@@ -369,7 +378,7 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
         epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
