@@ -27,6 +27,9 @@
 
 namespace {
 
+#ifndef G4_STAMPS
+#define G4_STAMPS 0
+#endif
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 constexpr uint32_t OOB = 0x80000000u;  // voffset beyond num_records -> returns zeros
@@ -263,7 +266,8 @@ __device__ __forceinline__ void lds_barrier() {
 
 template <int BM, int BN, int NTH, typename WritePass>
 __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, int64_t n0, const CDesc& Cd,
-                                              const svla_epilogue& E, char* smem, int t, WritePass write_pass) {
+                                              const svla_epilogue& E, char* smem, int t, WritePass write_pass,
+                                              unsigned long long* ep_stamps = nullptr) {
   constexpr int EPI_LD = BN + 4;
   float* Ei = reinterpret_cast<float*>(smem);
   int cs = 0;
@@ -278,8 +282,15 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
   const int cc = t % CPR;
 #pragma unroll 1
   for (int pass = 0; pass < BM / 64; ++pass) {
+#if G4_STAMPS
+    const unsigned long long e0 = __builtin_amdgcn_s_memtime();
+#endif
     write_pass(pass, Ei);
     lds_barrier();
+#if G4_STAMPS
+    const unsigned long long e1 = __builtin_amdgcn_s_memtime();
+    if (ep_stamps) ep_stamps[0] += e1 - e0;
+#endif
     if (kind == SVLA_EPI_GEGLU) {
       // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
       constexpr int HC = CPR / 2;
@@ -378,7 +389,17 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
         epi_chunk(E, kind, cbase + (m - cm0) * Cd.ld + n, m, n, nv, v);
       }
     }
+#if G4_STAMPS
+    const unsigned long long e2 = __builtin_amdgcn_s_memtime();
+#endif
     lds_barrier();
+#if G4_STAMPS
+    if (ep_stamps) {
+      const unsigned long long e3 = __builtin_amdgcn_s_memtime();
+      ep_stamps[1] += e2 - e1;
+      ep_stamps[2] += e3 - e2;
+    }
+#endif
   }
 }
 
@@ -947,7 +968,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #define G4_STAMPS 0  // diagnostic build: per-wave cycles spent in each wait of the k-loop (tools/gemm_stamps.py)
 #endif
 #if G4_STAMPS
-__device__ unsigned long long g4_stamps[16384][4][8];  // [block][wave][top lgkm, RB1, RB2, k-loop, prologue, epilogue, tiles, total]
+__device__ unsigned long long g4_stamps[16384][4][11];  // [block][wave][top lgkm, RB1, RB2, k-loop, prologue, epilogue, tiles, total]
 #endif
 #ifndef G4_GROUP_M
 #define G4_GROUP_M GROUP_M
@@ -1189,7 +1210,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 
   const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
 #if G4_STAMPS
-  unsigned long long stmp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stmp[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -1356,7 +1377,11 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         if (pass & 1) rows(std::integral_constant<int, 1>{});
         else rows(std::integral_constant<int, 0>{});
       }
+#if G4_STAMPS
+    }, stmp + 8);
+#else
     });
+#endif
   };
 
   const int64_t I = sk.sk_iters, G = sk.grid;
@@ -1460,7 +1485,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #if G4_STAMPS
   stmp[7] = __builtin_amdgcn_s_memtime() - tk0;
   if ((t_in & 63) == 0)
-    for (int i = 0; i < 8; ++i) g4_stamps[blockIdx.x % 16384][w][i] = stmp[i];
+    for (int i = 0; i < 11; ++i) g4_stamps[blockIdx.x % 16384][w][i] = stmp[i];
 #endif
 }
 

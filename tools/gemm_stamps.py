@@ -16,7 +16,7 @@ K.gemm_variant = 3
 for _ in range(5):
     K.gemm(M, N, Kd, A, B, [c], [0], N, K._epi())
 torch.cuda.synchronize()
-buf = np.zeros((16384, 4, 8), dtype=np.uint64)
+buf = np.zeros((16384, 4, 11), dtype=np.uint64)
 fn = lib.svla_diag_g4_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert fn(buf.ctypes.data, buf.nbytes) == 0
@@ -25,7 +25,11 @@ s = buf[:min(tiles, 16384)].astype(np.float64)
 s = s[s[:, 0, 6] > 0]
 nt = s[..., 6].sum(0)[0]
 print(f"blocks {len(s)}, tiles {nt:.0f}: per tile (ticks) prologue {s[..., 4].sum() / 4 / nt:.0f}, k-loop "
-      f"{s[..., 3].sum() / 4 / nt:.0f}, epilogue {s[..., 5].sum() / 4 / nt:.0f}; per block total {s[..., 7].mean():.0f}")
+      f"{s[..., 3].sum() / 4 / nt:.0f}, epilogue {s[..., 5].sum() / 4 / nt:.0f} (write+barrier "
+      f"{s[..., 8].sum() / 4 / nt:.0f}, read+epi+store {s[..., 9].sum() / 4 / nt:.0f}, end barrier "
+      f"{s[..., 10].sum() / 4 / nt:.0f}); per block total {s[..., 7].mean():.0f}")
+for w in range(4):
+    print(f"  wave {w}: write {s[:, w, 8].sum() / nt:.0f} read/store {s[:, w, 9].sum() / nt:.0f} endbar {s[:, w, 10].sum() / nt:.0f}")
 tot = s[..., 3].mean()
 print(f"{M}x{N}x{Kd}: k-loop mean {tot:.0f} ticks/wave; share waiting at top-lgkm {s[..., 0].mean() / tot:.3f}, "
       f"RB1 {s[..., 1].mean() / tot:.3f}, RB2 {s[..., 2].mean() / tot:.3f}; per wave (RB1, RB2): "
