@@ -253,6 +253,139 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
   }
 }
 
+// One 64-row pass of a row-local epilogue (STORE, BIAS, BIAS_GELU, BIAS_RESID, GELU_BWD, GEGLU_BWD, GEGLU) with the
+// kind fixed at compile time: every LDS read of the thread's chunks is issued before the first store, so the pass
+// costs one LDS round trip instead of one per chunk (the runtime-switched per-chunk loop took ~8k cycles per
+// 64-row pass of a 256-wide tile at 256 threads).
+template <int KIND, int BN, int NTH>
+__device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_t N, int64_t m0p, int64_t n0,
+                                              bf16_t* cbase, int64_t cm0, int64_t ldc, const svla_epilogue& E,
+                                              int t) {
+  constexpr int EPI_LD = BN + 4;
+  if constexpr (KIND == SVLA_EPI_GEGLU) {
+    constexpr int HC = BN / 16;                 // 8-column chunks per half row (gate | up)
+    constexpr int ITT = 64 * HC / NTH;          // chunks per thread
+    constexpr int IT = ITT < 2 ? ITT : 2;       // chunks in flight (register budget beside live accumulators)
+    const int64_t I = N >> 1;
+#pragma unroll 1
+    for (int ib = 0; ib < ITT; ib += IT) {
+    float g[IT][8], u[IT][8];
+#pragma unroll
+    for (int it0 = 0; it0 < IT; ++it0) {
+      const int it = ib + it0;
+      const int idx = t + it * NTH, row = idx / HC, c2 = idx % HC;
+      const float* pg = Ei + row * EPI_LD + 8 * c2;
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(pg), a1 = *reinterpret_cast<const f32x4*>(pg + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(pg + BN / 2), b1 = *reinterpret_cast<const f32x4*>(pg + BN / 2 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { g[it0][j] = a0[j]; g[it0][4 + j] = a1[j]; u[it0][j] = b0[j]; u[it0][4 + j] = b1[j]; }
+    }
+#pragma unroll
+    for (int it0 = 0; it0 < IT; ++it0) {
+      const int idx = t + (ib + it0) * NTH, row = idx / HC, c2 = idx % HC;
+      const int64_t m = m0p + row, n = (n0 >> 1) + 8 * c2;
+      if (m < M && n < I) {
+        float h[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          g[it0][j] = round_bf(g[it0][j]);
+          u[it0][j] = round_bf(u[it0][j]);
+          h[j] = round_bf(gelu_tanh(g[it0][j])) * u[it0][j];
+        }
+        store8(cbase + (m - cm0) * ldc + n, h, I - n);
+        store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g[it0], I - n);
+        store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u[it0], I - n);
+      }
+    }
+    }
+  } else {
+    constexpr int CPR = BN / 8;
+    constexpr int RPP = NTH / CPR;
+    constexpr int ITT = 64 / RPP;
+    constexpr int IT = ITT < 4 ? ITT : 4;  // chunks in flight (register budget beside live accumulators)
+    const int cc = t % CPR;
+    const int64_t n = n0 + 8 * cc;
+    const int64_t nv = N - n;
+    float b[8];
+    if constexpr (KIND == SVLA_EPI_BIAS || KIND == SVLA_EPI_BIAS_GELU || KIND == SVLA_EPI_BIAS_RESID) {
+      if (E.bias && nv > 0) load8f((const bf16_t*)E.bias + n, b, nv);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+    if (nv <= 0) return;
+#pragma unroll 1
+    for (int ib = 0; ib < ITT; ib += IT) {
+    float v[IT][8];
+#pragma unroll
+    for (int it0 = 0; it0 < IT; ++it0) {
+      const float* pe = Ei + (t / CPR + (ib + it0) * RPP) * EPI_LD + 8 * cc;
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(pe), x1 = *reinterpret_cast<const f32x4*>(pe + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[it0][j] = x0[j]; v[it0][4 + j] = x1[j]; }
+    }
+#pragma unroll
+    for (int it0 = 0; it0 < IT; ++it0) {
+      const int64_t m = m0p + t / CPR + (ib + it0) * RPP;
+      if (m >= M) continue;
+      bf16_t* cp = cbase + (m - cm0) * ldc + n;
+      float* x = v[it0];
+      if constexpr (KIND == SVLA_EPI_STORE) {
+        if (E.accumulate) {
+          float o[8];
+          load8f(cp, o, nv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = E.alpha * x[j] + o[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] *= E.alpha;
+        }
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_BIAS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = round_bf(x[j] + b[j]) * E.alpha;
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_BIAS_GELU) {
+        float pre[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pre[j] = round_bf(x[j] + b[j]);
+          x[j] = gelu_tanh(pre[j]);
+        }
+        store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_BIAS_RESID) {
+        float r[8];
+        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = round_bf(x[j] + b[j]) + r[j];
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_GELU_BWD) {
+        float pre[8];
+        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, pre, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = round_bf(x[j]) * gelu_tanh_grad(pre[j]);
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_GEGLU_BWD) {
+        float g[8], u[8], dg[8], du[8];
+        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, g, nv);
+        load8f((const bf16_t*)E.in1 + m * E.ld_in1 + n, u, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float dh = round_bf(x[j]);
+          const float act = round_bf(gelu_tanh(g[j]));
+          const float dact = round_bf(dh * u[j]);
+          du[j] = dh * act;
+          dg[j] = dact * gelu_tanh_grad(g[j]);
+        }
+        store8((bf16_t*)E.out1 + m * E.ld_out1 + n, dg, nv);
+        store8((bf16_t*)E.out2 + m * E.ld_out2 + n, du, nv);
+      }
+    }
+    }
+  }
+}
+
 // ---------------- epilogue: 64-row passes through an fp32 LDS image [64][BN+4]; write_pass(pass, Ei) stores
 // the accumulators of rows [64*pass, 64*pass+64) into the image
 // Workgroup barrier for the epilogue's LDS image only: waits for this wave's LDS accesses (lgkmcnt), not for its
@@ -264,7 +397,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int NTH, typename WritePass>
+template <int BM, int BN, int NTH, typename WritePass, bool FAST = false>
 __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, int64_t n0, const CDesc& Cd,
                                               const svla_epilogue& E, char* smem, int t, WritePass write_pass,
                                               unsigned long long* ep_stamps = nullptr) {
@@ -291,7 +424,28 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
     const unsigned long long e1 = __builtin_amdgcn_s_memtime();
     if (ep_stamps) ep_stamps[0] += e1 - e0;
 #endif
-    if (kind == SVLA_EPI_GEGLU) {
+    const int64_t m0p = m0 + 64 * pass;
+    bool fast = FAST;
+    if (FAST) switch (kind) {
+      case SVLA_EPI_STORE: epi_pass_fast<SVLA_EPI_STORE, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_BIAS: epi_pass_fast<SVLA_EPI_BIAS, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_BIAS_GELU:
+        epi_pass_fast<SVLA_EPI_BIAS_GELU, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
+      case SVLA_EPI_BIAS_RESID:
+        epi_pass_fast<SVLA_EPI_BIAS_RESID, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
+      case SVLA_EPI_GELU_BWD:
+        epi_pass_fast<SVLA_EPI_GELU_BWD, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
+      case SVLA_EPI_GEGLU_BWD:
+        epi_pass_fast<SVLA_EPI_GEGLU_BWD, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
+      case SVLA_EPI_GEGLU: epi_pass_fast<SVLA_EPI_GEGLU, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      default: fast = false;
+    }
+    if (fast) {
+    } else if (kind == SVLA_EPI_GEGLU) {
       // columns [0, BN/2) gate, [BN/2, BN) up of output columns n0/2 ..
       constexpr int HC = CPR / 2;
       const int64_t I = N >> 1;
@@ -1361,7 +1515,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 
   auto epilogue = [&](int64_t m0, int64_t n0, const int t) {
     const int lane = t & 63;
-    tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+    auto wp = [&](int pass, float* Ei) {
       // pass p holds rows [64p, 64p+64): wave row wr = p >> 1, fragments 4(p&1)..4(p&1)+3
       if ((pass >> 1) == wr) {
         auto rows = [&](auto H) {
@@ -1377,10 +1531,11 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         if (pass & 1) rows(std::integral_constant<int, 1>{});
         else rows(std::integral_constant<int, 0>{});
       }
+    };
 #if G4_STAMPS
-    }, stmp + 8);
+    tile_epilogue<BM, BN, NTH, decltype(wp), true>(M, N, m0, n0, Cd, E, smem, t, wp, stmp + 8);
 #else
-    });
+    tile_epilogue<BM, BN, NTH, decltype(wp), true>(M, N, m0, n0, Cd, E, smem, t, wp);
 #endif
   };
 
