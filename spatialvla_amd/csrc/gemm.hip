@@ -257,7 +257,13 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
 // kind fixed at compile time: every LDS read of the thread's chunks is issued before the first store, so the pass
 // costs one LDS round trip instead of one per chunk (the runtime-switched per-chunk loop took ~8k cycles per
 // 64-row pass of a 256-wide tile at 256 threads).
-template <int KIND, int BN, int NTH>
+#ifndef G8_EPI_IT
+#define G8_EPI_IT 1
+#endif
+#ifndef G2_EPI_IT
+#define G2_EPI_IT 1
+#endif
+template <int KIND, int BN, int NTH, int ITMAX>
 __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_t N, int64_t m0p, int64_t n0,
                                               bf16_t* cbase, int64_t cm0, int64_t ldc, const svla_epilogue& E,
                                               int t) {
@@ -265,7 +271,8 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
   if constexpr (KIND == SVLA_EPI_GEGLU) {
     constexpr int HC = BN / 16;                 // 8-column chunks per half row (gate | up)
     constexpr int ITT = 64 * HC / NTH;          // chunks per thread
-    constexpr int IT = ITT < 2 ? ITT : 2;       // chunks in flight (register budget beside live accumulators)
+    constexpr int IC = ITMAX < 2 ? ITMAX : 2;
+    constexpr int IT = ITT < IC ? ITT : IC;     // chunks in flight (register budget beside live accumulators)
     const int64_t I = N >> 1;
 #pragma unroll 1
     for (int ib = 0; ib < ITT; ib += IT) {
@@ -302,7 +309,7 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
     constexpr int CPR = BN / 8;
     constexpr int RPP = NTH / CPR;
     constexpr int ITT = 64 / RPP;
-    constexpr int IT = ITT < 4 ? ITT : 4;  // chunks in flight (register budget beside live accumulators)
+    constexpr int IT = ITT < ITMAX ? ITT : ITMAX;  // chunks in flight (register budget beside live accumulators)
     const int cc = t % CPR;
     const int64_t n = n0 + 8 * cc;
     const int64_t nv = N - n;
@@ -397,7 +404,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int NTH, typename WritePass, bool FAST = false>
+template <int BM, int BN, int NTH, typename WritePass, bool FAST = false, int ITMAX = 4>
 __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, int64_t n0, const CDesc& Cd,
                                               const svla_epilogue& E, char* smem, int t, WritePass write_pass,
                                               unsigned long long* ep_stamps = nullptr) {
@@ -427,21 +434,21 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
     const int64_t m0p = m0 + 64 * pass;
     bool fast = FAST;
     if (FAST) switch (kind) {
-      case SVLA_EPI_STORE: epi_pass_fast<SVLA_EPI_STORE, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
-      case SVLA_EPI_BIAS: epi_pass_fast<SVLA_EPI_BIAS, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_STORE: epi_pass_fast<SVLA_EPI_STORE, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_BIAS: epi_pass_fast<SVLA_EPI_BIAS, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
       case SVLA_EPI_BIAS_GELU:
-        epi_pass_fast<SVLA_EPI_BIAS_GELU, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        epi_pass_fast<SVLA_EPI_BIAS_GELU, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
       case SVLA_EPI_BIAS_RESID:
-        epi_pass_fast<SVLA_EPI_BIAS_RESID, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        epi_pass_fast<SVLA_EPI_BIAS_RESID, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
       case SVLA_EPI_GELU_BWD:
-        epi_pass_fast<SVLA_EPI_GELU_BWD, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        epi_pass_fast<SVLA_EPI_GELU_BWD, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
       case SVLA_EPI_GEGLU_BWD:
-        epi_pass_fast<SVLA_EPI_GEGLU_BWD, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        epi_pass_fast<SVLA_EPI_GEGLU_BWD, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
-      case SVLA_EPI_GEGLU: epi_pass_fast<SVLA_EPI_GEGLU, BN, NTH>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_GEGLU: epi_pass_fast<SVLA_EPI_GEGLU, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
       default: fast = false;
     }
     if (fast) {
@@ -626,7 +633,7 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
     }
   }
 
-  tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+  auto wp = [&](int pass, float* Ei) {
     // waves whose accumulator rows fall in [64*pass, 64*pass+64) write them
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -641,7 +648,9 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
         }
       }
     }
-  });
+  };
+  // the 256x256 instance has no registers to spare for the specialised passes (12-20 B of scratch)
+  tile_epilogue<BM, BN, NTH, decltype(wp), !(BM == 256 && BN == 256), G2_EPI_IT>(M, N, m0, n0, Cd, E, smem, t, wp);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -949,7 +958,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 
   auto epilogue = [&](int64_t m0, int64_t n0, const int t) {
     const int lane = t & 63;
-    tile_epilogue<BM, BN, NTH>(M, N, m0, n0, Cd, E, smem, t, [&](int pass, float* Ei) {
+    auto wp = [&](int pass, float* Ei) {
       // pass p holds rows [64p, 64p+64) = A half (p>>1), group (p&1)
       if ((pass & 1) == wr) {
 #pragma unroll
@@ -968,7 +977,8 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
               }
         }
       }
-    });
+    };
+    tile_epilogue<BM, BN, NTH, decltype(wp), true, G8_EPI_IT>(M, N, m0, n0, Cd, E, smem, t, wp);
   };
 
   // one work unit per iteration: whole tiles L, L+G, .. < dp_tiles, then this block's stream-K segments

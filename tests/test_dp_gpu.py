@@ -90,8 +90,15 @@ def test_dp2_train_step_equals_single_process(cuda):
         for r in res:
             got = r[3][n]
             tol = 2 * 2.0 ** -7 * np.abs(ref).max() + 1e-6
+            if n.endswith("k_proj.bias"):
+                # d loss / d k-bias is zero in exact arithmetic (softmax is shift-invariant per query row): AdamW
+                # normalises pure rounding noise, so each run moves it by up to lr per step in either direction
+                tol += 2 * STEPS * 1e-3
             assert np.abs(got - ref).max() <= tol, (n, r[0])
             m_ref, m_got = master1[n], r[2][n]
+            if n.endswith("k_proj.bias"):
+                assert np.abs(m_got - m_ref).max() <= 2 * STEPS * 1e-3 * 1.01, (n, r[0])
+                continue
             assert np.linalg.norm(m_got - m_ref) <= 2e-3 * np.linalg.norm(m_ref) + 1e-6, (n, r[0])
     for n in params1:  # ranks agree bitwise after the all-gather
         assert np.array_equal(res[0][3][n], res[1][3][n]), n

@@ -10,6 +10,6 @@ wait
 for spec in "$@"; do
   name=${spec%%:*}
   others=$(ls ../../build/obj/*.o | grep -v '/gemm\.o$')
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 ../../build/var/gemm_$name.o $others -o ../../build/var/libsvla_$name.so
+  /opt/rocm/bin/hipcc -shared -fPIC -Wl,-Bsymbolic --offload-arch=gfx950 ../../build/var/gemm_$name.o $others -o ../../build/var/libsvla_$name.so
   echo "built build/var/libsvla_$name.so"
 done
