@@ -1,4 +1,4 @@
-// Fused prefix-LM GQA attention with logit softcap and on-load RoPE (Gemma2, head_dim 256) and
+// Fused prefix-LM GQA attention with logit softcap (Gemma2, head_dim 256; RoPE transpose in the backward) and
 // plain bidirectional MHA (SigLIP, head_dim 72), forward and backward, for gfx950.
 //
 // Reference semantics: eager_attention_forward (model/modeling_gemma2.py:169-195): S = QK^T*scale,
@@ -13,9 +13,9 @@
 //  * V (and Q / dO / K where they feed a product over the key or query index) is consumed through
 //    ds_read_b64_tr_b16 transpose reads from row-major LDS tiles; all tiles use the XOR swizzle
 //    chunk ^ 2*(row&7), conflict-free for both the ds_read_b128 row reads and the tr reads.
-//  * RoPE (rotate_half, modeling_gemma2.py:123-154) is applied in registers while Q/K are
-//    loaded (d and d+128 sit in the same lane), and its transpose is applied to dQ/dK in the
-//    accumulators before the store — no separate RoPE pass over HBM.
+//  * RoPE (rotate_half, modeling_gemma2.py:123-154) is not applied here on the way in: q / k arrive rotated
+//    (the QKV GEMM's SVLA_EPI_ROPE epilogue).  The backward applies its transpose to dQ / dK in the accumulators
+//    before the store, so the gradients leave w.r.t. the pre-rotation q / k.
 //  * Backward is two deterministic kernels (dK/dV per key tile looping over the GQA query heads,
 //    dQ per query tile) — no float atomics.
 #include <atomic>
@@ -166,10 +166,49 @@ __device__ __forceinline__ void load_classes(uint8_t* lcls, const uint8_t* cls, 
 template <int D>
 constexpr int tile_bytes(int rows) { return rows * Cfg<D>::RS * 2; }
 
+// Softcapped scores without a running max (CAP): t = cap*tanh(s*scale/cap) lies in (-cap, cap), so p = exp(t)
+// stays a normal fp32 / bf16 number (Gemma2: cap 50, e^50 = 5e21) and the softmax needs neither the row max nor
+// the rescale of the output accumulators.  With r = 1/(1 + 2^(s*c2)), tanh = 1 - 2r and
+//   p = 2^(C0 + C1*r),  c2 = 2*scale*log2(e)/cap,  C0 = cap*log2(e),  C1 = -2*cap*log2(e)
+// -- two v_exp_f32 and one v_rcp_f32 per score.  A masked key gets p = 2^-120 instead of 0: at least one visible
+// key contributes >= e^-cap = 2e-22, so masked keys weigh < 1e-14 of a row, and a row with no visible key
+// becomes uniform over all keys, as the reference's softmax over equal finfo.min logits does.
+struct CapExp {
+  float c2, C0, C1;
+  __device__ __forceinline__ CapExp(float scale, float cap) {
+    const float LOG2E = 1.4426950408889634f;
+    c2 = 2.f * scale * LOG2E / cap;
+    C0 = cap * LOG2E;
+    C1 = -2.f * cap * LOG2E;
+  }
+  __device__ __forceinline__ float r(float s) const { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(s * c2)); }
+  // log2 of p = exp(t), given r
+  __device__ __forceinline__ float lg2p(float r) const { return fmaf(C1, r, C0); }
+};
+constexpr float MASKED_LG2P = -120.f;
+
+// every key of the 64-key tile at k0 is in range and visible to every query (class 0, no effective window):
+// the per-score mask test can be skipped (wave-uniform; one LDS byte per lane)
+__device__ __forceinline__ bool tile_plain(const uint8_t* lcls, int k0, int L, bool window_free, int lane) {
+  const int kj = k0 + lane;
+  const bool ok = kj < L && lcls[kj] == 0;
+  return window_free && __ballot(ok) == ~0ull;
+}
+
+// blocks of one (batch, head group) are consecutive logical ids; xcd_remap puts consecutive ids on one XCD so the
+// query tiles sharing a K/V stream share that XCD's L2
+__device__ __forceinline__ void block_coords(int nqt, int nhg, int& qt, int& hg, int& b) {
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  qt = id % nqt;
+  hg = (id / nqt) % nhg;
+  b = id / (nqt * nhg);
+}
+
 // ================================================================== forward
 // Block = (query tile of 64, NH query heads sharing one kv head, batch); 4 waves per head, 16 queries per wave.
 // K/V tiles stream through two LDS stages by LDS-DMA: tile kt+1 lands while tile kt is consumed.
-template <int D, int NH>
+template <int D, int NH, bool CAP>
 __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
                                                                int64_t ldo, float* __restrict__ lse) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
@@ -178,14 +217,16 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
 
-  const int b = blockIdx.z, qt = blockIdx.x;
+  const int L = a.L;
+  int qt, hg, b;
+  block_coords((L + 63) / 64, a.Hq / NH, qt, hg, b);
   const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int h = blockIdx.y * NH + (w >> 2), wq = w & 3;
+  const int h = hg * NH + (w >> 2), wq = w & 3;
   const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int L = a.L;
   const int qi = qt * 64 + 16 * wq + c;
   const bool qvalid = qi < L;
+  const bool window_free = a.sliding_window <= 0 || a.sliding_window >= L;
 
   const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
@@ -203,6 +244,7 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   for (int i = 0; i < NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
   const float LOG2E = 1.4426950408889634f;
+  const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
 
   for (int kt = 0; kt < nkt; ++kt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -215,6 +257,7 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
       glds_tile<RS, 64, NW>(nx, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
       glds_tile<RS, 64, NW>(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
     }
+    const bool plain = tile_plain(lcls, kt * 64, L, window_free, lane);
     f32x4 s[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -223,36 +266,56 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
       for (int ks = 0; ks < NKS; ++ks)
         s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsK, 16 * nt, ks, lane), qf[ks], s[nt], 0, 0, 0);
     }
-    float x[4][4];
-    float mt = -INFINITY;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kj = kt * 64 + 16 * nt + 4 * g + j;
-        float v = softcap_f(s[nt][j] * a.scale, a.softcap);
-        if (kj >= L) v = -INFINITY;
-        else if (!visible(lcls[kj], kj, qi, a.sliding_window)) v = MASKVAL;
-        x[nt][j] = v;
-        mt = fmaxf(mt, v);
-      }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mnew = fmaxf(m, mt);
-    const float alpha = __expf(m - mnew);  // m=-inf -> 0
-    float ps = 0.f;
     float p[4][4];
+    if constexpr (CAP) {
+      float ps = 0.f;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        p[nt][j] = exp2f((x[nt][j] - mnew) * LOG2E);
-        ps += p[nt][j];
-      }
-    l = l * alpha + ps;
-    m = mnew;
+        for (int j = 0; j < 4; ++j) {
+          float e = ce.lg2p(ce.r(s[nt][j]));
+          if (!plain) {
+            const int kj = kt * 64 + 16 * nt + 4 * g + j;
+            if (!visible(lcls[kj], kj, qi, a.sliding_window)) e = MASKED_LG2P;
+            if (kj >= L) e = -INFINITY;
+          }
+          p[nt][j] = __builtin_amdgcn_exp2f(e);
+          ps += p[nt][j];
+        }
+      l += ps;
+    } else {
+      float x[4][4];
+      float mt = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < NDT; ++i) acc[i] *= alpha;
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = s[nt][j] * (a.scale * LOG2E);  // log2 domain
+          if (!plain) {
+            const int kj = kt * 64 + 16 * nt + 4 * g + j;
+            if (kj >= L) v = -INFINITY;
+            else if (!visible(lcls[kj], kj, qi, a.sliding_window)) v = MASKVAL;
+          }
+          x[nt][j] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mnew = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m=-inf -> 0
+      float ps = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p[nt][j] = __builtin_amdgcn_exp2f(x[nt][j] - mnew);
+          ps += p[nt][j];
+        }
+      l = l * alpha + ps;
+      m = mnew;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) acc[i] *= alpha;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       float pv[8] = {p[2 * ks][0], p[2 * ks][1], p[2 * ks][2], p[2 * ks][3],
@@ -264,7 +327,8 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.0f / l;
-  if (qvalid && g == 0) lse[((int64_t)b * a.Hq + h) * L + qi] = m + __logf(l);
+  // natural-log lse of the scores (CAP: of p = exp(t) directly; else of the max-shifted log2-domain sum)
+  if (qvalid && g == 0) lse[((int64_t)b * a.Hq + h) * L + qi] = CAP ? __logf(l) : (m + __log2f(l)) / LOG2E;
 
   // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [16 q][DV] -> 16-B stores
   __syncthreads();
@@ -329,44 +393,70 @@ __device__ __forceinline__ void rope_t_acc(f32x4 (&acc)[NDT], const svla_attn_ar
     }
 }
 
+// Per-score backward factor z = dS * dt/ds * scale (the softcap chain rule), for the score s (raw dot product)
+// of a query with log2-domain lse2 and delta, or 0 when out of range.  Same p as the forward (CapExp, masked keys
+// at 2^-120 of the row scale).
+template <bool CAP>
+__device__ __forceinline__ float score_grad(float s, float dp, float lse2, float delta, bool masked, const CapExp& ce,
+                                            float scale) {
+  const float LOG2E = 1.4426950408889634f;
+  if constexpr (CAP) {
+    const float r = ce.r(s);
+    const float p = __builtin_amdgcn_exp2f((masked ? MASKED_LG2P : ce.lg2p(r)) - lse2);
+    return p * (dp - delta) * (4.f * r * (1.f - r)) * scale;  // d tanh = 1 - (1 - 2r)^2
+  } else {
+    const float p = __builtin_amdgcn_exp2f((masked ? MASKVAL : s * (scale * LOG2E)) - lse2);
+    return p * (dp - delta) * scale;
+  }
+}
+
 // ================================================================== backward: dK, dV
-// Block = (key tile of 64, kv head, batch), 4 waves x 16 keys.  K/V stay in LDS; the query heads of the group
-// and their 32-row Q / dO tiles stream through two LDS stages by LDS-DMA.  lse / delta of the group's heads
-// and the key classes are preloaded to LDS.
-template <int D, bool ROPE>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
+// Block = (key tile of 64, kv head, batch), 4 waves x 16 keys.  Each wave keeps the K rows of its keys in
+// registers (the B operand of S for every query) and reads its V rows from the block's LDS V tile.  The query
+// heads of the group and their 32-row Q / dO tiles stream through one LDS stage by LDS-DMA (a co-resident block
+// covers the load); lse / delta of the group's heads and the key classes are preloaded to LDS.  ~70 KiB of LDS: two blocks per CU where registers allow
+// (D=72; at D=256 the K-row registers plus both accumulators need more than 256 VGPRs).
+template <int D, bool ROPE, bool CAP>
+__global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
                                                               int64_t lddo, const float* __restrict__ lse,
                                                               const float* __restrict__ delta, bf16_t* __restrict__ dk,
                                                               int64_t lddk, bf16_t* __restrict__ dv, int64_t lddv) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
   constexpr int NKS = DP / 32, NDT = DV / 16;
-  constexpr int TB = tile_bytes<D>(64), QB = tile_bytes<D>(32), QSTAGE = 2 * QB;
+  constexpr int TB = tile_bytes<D>(64), QB = tile_bytes<D>(32);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ldsK = smem;
-  char* ldsV = smem + TB;
-  char* qst = smem + 2 * TB;  // 2 stages of {Q [32][RS], dO [32][RS]}
-  const int L = a.L;
+  char* ldsV = smem;
+  char* ldsQ = smem + TB;  // {Q [32][RS], dO [32][RS]}
+  char* ldsO = ldsQ + QB;
+  const int L = a.L, LP = (L + 35) / 32 * 32;  // lse/delta row stride: every 32-query tile in range
   const int grp = a.Hq / a.Hkv;
-  float* llse = (float*)(qst + 2 * QSTAGE);  // [grp][L]
-  float* ldel = llse + grp * L;
-  uint8_t* lcls = (uint8_t*)(ldel + grp * L);
+  float* llse = (float*)(ldsO + QB);  // [grp][LP], log2 domain
+  float* ldel = llse + grp * LP;
+  uint8_t* lcls = (uint8_t*)(ldel + grp * LP);
 
-  const int b = blockIdx.z, hk = blockIdx.y, kt = blockIdx.x;
+  int kt, hk, b;
+  block_coords((L + 63) / 64, a.Hkv, kt, hk, b);
   const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
+  const float LOG2E = 1.4426950408889634f;
 
   load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 256);
-  for (int i = t; i < grp * L; i += 256) {
-    const int hh = i / L, q = i % L;
+  for (int i = t; i < grp * LP; i += 256) {
+    const int hh = i / LP, q = i % LP;
     const int64_t o = ((int64_t)b * a.Hq + hk * grp + hh) * L + q;
-    llse[i] = lse[o];
-    ldel[i] = delta[o];
+    llse[i] = q < L ? lse[o] * LOG2E : 0.f;
+    ldel[i] = q < L ? delta[o] : 0.f;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int r0 = kt * 64;
-  glds_tile<RS, 64, 4>(ldsK, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
+  const int kl = 16 * w + c;  // this lane's key (local)
+  const int kj = r0 + kl;
+  bf16x8 kf[NKS];
+  load_row_frags<D>(kf, kbase + (int64_t)kj * a.ldk, kj < L, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // classes visible to tile_plain
+  const int kcls = kj < L ? lcls[kj] : 3;  // this lane's key class (3: beyond L)
   glds_tile<RS, 64, 4>(ldsV, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
 
   const int nqt = (L + 31) / 32, nsteps = grp * nqt;
@@ -378,32 +468,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
     glds_tile<RS, 32, 4>(dst, qb, a.ldq, L - q0, D, w, lane);
     glds_tile<RS, 32, 4>(dst + QB, ob, lddo, L - q0, D, w, lane);
   };
-  issue_q(0, qst);
 
-  const int kl = 16 * w + c;  // this lane's key (local)
-  const int kj = r0 + kl;
   f32x4 adk[NDT], adv[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) adk[i] = adv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float LOG2E = 1.4426950408889634f;
+  const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
 
   for (int step = 0; step < nsteps; ++step) {
+    if (step) __syncthreads();  // every wave is done with the previous Q / dO tile
+    issue_q(step, ldsQ);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const char* ldsQ = qst + (step & 1) * QSTAGE;
-    const char* ldsO = ldsQ + QB;
-    if (step + 1 < nsteps) issue_q(step + 1, qst + ((step + 1) & 1) * QSTAGE);
     const int hh = step / nqt, q0 = (step % nqt) * 32;
-    const float* sl = llse + hh * L;
-    const float* sd = ldel + hh * L;
+    const float* sl = llse + hh * LP;
+    const float* sd = ldel + hh * LP;
     f32x4 s[2], dp[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       s[mt] = dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsQ, 16 * mt, ks, lane),
-                                                        frag_row<RS>(ldsK, 16 * w, ks, lane), s[mt], 0, 0, 0);
+        s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsQ, 16 * mt, ks, lane), kf[ks], s[mt], 0, 0, 0);
         dp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsO, 16 * mt, ks, lane),
                                                          frag_row<RS>(ldsV, 16 * w, ks, lane), dp[mt], 0, 0, 0);
       }
@@ -411,22 +496,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
     // element (mt, j): query q0 + 16mt + 4g + j, key = lane col (kl)
     float pv[8], zv[8];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(sl + q0 + 16 * mt + 4 * g);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sd + q0 + 16 * mt + 4 * g);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int qi = q0 + 16 * mt + 4 * g + j;
-        float p = 0.f, z = 0.f;
-        if (qi < L && kj < L) {
-          const float sc = softcap_f(s[mt][j] * a.scale, a.softcap);
-          const float xv = visible(lcls[kj], kj, qi, a.sliding_window) ? sc : MASKVAL;
-          p = exp2f((xv - sl[qi]) * LOG2E);
-          const float ds = p * (dp[mt][j] - sd[qi]);
-          const float dcap = a.softcap > 0.f ? (1.0f - (sc / a.softcap) * (sc / a.softcap)) : 1.0f;
-          z = ds * dcap * a.scale;
+        const bool live = qi < L && kcls != 3;
+        const bool masked = !visible(kcls, kj, qi, a.sliding_window);
+        float p, z;
+        if constexpr (CAP) {
+          const float r = ce.r(s[mt][j]);
+          p = __builtin_amdgcn_exp2f((masked ? MASKED_LG2P : ce.lg2p(r)) - l4[j]);
+          z = p * (dp[mt][j] - d4[j]) * (4.f * r * (1.f - r)) * a.scale;
+        } else {
+          p = __builtin_amdgcn_exp2f((masked ? MASKVAL : s[mt][j] * (a.scale * LOG2E)) - l4[j]);
+          z = p * (dp[mt][j] - d4[j]) * a.scale;
         }
-        pv[4 * mt + j] = p;
-        zv[4 * mt + j] = z;
+        pv[4 * mt + j] = live ? p : 0.f;
+        zv[4 * mt + j] = live ? z : 0.f;
       }
+    }
     const bf16x8 pa = pack_frag(pv), za = pack_frag(zv);
     mfma_tr_sweep<RS, NDT, false>(adv, ldsO, 0, pa, lane);
     mfma_tr_sweep<RS, NDT, false>(adk, ldsQ, 0, za, lane);
@@ -462,7 +552,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkv_kernel(svla_attn_args a, 
 // ================================================================== backward: dQ
 // Block = (query tile of 64, NH query heads sharing one kv head, batch), like the forward: K/V tiles stream
 // through two LDS stages by LDS-DMA.
-template <int D, int NH, bool ROPE>
+template <int D, int NH, bool ROPE, bool CAP>
 __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
                                                                   int64_t lddo, const float* __restrict__ lse,
                                                                   const float* __restrict__ delta,
@@ -473,24 +563,27 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
 
-  const int b = blockIdx.z, qt = blockIdx.x;
+  const int L = a.L;
+  int qt, hg, b;
+  block_coords((L + 63) / 64, a.Hq / NH, qt, hg, b);
   const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int h = blockIdx.y * NH + (w >> 2), wq = w & 3;
+  const int h = hg * NH + (w >> 2), wq = w & 3;
   const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int L = a.L;
   const int qi = qt * 64 + 16 * wq + c;
   const bool qvalid = qi < L;
+  const bool window_free = a.sliding_window <= 0 || a.sliding_window >= L;
   const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
   const bf16_t* obase = dout + (int64_t)b * L * lddo + (int64_t)h * D;
   const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
+  const float LOG2E = 1.4426950408889634f;
 
   load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 64 * NW);
   bf16x8 qf[NKS], of[NKS];
   load_row_frags<D>(qf, qbase + (int64_t)qi * a.ldq, qvalid, lane);
   load_row_frags<D>(of, obase + (int64_t)qi * lddo, qvalid, lane);
-  const float lq = qvalid ? lse[((int64_t)b * a.Hq + h) * L + qi] : 0.f;
+  const float lq = qvalid ? lse[((int64_t)b * a.Hq + h) * L + qi] * LOG2E : 0.f;
   const float dq_ = qvalid ? delta[((int64_t)b * a.Hq + h) * L + qi] : 0.f;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nkt = (L + 63) / 64;
@@ -500,7 +593,7 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
   f32x4 acc[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float LOG2E = 1.4426950408889634f;
+  const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
   for (int kt = 0; kt < nkt; ++kt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -512,6 +605,7 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
       glds_tile<RS, 64, NW>(nx, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, D, w, lane);
       glds_tile<RS, 64, NW>(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
     }
+    const bool plain = tile_plain(lcls, kt * 64, L, window_free, lane);
     f32x4 s[4], dp[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -528,16 +622,13 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int kj = kt * 64 + 16 * nt + 4 * g + j;
-        float z = 0.f;
-        if (qvalid && kj < L) {
-          const float sc = softcap_f(s[nt][j] * a.scale, a.softcap);
-          const float xv = visible(lcls[kj], kj, qi, a.sliding_window) ? sc : MASKVAL;
-          const float p = exp2f((xv - lq) * LOG2E);
-          const float ds = p * (dp[nt][j] - dq_);
-          const float dcap = a.softcap > 0.f ? (1.0f - (sc / a.softcap) * (sc / a.softcap)) : 1.0f;
-          z = ds * dcap * a.scale;
+        bool masked = false, live = qvalid;
+        if (!plain) {
+          live = live && kj < L;
+          masked = !visible(lcls[kj < L ? kj : 0], kj, qi, a.sliding_window);
         }
-        zz[nt][j] = z;
+        const float z = score_grad<CAP>(s[nt][j], dp[nt][j], lq, dq_, masked, ce, a.scale);
+        zz[nt][j] = live ? z : 0.f;
       }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -594,30 +685,32 @@ int check_args(const svla_attn_args* a) {
 
 int round16(int x) { return (x + 15) & ~15; }
 
-template <int D, int NH>
+template <int D, int NH, bool CAP>
 int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
   const int lds = 4 * tile_bytes<D>(64) + round16(a.L);
   SVLA_CHECK_ARG(lds <= 160 * 1024, "attn_fwd: L too large for the LDS-resident key classes");
-  dim3 grid((a.L + 63) / 64, a.Hq / NH, a.B), block(256 * NH);
-  set_lds_once<attn_fwd_kernel<D, NH>>(lds);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NH>), grid, block, lds, s, a, out, ldo, lse);
+  const int64_t nblk = (int64_t)((a.L + 63) / 64) * (a.Hq / NH) * a.B;
+  SVLA_CHECK_ARG(nblk < (1LL << 31), "attn_fwd: grid too large");
+  set_lds_once<attn_fwd_kernel<D, NH, CAP>>(lds);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NH, CAP>), dim3((unsigned)nblk), dim3(256 * NH), lds, s, a, out, ldo, lse);
   return svla::check_launch("attn_fwd");
 }
 
-template <int D, int NH, bool ROPE>
+template <int D, int NH, bool ROPE, bool CAP>
 int bwd_launch(const svla_attn_args& a, const bf16_t* dout, int64_t lddo, const float* lse, const float* delta,
                bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv, int64_t lddv, hipStream_t s) {
   const int grp = a.Hq / a.Hkv;
-  const int lds_kv = 2 * tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + round16(8 * grp * a.L) + round16(a.L);
+  const int LP = (a.L + 35) / 32 * 32;
+  const int lds_kv = tile_bytes<D>(64) + 2 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
   SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
   const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
   const int nt = (a.L + 63) / 64;
-  set_lds_once<attn_bwd_dkv_kernel<D, ROPE>>(lds_kv);
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE>), dim3(nt, a.Hkv, a.B), dim3(256), lds_kv, s, a, dout, lddo, lse,
-                     delta, dk, lddk, dv, lddv);
-  set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE>>(lds_q);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE>), dim3(nt, a.Hq / NH, a.B), dim3(256 * NH), lds_q, s, a, dout,
-                     lddo, lse, delta, dq, lddq);
+  set_lds_once<attn_bwd_dkv_kernel<D, ROPE, CAP>>(lds_kv);
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE, CAP>), dim3((unsigned)(nt * a.Hkv * a.B)), dim3(256), lds_kv, s, a,
+                     dout, lddo, lse, delta, dk, lddk, dv, lddv);
+  set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE, CAP>>(lds_q);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE, CAP>), dim3((unsigned)(nt * (a.Hq / NH) * a.B)), dim3(256 * NH),
+                     lds_q, s, a, dout, lddo, lse, delta, dq, lddq);
   return svla::check_launch("attn_bwd");
 }
 
@@ -629,9 +722,24 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
   SVLA_CHECK_ARG(!a->rope_cos && !a->rope_sin, "attn_fwd: q/k must arrive rotated (RoPE is a GEMM epilogue)");
   hipStream_t s = (hipStream_t)stream;
   const bool pair = (a->Hq / a->Hkv) % 2 == 0;  // two query heads of a GQA group share the K/V stream
-  if (a->D == 256) return pair ? fwd_launch<256, 2>(*a, (bf16_t*)out, ldo, lse, s)
-                               : fwd_launch<256, 1>(*a, (bf16_t*)out, ldo, lse, s);
-  return fwd_launch<72, 1>(*a, (bf16_t*)out, ldo, lse, s);
+  const bool cap = a->softcap > 0.f;
+  bf16_t* o = (bf16_t*)out;
+  if (a->D == 256) {
+    if (pair) return cap ? fwd_launch<256, 2, true>(*a, o, ldo, lse, s) : fwd_launch<256, 2, false>(*a, o, ldo, lse, s);
+    return cap ? fwd_launch<256, 1, true>(*a, o, ldo, lse, s) : fwd_launch<256, 1, false>(*a, o, ldo, lse, s);
+  }
+  return cap ? fwd_launch<72, 1, true>(*a, o, ldo, lse, s) : fwd_launch<72, 1, false>(*a, o, ldo, lse, s);
+}
+
+template <int D, int NH>
+static int bwd_dispatch(const svla_attn_args& a, bool rope, bool cap, const bf16_t* d_o, int64_t lddo,
+                        const float* lse, const float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
+                        int64_t lddv, hipStream_t s) {
+  bf16_t *q = (bf16_t*)dq, *k = (bf16_t*)dk, *v = (bf16_t*)dv;
+  if (rope) return cap ? bwd_launch<D, NH, true, true>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
+                       : bwd_launch<D, NH, true, false>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
+  return cap ? bwd_launch<D, NH, false, true>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
+             : bwd_launch<D, NH, false, false>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
 }
 
 extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
@@ -649,18 +757,11 @@ extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t l
                      (const bf16_t*)out, ldo, (const bf16_t*)dout, lddo, workspace);
   if (int rc = svla::check_launch("attn_delta")) return rc;
   const bool pair = (a->Hq / a->Hkv) % 2 == 0;
+  const bool cap = a->softcap > 0.f;
   const bf16_t* d_o = (const bf16_t*)dout;
-  if (a->D == 256) {
-    if (pair)
-      return rope ? bwd_launch<256, 2, true>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
-                                             (bf16_t*)dv, lddv, s)
-                  : bwd_launch<256, 2, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
-                                              (bf16_t*)dv, lddv, s);
-    return rope ? bwd_launch<256, 1, true>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
-                                           (bf16_t*)dv, lddv, s)
-                : bwd_launch<256, 1, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk,
-                                            (bf16_t*)dv, lddv, s);
-  }
-  return bwd_launch<72, 1, false>(*a, d_o, lddo, lse, workspace, (bf16_t*)dq, lddq, (bf16_t*)dk, lddk, (bf16_t*)dv,
-                                  lddv, s);
+  if (a->D == 256)
+    return pair ? bwd_dispatch<256, 2>(*a, rope, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s)
+                : bwd_dispatch<256, 1>(*a, rope, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
+  SVLA_CHECK_ARG(!rope, "attn_bwd: RoPE only with D=256");
+  return bwd_dispatch<72, 1>(*a, false, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
 }
