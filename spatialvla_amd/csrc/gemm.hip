@@ -1944,18 +1944,7 @@ struct GemmCtx {
   int variant;
 };
 
-int num_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) dev = 0;
-  if (cus[dev] == 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cus[dev] = v;
-  }
-  return cus[dev];
-}
+using svla::num_cus;
 
 // 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
 size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }

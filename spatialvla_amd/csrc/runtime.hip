@@ -21,6 +21,20 @@ int check_launch(const char* what) {
   }
   return SVLA_OK;
 }
+
+// compute units of the current device (cached per device; 256 on MI355X)
+int num_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cus[dev] = v;
+  }
+  return cus[dev];
+}
 }  // namespace svla
 
 extern "C" const char* svla_last_error(void) { return svla::g_err; }

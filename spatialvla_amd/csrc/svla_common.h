@@ -26,8 +26,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (RNE) in ONE v_cvt_pk_bf16_f32 (the scalar form f2bf(a) | f2bf(b) << 16 costs
+// two converts plus a shift and an or)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 __device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
 #pragma unroll
@@ -108,6 +113,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 namespace svla {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+int num_cus();
 }  // namespace svla
 
 #define SVLA_CHECK_ARG(cond, ...)            \

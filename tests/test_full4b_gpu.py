@@ -155,7 +155,9 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
     assert hip["act"] <= max(H.LOGITS_TOL, 1.5 * ora["act"])
     assert hip["cols"] <= max(H.LOGITS_TOL, 1.5 * ora["cols"])
     assert hip["agree_025"] == 1.0
-    assert hip["agree_005"] >= ora["agree_005"] - 0.01
+    # margin 0.05 is below one bf16 ulp of logits of magnitude 8-30 (0.06-0.125): those rows are ties at the
+    # logits' precision, so only a loose bound (8 of 256 rows) -- the 0.25-margin rows above must agree exactly
+    assert hip["agree_005"] >= ora["agree_005"] - 0.03
     assert max(hip["gradnorm"].values()) < H.GRAD_TOL, worst_n
     assert len(full_rel) > 700 and max(full_rel.values()) <= 8e-2, worst_f
 
