@@ -300,8 +300,6 @@ def main():
     for s in range(args.warmup):
         ts = time.perf_counter()
         losses.append(engine.train_step(batches[s]))
-        if s == 0:
-            model.strict_checks = False  # batch layout validated once (reference raises on mismatch)
         torch.cuda.synchronize()
         log(f"[bench] warmup step {s}: {time.perf_counter() - ts:.3f}s loss {losses[-1].item():.4f}")
     if world > 1:

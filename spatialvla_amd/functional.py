@@ -609,6 +609,7 @@ class LMHeadCEFn(torch.autograd.Function):
         stash["n_valid"] = loss2[1:2]
         ctx.save_for_backward(h, w, logits_buf, lse, target, loss2)
         ctx.cap, ctx.V = cap, V
+        ctx.row_plan = stash.pop("row_plan", None) if stash is not None else None
         ctx.mark_non_differentiable(logits_buf)
         return logits_buf[:, :V], loss2[0]
 
@@ -623,8 +624,15 @@ class LMHeadCEFn(torch.autograd.Function):
         M, ldv = logits_buf.shape
         V = ctx.V
         gscale = (dloss.float() / torch.clamp(loss2[1], min=1.0)).reshape(1).contiguous()
-        rows = torch.nonzero(target >= 0).view(-1)
-        R = int(rows.numel())  # one host sync per step
+        if ctx.row_plan is not None:  # labelled rows first + their count, fetched behind the forward's event
+            order, cnt, ev = ctx.row_plan
+            if ev is not None:
+                ev.synchronize()
+                cnt = int(cnt[0])
+            rows = order[:cnt]
+        else:
+            rows = torch.nonzero(target >= 0).view(-1)
+        R = int(rows.numel())
         dh = torch.zeros_like(h) if ctx.needs_input_grad[0] else None
         dw, acc, rw = _grad_dest(w, ctx.needs_input_grad[1])
         if R == 0:

@@ -152,9 +152,36 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         self.pad_token_id = config.pad_token_id if config.pad_token_id is not None else -1
         # predict_action replays each decode step from a captured HIP graph (SVLA_DECODE_GRAPHS=0: eager launches)
         self.decode_graphs = os.environ.get("SVLA_DECODE_GRAPHS", "1") != "0"
-        self.strict_checks = True   # reference raises on an image-token count mismatch (needs a host sync)
+        # reference raises on an image-token count mismatch (:379-385); here the count is copied to pinned host
+        # memory behind an event and checked at the next forward (check_deferred), so no step waits on the GPU
+        self.strict_checks = True
+        self._deferred = []
         self.last_stash = {}
         self.post_init()
+
+    # ------------------------------------------------------------------ deferred host checks
+    @staticmethod
+    def _pinned_i64(dev):
+        return torch.zeros(1, dtype=torch.int64, pin_memory=dev.type == "cuda")  # torch's caching host allocator
+
+    def _defer(self, value, check):
+        """Copy the device scalar `value` to pinned host memory behind an event; check(v) runs at the next
+        check_deferred().  CPU tensors are checked at once."""
+        if value.device.type != "cuda":
+            check(int(value))
+            return
+        buf = self._pinned_i64(value.device)
+        buf.copy_(value.reshape(1).to(torch.int64), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._deferred.append((buf, ev, check))
+
+    def check_deferred(self):
+        """Run the pending host checks (waits for their events: recorded one forward earlier, long complete)."""
+        pend, self._deferred = self._deferred, []
+        for buf, ev, check in pend:
+            ev.synchronize()
+            check(int(buf[0]))
 
     # ------------------------------------------------------------------ reference accessors
     def get_input_embeddings(self):
@@ -253,14 +280,18 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         img_index = None
         if image_features is not None:
             img_mask = ids == cfg.image_token_index
+            n_img = image_features.shape[0] * image_features.shape[1]
             if self.strict_checks:
-                n_tok = int(img_mask.sum().item())
-                if n_tok * image_features.shape[-1] != image_features.numel():
-                    raise ValueError(
-                        "Number of images does not match number of special image tokens in the input text. "
-                        f"Got {n_tok} image tokens in the text but {image_features.shape[0] * image_features.shape[1]} "
-                        "tokens from image embeddings.")
-            img_index = torch.where(img_mask, torch.cumsum(img_mask.to(torch.int32), 0) - 1, -1).to(torch.int32)
+                def check(n_tok, n_img=n_img):
+                    if n_tok != n_img:
+                        raise ValueError(
+                            "Number of images does not match number of special image tokens in the input text. "
+                            f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
+                self._defer(img_mask.sum(), check)
+            # image rows beyond the features (a mismatch, reported by the deferred check) read the text embedding
+            # instead of past the end of the feature rows
+            idx = torch.cumsum(img_mask.to(torch.int32), 0) - 1
+            img_index = torch.where(img_mask & (idx < n_img), idx, -1).to(torch.int32)
         spatial_w, sort_rows, offsets, a0 = None, None, None, 0
         if cfg.use_spatial_token:
             spatial_w = self.spatial_embed_tokens.weight
@@ -278,6 +309,20 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         img2d = image_features.reshape(-1, image_features.shape[-1]) if image_features is not None else None
         out = Fn.EmbedMergeFn.apply(ids, img_index, img2d, spatial_w, embed_w, a0, normalizer, sort_rows, offsets)
         return out.view(B, Lq, hidden)
+
+    def _label_rows(self, target):
+        """Rows with a label, for the lm_head backward, without a host sync: the labelled rows first in order
+        (stable sort of the validity flag) and their count copied to pinned memory behind an event recorded
+        here -- the backward reads it after the whole forward, when the event has long completed."""
+        valid = target >= 0
+        order = torch.argsort((~valid).to(torch.int8), stable=True)
+        if target.device.type != "cuda":
+            return order, int(valid.sum()), None
+        buf = self._pinned_i64(target.device)
+        buf.copy_(valid.sum().reshape(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return order, buf, ev
 
     @staticmethod
     def _targets(labels, attention_mask, B, Lq, dev, pad_mask=None):
@@ -313,6 +358,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         num_logits_to_keep: int = 0,
         kv_mask: Optional[KVMask] = None,
     ) -> Union[Tuple, SpatialVLACausalLMOutputWithPast]:
+        self.check_deferred()
         cache = past_key_values
         if cache is not None and not isinstance(cache, Gemma2KVCache):
             raise ValueError("past_key_values must be a Gemma2KVCache (see new_cache())")
@@ -331,8 +377,9 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         if pixel_values is not None:
             image_features = self.get_image_features(pixel_values, intrinsic)
 
-        if labels is not None and (labels == self.pad_token_id).any():  # reference :390-395 (BC path)
-            labels = torch.where(input_ids == self.pad_token_id, -100, labels)
+        if labels is not None:  # reference :390-395 (BC path: only when pad_token_id occurs in labels), sync-free
+            has_pad = (labels == self.pad_token_id).any()
+            labels = torch.where(has_pad & (input_ids == self.pad_token_id), -100, labels)
 
         hidden = self._merge_inputs(input_ids, image_features)
         past = cache.seen_tokens if cache is not None else 0
@@ -355,6 +402,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
 
         target = self._targets(labels, attention_mask, B, Lq, dev)
         stash = {}
+        if labels is not None and torch.is_grad_enabled():
+            stash["row_plan"] = self._label_rows(target)
         logits2d, loss = self.language_model.head(h, target, stash)
         self.last_stash = stash
         logits = logits2d.view(B, Lq, -1)

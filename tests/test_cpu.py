@@ -229,6 +229,44 @@ def test_model_state_dict_keys_match_reference_weight_abi():
     assert extra == {"language_model.model.embed_tokens.weight"}  # frozen in the reference
 
 
+def test_from_pretrained_roundtrip_reference_layout(tmp_path):
+    """save_pretrained -> from_pretrained on a checkpoint in the reference's key layout (the transformers
+    SiglipVisionModel / Gemma2ForCausalLM names of tests/golden/tiny_train.safetensors): every tensor comes back
+    bitwise, and the last spatial_token_num rows of embed_tokens are overwritten by spatial_embed_tokens as the
+    reference's from_pretrained does (model/modeling_spatialvla.py:524-525)."""
+    from safetensors.torch import load_file
+    from spatialvla_amd import SpatialVLAConfig
+    from spatialvla_amd.detinit import deterministic_init_
+    from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration
+    cfg = SpatialVLAConfig(**H.cfg_dict("tiny"))
+    m = SpatialVLAForConditionalGeneration(cfg).to(torch.bfloat16)
+    deterministic_init_(m, seed=5)
+    n = cfg.spatial_token_num
+    with torch.no_grad():  # make the tail copy observable: stored tail != spatial_embed_tokens
+        m.language_model.model.embed_tokens.weight[-n:] = 0.25
+    m.save_pretrained(tmp_path, safe_serialization=True)
+    files = sorted(tmp_path.glob("*.safetensors"))
+    assert files
+    saved = {}
+    for f in files:
+        saved.update(load_file(str(f)))
+    ref_keys = {k[5:] for k in _load("tiny_train.safetensors") if k.startswith("grad.")}
+    on_disk = {k.replace("vision_tower.vision_model.", "vision_tower.") for k in saved}
+    assert ref_keys <= on_disk  # the checkpoint carries the reference's names
+    m2 = SpatialVLAForConditionalGeneration.from_pretrained(tmp_path, torch_dtype=torch.bfloat16)
+    sd1, sd2 = m.state_dict(), m2.state_dict()
+    assert set(sd1) == set(sd2)
+    emb = "language_model.model.embed_tokens.weight"
+    for k, v in sd1.items():
+        if k in (emb, "language_model.lm_head.weight"):
+            continue
+        assert torch.equal(sd2[k], v), k
+    e1, e2 = sd1[emb], sd2[emb]
+    assert torch.equal(e2[:-n], e1[:-n])
+    assert torch.equal(e2[-n:], sd2["spatial_embed_tokens.weight"])
+    assert not torch.equal(e2[-n:], e1[-n:])
+
+
 def test_product_fails_loudly_without_gpu():
     from spatialvla_amd import SpatialVLAConfig
     from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration

@@ -73,6 +73,38 @@ def _check_variants(outs, tol=2e-3):
         assert rel_l2(_flat(outs[v]), _flat(outs[1])) < tol, v
 
 
+def test_gemm_two_streams_bitwise(cuda):
+    """svla_gemm_bf16 is re-entrant across streams (include/svla.h): GEMMs that use stream-K (slabs + arrival
+    counters in the caller's workspace) run concurrently on two streams, each with its own workspace, and return
+    exactly what they return one at a time."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(21)
+    shapes = [(4096, 2304, 4096), (2048, 4608, 3072), (9984, 2304, 2304)]  # < 1 or ragged waves of tiles: stream-K
+    xs = [_r(m, k) for m, n, k in shapes]
+    ws = [_r(n, k, scale=0.05) for m, n, k in shapes]
+    ref = []
+    for x, w in zip(xs, ws):
+        o = torch.empty(x.shape[0], w.shape[0], dtype=BF, device=cuda)
+        Kn.linear_fwd(x, [w], o)
+        ref.append(o)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[torch.empty_like(r) for r in ref] for _ in streams]
+    for rep in range(4):
+        for i in range(len(shapes)):  # interleave the launches of both streams
+            for si, st in enumerate(streams):
+                with torch.cuda.stream(st):
+                    j = (i + si) % len(shapes)
+                    Kn.linear_fwd(xs[j], [ws[j]], outs[si][j])
+    torch.cuda.synchronize()
+    w0 = Kn.gemm_workspace(streams[0])
+    w1 = Kn.gemm_workspace(streams[1])
+    assert w0.data_ptr() != w1.data_ptr()
+    for si in range(2):
+        for j in range(len(shapes)):
+            assert torch.equal(outs[si][j], ref[j]), (si, j)
+
+
 @pytest.mark.parametrize("M,N,K", [(2000, 16500, 200), (2304, 14336, 1000), (4100, 8200, 64), (9984, 2304, 2048),
                                    (1000, 3000, 8192)])
 @pytest.mark.parametrize("layouts", ["nt", "nn", "tn"])

@@ -266,3 +266,28 @@ def test_decode_states_bounded_and_invalidated(cuda):
     assert len(model._svla_decode_states) == 0
     again = model.predict_action(dict(base, input_ids=ids), max_new_tokens=3, eos_token_id=-1)
     assert torch.equal(again, ref)
+
+
+def test_image_token_mismatch_raises_deferred(cuda):
+    """The reference raises when the image-token count differs from the image feature rows (:379-385).  The HIP
+    forward copies the count to pinned memory behind an event and raises at check_deferred() (run at the start of
+    the next forward), so a training step never waits on it; meanwhile the surplus image positions read the text
+    embedding instead of running past the feature rows."""
+    g = _load("tiny_train.safetensors")
+    cfgd = H.cfg_dict("tiny")
+    model = H.build_hip_model(cfgd, "cuda:0")
+    batch = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
+    model.predict_depth = lambda pv: g["out.depth"].to(cuda)
+    ids = batch["input_ids"].clone()
+    img_pos = (ids[0] == model.config.image_token_index).nonzero().view(-1)
+    ids[0, img_pos[0]] = model.config.image_token_index + 1  # one image token fewer than feature rows
+    batch["input_ids"] = ids
+    with torch.no_grad():
+        out = model(**batch)
+    assert torch.isfinite(out.logits.float()).all()
+    with pytest.raises(ValueError, match="Number of images does not match"):
+        model.check_deferred()
+    with torch.no_grad():  # a well-formed batch afterwards runs clean
+        batch["input_ids"] = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}["input_ids"]
+        model(**batch)
+        model.check_deferred()
