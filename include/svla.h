@@ -66,10 +66,14 @@ enum {
   SVLA_EPI_GEGLU_BWD = 5,  /* acc = dH; in0=g, in1=u: out1 = dH*u*gelu'(g), out2 = dH*gelu(g) */
   SVLA_EPI_GELU_BWD = 6,   /* acc = dAct; in0 = pre-activation: C = dAct*gelu'(pre)           */
   SVLA_EPI_SOFTCAP_CE = 7, /* C = cap*tanh(acc/cap); row_stats[m, tile_n] = {max,sumexp,argmax} */
-  SVLA_EPI_ROPE = 8        /* C = bf16(acc), then Gemma2 rotate_half RoPE on columns < rope_cols (heads of
+  SVLA_EPI_ROPE = 8,       /* C = bf16(acc), then Gemma2 rotate_half RoPE on columns < rope_cols (heads of
                               rope_D, position m % rope_L, tables [rope_L][rope_D/2]) with the reference's bf16
                               rounding: bf16(bf16(x*cos) + bf16(rotate_half(x)*sin))
                               (model/modeling_gemma2.py:123-154) — q/k leave the QKV GEMM rotated */
+  SVLA_EPI_BIAS_GELU_ERF = 9,    /* C = bf16(gelu_erf(bf16(acc + bias[n])))  (BEiT MLP fc1 + exact GELU, no
+                                    pre-activation output: the ZoeDepth backbone is frozen) */
+  SVLA_EPI_BIAS_SCALE_RESID = 10 /* C = bf16(bf16(colscale[n] * bf16(acc + bias[n])) + in0[m,n])  (BEiT layer
+                                    scale lambda * sublayer + residual; bias optional) */
 };
 
 typedef struct {
@@ -89,6 +93,7 @@ typedef struct {
   int64_t rope_cols;         /* columns [0, rope_cols) are rotated (q and k heads), the rest (v) plain */
   int32_t rope_L;            /* sequence length: row m is position m % rope_L */
   int32_t rope_D;            /* head dim; the GEMM tile width must be a multiple of it */
+  const void* colscale;      /* [N] bf16 (BIAS_SCALE_RESID) */
 } svla_epilogue;
 
 /* C: up to 4 row segments (c_seg_start tile-aligned to 128) — lets dW of q/k/v (or gate/up)
@@ -126,7 +131,10 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
  * rope_cos/rope_sin ([L][D/2] bf16, row stride rope_ld) are for svla_attn_bwd only: with them dq/dk are
  * returned w.r.t. the pre-rotation q/k (the transpose of rotate_half RoPE applied to the gradients);
  * svla_attn_fwd rejects them.
- * head_dim D in {256, 72}; L <= 8192.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
+ * bias (optional, forward only): an additive score bias shared by the batch, element (h, i, j) at
+ * bias + (h*L + i)*bias_ld + j (bf16) — BEiT's relative position bias (transformers beit BeitLayer [3p], the
+ * ZoeDepth backbone called at model/modeling_spatialvla.py:314-323); not combined with softcap or kv_class.
+ * head_dim D in {256, 72, 64}; L <= 8192.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
  * ---------------------------------------------------------------------------------------- */
 typedef struct {
   int32_t B, L, Hq, Hkv, D;
@@ -140,6 +148,8 @@ typedef struct {
   const void* rope_cos;      /* [L][D/2] bf16 or NULL (backward only) */
   const void* rope_sin;
   int64_t rope_ld;
+  const void* bias;          /* [Hq][L][bias_ld] bf16 additive score bias or NULL (forward only) */
+  int64_t bias_ld;
 } svla_attn_args;
 
 int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, float* lse, void* stream);

@@ -22,7 +22,8 @@ c_vp = ctypes.c_void_p
 # enums mirrored from include/svla.h
 LAYOUT_KC, LAYOUT_RC = 0, 1
 SEG_OUTER, SEG_K, SEG_GEGLU = 0, 1, 2
-EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EPI_GELU_BWD, EPI_SOFTCAP_CE, EPI_ROPE = range(9)
+(EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_GEGLU, EPI_GEGLU_BWD, EPI_GELU_BWD, EPI_SOFTCAP_CE, EPI_ROPE,
+ EPI_BIAS_GELU_ERF, EPI_BIAS_SCALE_RESID) = range(11)
 
 
 class Operand(ctypes.Structure):
@@ -35,14 +36,15 @@ class Epilogue(ctypes.Structure):
                 ("in0", c_vp), ("ld_in0", c_i64), ("in1", c_vp), ("ld_in1", c_i64), ("out1", c_vp),
                 ("ld_out1", c_i64), ("out2", c_vp), ("ld_out2", c_i64), ("row_stats", c_vp),
                 ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64), ("rope_cols", c_i64), ("rope_L", c_i32),
-                ("rope_D", c_i32)]
+                ("rope_D", c_i32), ("colscale", c_vp)]
 
 
 class AttnArgs(ctypes.Structure):
     _fields_ = [("B", c_i32), ("L", c_i32), ("Hq", c_i32), ("Hkv", c_i32), ("D", c_i32),
                 ("sliding_window", c_i32), ("scale", c_f32), ("softcap", c_f32),
                 ("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
-                ("kv_class", c_vp), ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64)]
+                ("kv_class", c_vp), ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64),
+                ("bias", c_vp), ("bias_ld", c_i64)]
 
 
 

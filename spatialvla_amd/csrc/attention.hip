@@ -29,6 +29,7 @@ constexpr float MASKVAL = -3.3895313892515355e38f;  // torch.finfo(bfloat16).min
 template <int D> struct Cfg;
 template <> struct Cfg<256> { static constexpr int DP = 256, DV = 256, RS = 256; };
 template <> struct Cfg<72>  { static constexpr int DP = 96,  DV = 80,  RS = 128; };
+template <> struct Cfg<64>  { static constexpr int DP = 64,  DV = 64,  RS = 128; };  // BEiT (ZoeDepth backbone)
 
 // byte offset of 16-B chunk `ch` of row `r` in a [64][RS] bf16 LDS tile
 template <int RS>
@@ -208,7 +209,7 @@ __device__ __forceinline__ void block_coords(int nqt, int nhg, int& qt, int& hg,
 // ================================================================== forward
 // Block = (query tile of 64, NH query heads sharing one kv head, batch); 4 waves per head, 16 queries per wave.
 // K/V tiles stream through two LDS stages by LDS-DMA: tile kt+1 lands while tile kt is consumed.
-template <int D, int NH, bool CAP>
+template <int D, int NH, bool CAP, bool BIAS = false>
 __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
                                                                int64_t ldo, float* __restrict__ lse) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
@@ -286,11 +287,27 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
     } else {
       float x[4][4];
       float mt = -INFINITY;
+      float bb[4][4];  // additive score bias (BEiT relative position bias), row qi, keys 16nt + 4g + j of tile kt
+      if constexpr (BIAS) {
+        const bf16_t* brow = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid ? qi : 0)) * a.bias_ld + kt * 64 + 4 * g;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          if (plain) {
+            const u32x2 w2 = *reinterpret_cast<const u32x2*>(brow + 16 * nt);
+            bb[nt][0] = __uint_as_float(w2[0] << 16); bb[nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
+            bb[nt][2] = __uint_as_float(w2[1] << 16); bb[nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bb[nt][j] = kt * 64 + 16 * nt + 4 * g + j < L ? bf2f(brow[16 * nt + j]) : 0.f;
+          }
+        }
+      }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float v = s[nt][j] * (a.scale * LOG2E);  // log2 domain
+          if constexpr (BIAS) v = fmaf(bb[nt][j], LOG2E, v);
           if (!plain) {
             const int kj = kt * 64 + 16 * nt + 4 * g + j;
             if (kj >= L) v = -INFINITY;
@@ -675,7 +692,7 @@ int check_args(const svla_attn_args* a) {
   SVLA_CHECK_ARG(a, "attn: args NULL");
   SVLA_CHECK_ARG(a->B > 0 && a->L > 0 && a->L <= 8192 && a->Hq > 0 && a->Hkv > 0 && a->Hq % a->Hkv == 0,
                  "attn: bad B/L/H (L <= 8192)");
-  SVLA_CHECK_ARG(a->D == 256 || a->D == 72, "attn: head_dim %d unsupported (256 or 72)", a->D);
+  SVLA_CHECK_ARG(a->D == 256 || a->D == 72 || a->D == 64, "attn: head_dim %d unsupported (256, 72 or 64)", a->D);
   SVLA_CHECK_ARG(a->q && a->k && a->v, "attn: q/k/v NULL");
   SVLA_CHECK_ARG(a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0, "attn: ld must be multiples of 8");
   SVLA_CHECK_ARG(((uintptr_t)a->q & 15) == 0 && ((uintptr_t)a->k & 15) == 0 && ((uintptr_t)a->v & 15) == 0,
@@ -685,14 +702,14 @@ int check_args(const svla_attn_args* a) {
 
 int round16(int x) { return (x + 15) & ~15; }
 
-template <int D, int NH, bool CAP>
+template <int D, int NH, bool CAP, bool BIAS = false>
 int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
   const int lds = 4 * tile_bytes<D>(64) + round16(a.L);
   SVLA_CHECK_ARG(lds <= 160 * 1024, "attn_fwd: L too large for the LDS-resident key classes");
   const int64_t nblk = (int64_t)((a.L + 63) / 64) * (a.Hq / NH) * a.B;
   SVLA_CHECK_ARG(nblk < (1LL << 31), "attn_fwd: grid too large");
-  set_lds_once<attn_fwd_kernel<D, NH, CAP>>(lds);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NH, CAP>), dim3((unsigned)nblk), dim3(256 * NH), lds, s, a, out, ldo, lse);
+  set_lds_once<attn_fwd_kernel<D, NH, CAP, BIAS>>(lds);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NH, CAP, BIAS>), dim3((unsigned)nblk), dim3(256 * NH), lds, s, a, out, ldo, lse);
   return svla::check_launch("attn_fwd");
 }
 
@@ -724,9 +741,20 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
   const bool pair = (a->Hq / a->Hkv) % 2 == 0;  // two query heads of a GQA group share the K/V stream
   const bool cap = a->softcap > 0.f;
   bf16_t* o = (bf16_t*)out;
+  SVLA_CHECK_ARG(!a->bias || a->D == 64, "attn_fwd: an additive bias is only supported with head_dim 64");
   if (a->D == 256) {
     if (pair) return cap ? fwd_launch<256, 2, true>(*a, o, ldo, lse, s) : fwd_launch<256, 2, false>(*a, o, ldo, lse, s);
     return cap ? fwd_launch<256, 1, true>(*a, o, ldo, lse, s) : fwd_launch<256, 1, false>(*a, o, ldo, lse, s);
+  }
+  if (a->D == 64) {  // BEiT: plain MHA with the additive relative position bias, nothing else
+    SVLA_CHECK_ARG(!cap && !a->kv_class && a->sliding_window <= 0 && a->Hq == a->Hkv,
+                   "attn_fwd: head_dim 64 is the BEiT path (MHA, no softcap, kv_class or window)");
+    if (a->bias) {
+      SVLA_CHECK_ARG(a->bias_ld >= a->L && a->bias_ld % 4 == 0 && ((uintptr_t)a->bias & 7) == 0,
+                     "attn_fwd: bias rows must hold L keys, ld a multiple of 4, 8-B aligned");
+      return fwd_launch<64, 1, false, true>(*a, o, ldo, lse, s);
+    }
+    return fwd_launch<64, 1, false>(*a, o, ldo, lse, s);
   }
   return cap ? fwd_launch<72, 1, true>(*a, o, ldo, lse, s) : fwd_launch<72, 1, false>(*a, o, ldo, lse, s);
 }
@@ -746,6 +774,7 @@ extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t l
                              const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
                              float* workspace, void* stream) {
   if (int rc = check_args(a)) return rc;
+  SVLA_CHECK_ARG(a->D != 64 && !a->bias, "attn_bwd: head_dim 64 / additive bias are forward-only (frozen BEiT)");
   const bool rope = a->rope_cos != nullptr;
   if (rope) SVLA_CHECK_ARG(a->D == 256 && a->rope_sin && a->rope_ld % 8 == 0, "attn_bwd: RoPE needs D=256, sin, ld%8");
   SVLA_CHECK_ARG(out && dout && lse && dq && dk && dv && workspace, "attn_bwd: NULL buffer");

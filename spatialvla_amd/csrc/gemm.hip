@@ -215,6 +215,25 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
       store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
       store8(cp, v, nv);
     } break;
+    case SVLA_EPI_BIAS_GELU_ERF: {
+      float b[8];
+      load8f((const bf16_t*)E.bias + n, b, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = gelu_erf(round_bf(v[j] + b[j]));
+      store8(cp, v, nv);
+    } break;
+    case SVLA_EPI_BIAS_SCALE_RESID: {
+      float b[8], sc[8], r[8];
+      if (E.bias) load8f((const bf16_t*)E.bias + n, b, nv);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+      load8f((const bf16_t*)E.colscale + n, sc, nv);
+      load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = round_bf(sc[j] * round_bf(v[j] + b[j])) + r[j];
+      store8(cp, v, nv);
+    } break;
     case SVLA_EPI_BIAS_RESID: {
       float b[8], r[8];
       if (E.bias) load8f((const bf16_t*)E.bias + n, b, nv);
@@ -314,11 +333,16 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
     const int64_t n = n0 + 8 * cc;
     const int64_t nv = N - n;
     float b[8];
-    if constexpr (KIND == SVLA_EPI_BIAS || KIND == SVLA_EPI_BIAS_GELU || KIND == SVLA_EPI_BIAS_RESID) {
+    if constexpr (KIND == SVLA_EPI_BIAS || KIND == SVLA_EPI_BIAS_GELU || KIND == SVLA_EPI_BIAS_RESID ||
+                  KIND == SVLA_EPI_BIAS_GELU_ERF || KIND == SVLA_EPI_BIAS_SCALE_RESID) {
       if (E.bias && nv > 0) load8f((const bf16_t*)E.bias + n, b, nv);
       else
 #pragma unroll
         for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+    float sc[8];
+    if constexpr (KIND == SVLA_EPI_BIAS_SCALE_RESID) {
+      if (nv > 0) load8f((const bf16_t*)E.colscale + n, sc, nv);
     }
     if (nv <= 0) return;
 #pragma unroll 1
@@ -366,6 +390,16 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
         load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = round_bf(x[j] + b[j]) + r[j];
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_BIAS_GELU_ERF) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = gelu_erf(round_bf(x[j] + b[j]));
+        store8(cp, x, nv);
+      } else if constexpr (KIND == SVLA_EPI_BIAS_SCALE_RESID) {
+        float r[8];
+        load8f((const bf16_t*)E.in0 + m * E.ld_in0 + n, r, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = round_bf(sc[j] * round_bf(x[j] + b[j])) + r[j];
         store8(cp, x, nv);
       } else if constexpr (KIND == SVLA_EPI_GELU_BWD) {
         float pre[8];
@@ -449,6 +483,12 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
         epi_pass_fast<SVLA_EPI_GEGLU_BWD, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
       case SVLA_EPI_GEGLU: epi_pass_fast<SVLA_EPI_GEGLU, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_BIAS_GELU_ERF:
+        epi_pass_fast<SVLA_EPI_BIAS_GELU_ERF, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
+      case SVLA_EPI_BIAS_SCALE_RESID:
+        epi_pass_fast<SVLA_EPI_BIAS_SCALE_RESID, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
+        break;
       default: fast = false;
     }
     if (fast) {
@@ -2141,6 +2181,11 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
       SVLA_CHECK_ARG(epi->in0 && epi->in1 && epi->out1 && epi->out2, "gemm: GEGLU_BWD needs in0,in1,out1,out2");
       break;
     case SVLA_EPI_GELU_BWD: SVLA_CHECK_ARG(epi->in0, "gemm: GELU_BWD needs in0"); break;
+    case SVLA_EPI_BIAS_GELU_ERF: SVLA_CHECK_ARG(epi->bias && aligned16(epi->bias), "gemm: BIAS_GELU_ERF needs bias"); break;
+    case SVLA_EPI_BIAS_SCALE_RESID:
+      SVLA_CHECK_ARG(epi->colscale && epi->in0 && epi->ld_in0 % 8 == 0 && (!epi->bias || aligned16(epi->bias)),
+                     "gemm: BIAS_SCALE_RESID needs colscale, in0");
+      break;
     case SVLA_EPI_SOFTCAP_CE: SVLA_CHECK_ARG(epi->row_stats && epi->cap > 0.f, "gemm: SOFTCAP_CE needs row_stats, cap"); break;
     case SVLA_EPI_ROPE:
       SVLA_CHECK_ARG(epi->rope_cos && epi->rope_sin && epi->rope_L > 0 && epi->rope_D >= 16 &&

@@ -78,6 +78,8 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   float u = k0 * (x + k1 * x * x * x);
   return 0.5f * x * (1.0f + fast_tanh(u));
 }
+// torch GELU(approximate="none") in fp32: x/2 * (1 + erf(x / sqrt(2)))
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;

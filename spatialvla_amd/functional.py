@@ -723,3 +723,65 @@ class _PluginAttnFn(torch.autograd.Function):
         K.attn_bwd(a, out, do, lse, dq, dq.stride(0), dk, dk.stride(0), dv, dv.stride(0))
         tr = lambda t, H: t.view(B, Lq, H, D).transpose(1, 2)  # noqa: E731
         return tr(dq, Hq), tr(dk, Hkv), tr(dv, Hkv), None, None, None, None
+
+
+# ------------------------------------------------------------------------------------ BEiT layer (ZoeDepth)
+def _beit_weights(layer):
+    """q|k|v weight [3H, H] and bias [3H] (k has none) of a BeitLayer, concatenated once and cached against the
+    parameters' storage and version (the estimator is frozen)."""
+    at = layer.attention
+    ps = (at.q_proj.weight, at.k_proj.weight, at.v_proj.weight, at.q_proj.bias, at.v_proj.bias)
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    hit = getattr(layer, "_svla_qkv", None)
+    if hit is not None and hit[0] == key:
+        return hit[1], hit[2]
+    w = torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight], 0).contiguous()
+    b = torch.cat([at.q_proj.bias, torch.zeros_like(at.k_proj.weight[:, 0]), at.v_proj.bias], 0).contiguous()
+    layer._svla_qkv = (key, w, b)
+    return w, b
+
+
+def _layer_scale(lam, H, like):
+    if isinstance(lam, torch.Tensor):
+        return _c(lam.to(like.dtype))
+    return torch.full((H,), float(lam), dtype=like.dtype, device=like.device)
+
+
+def beit_layer(layer, hidden_states, bias):
+    """transformers BeitLayer.forward [3p] (the ZoeDepth backbone, called at model/modeling_spatialvla.py:314-323)
+    in inference on the HIP kernels:
+        h = x + lambda_1 * o_proj(attn(q_proj|k_proj|v_proj(LN_before(x)), + rel-pos bias))
+        y = h + lambda_2 * fc2(gelu(fc1(LN_after(h))))
+    LayerNorm: svla_layernorm_fwd; the three projections one GEMM with the [bq, 0, bv] bias epilogue; attention
+    svla_attn_fwd at head_dim 64 with the additive bias (fp32 scores and softmax, P in bf16); o_proj and fc2 with
+    the BIAS_SCALE_RESID epilogue (bf16(bf16(lambda * bf16(acc + b)) + residual), the module's rounding points);
+    fc1 with BIAS_GELU_ERF.  bias: [heads, L, ld] bf16 or None."""
+    B, Lq, H = hidden_states.shape
+    at = layer.attention
+    D = at.head_dim
+    nh = at.num_attention_heads
+    x = _c(hidden_states).view(B * Lq, H)
+    M = B * Lq
+    ln_before, ln_after = layer.layernorm_before, layer.layernorm_after
+    mean = _empty(M, dtype=F32, like=x)
+    rstd = _empty(M, dtype=F32, like=x)
+    xn = _empty(M, H, like=x)
+    K.layernorm_fwd(x, ln_before.weight, ln_before.bias, float(ln_before.eps), xn, mean, rstd)
+    wqkv, bqkv = _beit_weights(layer)
+    qkv = _empty(M, 3 * H, like=x)
+    K.linear_fwd(xn, [wqkv], qkv, kind=L.EPI_BIAS, bias=bqkv)
+    a = K.attn_args(B, Lq, nh, nh, D, qkv[:, :H], qkv.stride(0), qkv[:, H:2 * H], qkv.stride(0), qkv[:, 2 * H:],
+                    qkv.stride(0), float(at.scaling), 0.0, None, 0, bias=bias)
+    ctx = _empty(M, H, like=x)
+    lse = _empty(B, nh, Lq, dtype=F32, like=x)
+    K.attn_fwd(a, ctx, lse)
+    h = _empty(M, H, like=x)
+    K.linear_fwd(ctx, [at.o_proj.weight], h, kind=L.EPI_BIAS_SCALE_RESID, bias=at.o_proj.bias,
+                 colscale=_layer_scale(layer.lambda_1, H, x), in0=x)
+    K.layernorm_fwd(h, ln_after.weight, ln_after.bias, float(ln_after.eps), xn, mean, rstd)
+    f1 = _empty(M, layer.mlp.fc1.weight.shape[0], like=x)
+    K.linear_fwd(xn, [layer.mlp.fc1.weight], f1, kind=L.EPI_BIAS_GELU_ERF, bias=layer.mlp.fc1.bias)
+    y = _empty(M, H, like=x)
+    K.linear_fwd(f1, [layer.mlp.fc2.weight], y, kind=L.EPI_BIAS_SCALE_RESID, bias=layer.mlp.fc2.bias,
+                 colscale=_layer_scale(layer.lambda_2, H, x), in0=h)
+    return y.view(B, Lq, H)

@@ -60,8 +60,9 @@ def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUT
 
 
 def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=None, in1=None, out1=None,
-         out2=None, row_stats=None, rope=None) -> L.Epilogue:
+         out2=None, row_stats=None, rope=None, colscale=None) -> L.Epilogue:
     e = L.Epilogue()
+    e.colscale = _ptr(colscale)
     e.kind = kind
     e.accumulate = 1 if accumulate else 0
     e.alpha = alpha
@@ -155,7 +156,7 @@ def _aligned(sizes, mult):
 
 
 def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, kind=L.EPI_STORE, bias=None,
-               alpha=1.0, in0=None, out1=None, out2=None, row_stats=None, cap=0.0, rope=None):
+               alpha=1.0, in0=None, out1=None, out2=None, row_stats=None, cap=0.0, rope=None, colscale=None):
     """out[M, sum N_i] = epi(x[M,K] @ cat(weights)^T).  Weights [N_i, K] are read in place."""
     M, K = x.shape
     sizes = [w.shape[0] for w in weights]
@@ -170,7 +171,8 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
     A = _operand([x], L.LAYOUT_KC)
     B = _operand(weights, L.LAYOUT_KC, L.SEG_OUTER, starts)
     gemm(M, N, K, A, B, [out], [0], _ld(out),
-         _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap, rope=rope))
+         _epi(kind, alpha=alpha, bias=bias, in0=in0, out1=out1, out2=out2, row_stats=row_stats, cap=cap, rope=rope,
+              colscale=colscale))
 
 
 # Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch
@@ -320,7 +322,7 @@ def colsum_bf16(x, out, accumulate=False):
 
 # ---------------------------------------------------------------------------------------- attention
 def attn_args(B, Lq, Hq, Hkv, D, q, ldq, k, ldk, v, ldv, scale, softcap=0.0, kv_class=None, window=0,
-              cos=None, sin=None) -> L.AttnArgs:
+              cos=None, sin=None, bias=None) -> L.AttnArgs:
     a = L.AttnArgs()
     a.B, a.L, a.Hq, a.Hkv, a.D = B, Lq, Hq, Hkv, D
     a.sliding_window = int(window)
@@ -330,6 +332,10 @@ def attn_args(B, Lq, Hq, Hkv, D, q, ldq, k, ldk, v, ldv, scale, softcap=0.0, kv_
     a.kv_class = _ptr(kv_class)
     if cos is not None:
         a.rope_cos, a.rope_sin, a.rope_ld = cos.data_ptr(), sin.data_ptr(), cos.stride(0)
+    if bias is not None:  # [Hq, L, ld] bf16, rows contiguous
+        _req(bias.dim() == 3 and bias.stride(2) == 1 and bias.stride(0) == Lq * bias.stride(1),
+             "attn bias must be [Hq, L, ld] with contiguous rows")
+        a.bias, a.bias_ld = bias.data_ptr(), bias.stride(1)
     return a
 
 

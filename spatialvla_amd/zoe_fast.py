@@ -1,5 +1,7 @@
-"""Numerically identical fast paths for the frozen ZoeDepth estimator (transformers ZoeDepth/BEiT [3p], called
-by the reference at model/modeling_spatialvla.py:314-323).  Installed per instance by `install(zoe)`:
+"""Fast paths for the frozen ZoeDepth estimator (transformers ZoeDepth/BEiT [3p], called by the reference at
+model/modeling_spatialvla.py:314-323), installed per instance by `install(zoe)`.  All are bitwise identical to the
+stock modules except the BEiT layers and the metric tail, which keep the modules' bf16 rounding points but sum in
+another order (tolerances in tests/test_model_gpu.py):
 
 * BEiT relative position bias (transformers beit BeitRelativePositionBias.forward): the reference path
   re-interpolates the bias table and rebuilds the [577, 577] index on the host for every layer and every
@@ -11,6 +13,9 @@ by the reference at model/modeling_spatialvla.py:314-323).  Installed per instan
 * DPT neck resizes (ZoeDepthFeatureFusionLayer's interpolate(scale_factor=2, align_corners=True) and the relative
   head's nn.Upsample) on channels-last bf16 maps: svla_upsample_bilinear_nhwc (csrc/zoe.hip), torch's NHWC bilinear
   arithmetic at 8 channels per thread instead of one element (the stock kernel moved ~0.5 TB/s).
+* BEiT layers (BeitLayer.forward) in inference: LayerNorm, the q|k|v / o / fc1 / fc2 GEMMs with fused bias, exact
+  GELU and layer-scale + residual epilogues, and the head_dim-64 attention with the additive relative position
+  bias, all on libsvla (functional.beit_layer); the bias is copied once per layer into [heads, L, round8(L)] rows.
 * Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
   relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
   and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
@@ -100,9 +105,44 @@ def _upsample_forward(self, x):
     return type(self).forward(self, x)
 
 
-def install(zoe: torch.nn.Module, tail: bool = True) -> torch.nn.Module:
-    """Patch the instances inside `zoe` (idempotent).  tail=False keeps the stock metric-head tail (the other
-    two paths are bitwise identical to the stock module)."""
+def _padded_bias(layer, rpb):
+    """[1, heads, L, L] relative position bias -> [heads, L, round8(L)] rows for svla_attn_fwd, cached per layer
+    against the (cached) bias tensor."""
+    key = (rpb.data_ptr(), rpb._version, tuple(rpb.shape))
+    hit = getattr(layer, "_svla_bias", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    h, L = rpb.shape[1], rpb.shape[-1]
+    out = torch.zeros(h, L, (L + 7) // 8 * 8, dtype=torch.bfloat16, device=rpb.device)
+    out[:, :, :L] = rpb[0]
+    layer._svla_bias = (key, out)
+    return out
+
+
+def _beit_layer_forward(self, hidden_states, attention_mask=None, interpolate_pos_encoding=False, resolution=None,
+                        **kwargs):
+    """BeitLayer.forward (transformers beit [3p]) on the HIP kernels (functional.beit_layer) for the frozen
+    estimator's inference: bf16 on the GPU, head_dim 64, no extra attention mask; anything else keeps the stock
+    module."""
+    at = self.attention
+    if (not hidden_states.is_cuda or hidden_states.dtype != torch.bfloat16 or attention_mask is not None
+            or self.training or torch.is_grad_enabled() or at.head_dim != 64
+            or getattr(self, "_svla_stock", False)):
+        return type(self).forward(self, hidden_states, attention_mask=attention_mask,
+                                  interpolate_pos_encoding=interpolate_pos_encoding, resolution=resolution, **kwargs)
+    bias = None
+    if self.relative_position_bias is not None:
+        height, width = resolution
+        window_size = (height // self.patch_size, width // self.patch_size)
+        rpb = self.relative_position_bias(window_size, interpolate_pos_encoding, dim_size=hidden_states.shape[1])
+        bias = _padded_bias(self, rpb.to(torch.bfloat16))
+    from . import functional as Fn
+    return Fn.beit_layer(self, hidden_states, bias)
+
+
+def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True) -> torch.nn.Module:
+    """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False keep the stock metric-head tail /
+    BEiT layers (the other paths are bitwise identical to the stock modules)."""
     for m in zoe.modules():
         name = type(m).__name__
         if name == "BeitRelativePositionBias" and not getattr(m, "_svla_fast", False):
@@ -116,6 +156,9 @@ def install(zoe: torch.nn.Module, tail: bool = True) -> torch.nn.Module:
             m._svla_fast = True
         elif (isinstance(m, torch.nn.Upsample) and m.mode == "bilinear" and not getattr(m, "_svla_fast", False)):
             m.forward = types.MethodType(_upsample_forward, m)
+            m._svla_fast = True
+        elif name == "BeitLayer" and beit and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_beit_layer_forward, m)
             m._svla_fast = True
         elif name == "ZoeDepthMetricDepthEstimationHead" and tail and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_metric_head_forward, m)

@@ -73,6 +73,53 @@ def _check_variants(outs, tol=2e-3):
         assert rel_l2(_flat(outs[v]), _flat(outs[1])) < tol, v
 
 
+@pytest.mark.parametrize("M,N,K", [(1154, 4096, 1024), (1154, 1024, 4096), (300, 200, 64)])
+def test_gemm_beit_epilogues(cuda, M, N, K):
+    """BIAS_GELU_ERF: bf16(gelu_erf(bf16(acc + b))); BIAS_SCALE_RESID: bf16(bf16(s * bf16(acc + b)) + r) -- the
+    rounding points of BeitLayer's fc1 + exact GELU and of lambda * sublayer + residual; vs torch on the same
+    bf16 products (fp32 accumulation order differs: a bf16 ulp at most on a few elements)."""
+    from spatialvla_amd import kernels as Kn, _lib as L_
+    torch.manual_seed(12)
+    x, w = _r(M, K), _r(N, K, scale=0.05)
+    b, sc, res = _r(N, scale=0.5), _r(N, scale=0.3), _r(M, N)
+    acc = (x.float() @ w.float().T)
+    pre = (acc + b.float()).to(BF).float()
+    ref_g = F.gelu(pre).to(BF)
+    ref_s = ((sc.float() * pre).to(BF).float() + res.float()).to(BF)
+    out_g = torch.empty(M, N, dtype=BF, device=cuda)
+    out_s = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], out_g, kind=L_.EPI_BIAS_GELU_ERF, bias=b)
+    Kn.linear_fwd(x, [w], out_s, kind=L_.EPI_BIAS_SCALE_RESID, bias=b, colscale=sc, in0=res)
+    assert rel_l2(out_g, ref_g) < 5e-3 and rel_l2(out_s, ref_s) < 5e-3
+    ulp = lambda t: torch.abs(t.float()) * 2.0 ** -7 + 1e-6  # noqa: E731
+    assert (torch.abs(out_g.float() - ref_g.float()) <= 2 * ulp(ref_g)).float().mean() > 0.999
+    assert (torch.abs(out_s.float() - ref_s.float()) <= 2 * ulp(ref_s)).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("L", [577, 130])
+def test_attention_d64_bias(cuda, L):
+    """head_dim 64 MHA with an additive [heads, L, L] score bias (BEiT relative position bias): fp32 reference
+    softmax(q k^T / 8 + bias) v."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(13)
+    B, Hn, D = 2, 4, 64
+    qkv = _r(B * L, 3 * Hn * D)
+    ld = qkv.stride(0)
+    q, k, v = qkv[:, :Hn * D], qkv[:, Hn * D:2 * Hn * D], qkv[:, 2 * Hn * D:]
+    bias_full = _r(Hn, L, L, scale=2.0)
+    bias = torch.zeros(Hn, L, (L + 7) // 8 * 8, dtype=BF, device=cuda)
+    bias[:, :, :L] = bias_full
+    a = Kn.attn_args(B, L, Hn, Hn, D, q, ld, k, ld, v, ld, D ** -0.5, 0.0, None, 0, bias=bias)
+    out = torch.empty(B * L, Hn * D, dtype=BF, device=cuda)
+    lse = torch.empty(B, Hn, L, device=cuda)
+    Kn.attn_fwd(a, out, lse)
+    qf, kf, vf = (t.float().view(B, L, Hn, D).transpose(1, 2) for t in (q, k, v))
+    s_ = qf @ kf.transpose(-1, -2) * D ** -0.5 + bias_full.float()[None]
+    ref = (torch.softmax(s_, -1) @ vf).transpose(1, 2).reshape(B * L, Hn * D)
+    assert rel_l2(out, ref) < 1e-2
+    assert rel_l2(lse, torch.logsumexp(s_, -1)) < 1e-4
+
+
 def test_gemm_two_streams_bitwise(cuda):
     """svla_gemm_bf16 is re-entrant across streams (include/svla.h): GEMMs that use stream-K (slabs + arrival
     counters in the caller's workspace) run concurrently on two streams, each with its own workspace, and return
