@@ -31,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_BF16_TFLOPS = 2500.0          # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0           # MI355X dense fp8 (MX-scaled e4m3) MFMA
 GFLOP_PER_EPISODE = 6136.1         # fwd+bwd algorithmic FLOPs per episode at L=312
 
 
@@ -45,6 +46,8 @@ def parse():
     ap.add_argument("--no-decode", action="store_true", help="skip the B=1 decode-latency leg")
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--fp8", action="store_true",
+                    help="BASELINE configs[4]: Gemma2 q|k|v, o, gate|up, down forward projections on the fp8 MFMA GEMM")
     return ap.parse_args()
 
 
@@ -100,19 +103,23 @@ def pmc_traffic():
     return None
 
 
-def dominant_kernel_roofline(records):
+def dominant_kernel_roofline(records, fp8=False):
     """Roofline of the Gemma2 gate/up GEMM with the fused GeGLU epilogue (the largest kernel of the step):
-    its launches inside the timed region, each bracketed by HIP events on the stream it was launched on."""
+    its launches inside the timed region, each bracketed by HIP events on the stream it was launched on.
+    fp8 (configs[4]): the e4m3 MFMA kernel against the dense fp8 peak."""
     ms = [e0.elapsed_time(e1) for (e0, e1, *_s) in records]
     M, N, K = records[0][2:]
     avg = float(np.mean(ms))
     flops = 2.0 * M * N * K                          # algorithmic: M x (2I) x H multiply-adds
     ach = flops / (avg * 1e-3) / 1e12
-    bytes_alg = 2.0 * (M * K + N * K + 3 * M * (N // 2))   # x, Wg, Wu read; h, g, u written (bf16)
-    return {"kernel": "svla gemm4_kernel_00 (256x256 tile, 4 waves x 128x128, AGPR accumulators) EPI_GEGLU "
-                      "(Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
-            "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(), "avg_launch_ms": round(avg, 4),
+    ob = 1 if fp8 else 2                             # operand bytes per element
+    bytes_alg = ob * (M * K + N * K) + 2.0 * 3 * M * (N // 2)   # x, Wg, Wu read; h, g, u written (bf16)
+    peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
+    kern = ("svla gemm4f8_kernel (256x256 tile, 4 waves x 128x128, v_mfma_scale_f32_32x32x64_f8f6f4 e4m3, row scales)"
+            if fp8 else "svla gemm4_kernel_00 (256x256 tile, 4 waves x 128x128, AGPR accumulators)")
+    return {"kernel": kern + " EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
+            "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": None if fp8 else pmc_traffic(), "avg_launch_ms": round(avg, 4),
             "launches_timed": len(ms), "algorithmic_flops_per_launch": flops,
             "algorithmic_bytes_per_launch": bytes_alg}
 
@@ -288,6 +295,8 @@ def main():
     B = args.batch
     t0 = time.perf_counter()
     model = build_model(cfgd, device)
+    if args.fp8:
+        model.enable_fp8_projections(True)
     n_train = sum(p.numel() for p in model.parameters() if p.requires_grad)
     total = args.warmup + args.steps
     engine = TrainEngine(model, lr=2e-5, weight_decay=0.0, max_grad_norm=1.0, warmup_ratio=0.005,
@@ -306,7 +315,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     from spatialvla_amd import kernels as K
-    geglu_events = K.launch_timer["geglu"] = []
+    tkey = "geglu_fp8" if args.fp8 else "geglu"
+    geglu_events = K.launch_timer[tkey] = []
     t_start = time.perf_counter()
     for s in range(args.steps):
         if s == args.steps - 1 and os.environ.get("SVLA_GEMM_LOG"):  # tools/ab_trace.py: GEMM call sequence
@@ -316,7 +326,7 @@ def main():
         json.dump(K.gemm_log, open(os.environ["SVLA_GEMM_LOG"], "w"))
         K.gemm_log = None
     torch.cuda.synchronize()
-    K.launch_timer.pop("geglu")
+    K.launch_timer.pop(tkey)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t_start
@@ -331,22 +341,24 @@ def main():
         "metric": "episodes/sec fwd+bwd SpatialVLA-4B, 224px+56tok batch, 1/2/4/8 MI355X",
         "value": round(eps, 3), "unit": "episodes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16", "data": "synthetic OXE-shaped batches (random ids/pixels), random-init weights",
-        "config": {"workload": "SpatialVLA-4B fwd+bwd+AdamW (BASELINE configs[2]/[3])", "model": args.config,
+        "dtype": "fp8-e4m3 fwd projections / bf16" if args.fp8 else "bf16",
+        "data": "synthetic OXE-shaped batches (random ids/pixels), random-init weights",
+        "config": {"workload": ("SpatialVLA-4B fwd+bwd+AdamW, fp8 Gemma2 projections (BASELINE configs[4])" if args.fp8
+                                else "SpatialVLA-4B fwd+bwd+AdamW (BASELINE configs[2]/[3])"), "model": args.config,
                    "global_batch": world * B, "per_gpu_batch": B, "seq_len": 312, "parallelism": f"dp{world}",
                    "trainable_params": n_train},
         "mfu_model_flops": round(eps * GFLOP_PER_EPISODE / 1e3 / (world * PEAK_BF16_TFLOPS), 4),
         "final_loss": round(final_loss, 4),
     }
     if rank == 0:
-        result["roofline"] = dominant_kernel_roofline(geglu_events)
+        result["roofline"] = dominant_kernel_roofline(geglu_events, fp8=args.fp8)
         if args.config == "spatialvla_4b":
             result["gemma2_block"] = gemma2_block_roofline(model, B, 312, device)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.fp8:
             del batches, engine
             torch.cuda.empty_cache()
             result["cpu_baseline"] = cpu_baseline(cfgd, args.cpu_iters)
-        if world == 1 and args.config == "spatialvla_4b" and not args.no_decode:
+        if world == 1 and args.config == "spatialvla_4b" and not args.no_decode and not args.fp8:
             result["decode"] = decode_latency(model, cfgd, device)
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -117,6 +117,23 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
                       const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * fp8 projections (BASELINE configs[4]; OCP e4m3, MX-scaled MFMA v_mfma_scale_f32_32x32x64_f8f6f4 at unit block
+ * scales, fp32 accumulate).  Replaces the bf16 forward nn.Linear of Gemma2 q/k/v/o and gate/up/down
+ * (model/modeling_gemma2.py:86-92, 351-354, 376-408) when fp8 projections are enabled; the backward stays bf16.
+ * ---------------------------------------------------------------------------------------- */
+/* Row-wise quantisation: scale[r] = amax_r/448, q[r,k] = e4m3(clamp(x[r,k]*448/amax_r, +-448)) (RNE; a zero row
+ * gives q = 0, scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0, K <= 9216. */
+int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq, float* scale,
+                        void* stream);
+/* C[M,N] = epilogue( a_scale[m] * b_scale[n] * sum_k A(m,k) B(n,k) ) with A, B e4m3 KC operands (ld in bytes, a
+ * multiple of 16; K and k_valid multiples of 16; A one segment; B one segment, or two SVLA_SEG_GEGLU segments of
+ * N/2 rows with SVLA_EPI_GEGLU, b_scale then [N]: gate rows then up rows).  Scales fp32, 16-B aligned.  Epilogues
+ * STORE (alpha 1), BIAS, BIAS_RESID, GEGLU, ROPE as svla_gemm_bf16; workspace as svla_gemm_bf16. */
+int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const float* a_scale, const svla_operand* B,
+                  const float* b_scale, void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Attention.  Reference: eager_attention_forward (model/modeling_gemma2.py:169-195) selected via
  * GEMMA2_ATTENTION_FUNCTION (:317-322) with the prefix-LM additive mask of
  * _update_causal_mask (model/modeling_spatialvla.py:258-306) and Gemma2 RoPE

@@ -22,6 +22,8 @@
 //  * Block ids are remapped XCD-aware (consecutive tiles share an XCD L2) and grouped along M.
 #include "svla_common.h"
 #include "agpr.h"
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+#include "agpr_f8.h"
 
 #include <type_traits>
 
@@ -1380,6 +1382,61 @@ __device__ __forceinline__ void agpr_set(const f32x4& v) {
       : SVLA_AGPR_CLOBBERS);
 }
 
+// ---- fp8 (OCP e4m3) operands of the 4-wave kernel (svla_gemm_fp8).  An fp8 KC operand tile of 256 rows x 128 k is
+// byte-for-byte the bf16 KC tile of 256 x 64 (128-B rows), so staging, swizzles, zero-fill and stream-K run unchanged
+// on "k units" of two fp8 values; only the fragments, the MFMA and the epilogue's read-out differ:
+//  * v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate), unit block scales; a wave's 128x128 = 4x4 blocks of
+//    32x32 in the same 256 AGPRs; a k-tile (128 fp8 k) = 2 k-halves x 16 MFMAs, each 4x a 16x16x32 bf16 MFMA, so the
+//    k-tile takes the time of the bf16 k-tile (64 k) and every gap holds 4x the issue slots.
+//  * fragment (32 rows at rb, k-half h): lane l holds row rb + (l & 31), bytes 64h + 32(l >> 5) .. +31 of the row
+//    (two 16-B chunks).  A and B use the same lane -> k map, so the product sums matching k whatever the
+//    instruction's internal k order.
+//  * epilogue: C = acc * sa[m] * sb[n] (per-row scales of A and of B = the output column), then the usual epilogue.
+struct F8Scales {
+  const float* sa;   // [M] row scales of A (activation rows)
+  const float* sb;   // [N] (GEGLU: [2 I], gate rows then up rows) row scales of B (weight rows)
+  int64_t na, nb;    // readable entries of sa / sb
+  int64_t geglu_I;   // GEGLU: rows per weight half (tile column c < 128 -> gate row, else up row I + ..), else 0
+};
+
+struct FragF8 {
+  i32x8 v;
+  __device__ __forceinline__ void load(const char* img, int rb, int h, int lane) {
+    const int row = rb + (lane & 31);
+    const int c0 = 4 * h + 2 * (lane >> 5);
+    const char* base = img + row * 128;
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(base + ((c0 ^ (row & 7)) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ (row & 7)) << 4));
+    v = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pb = (void*)(((uint64_t)hi << 32) | lo);
+  const int n = (int)__builtin_amdgcn_readfirstlane((uint32_t)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, n, 0x00020000);
+}
+
+// fp8 k-tile schedule (32 MFMA slots): F1 reads at 0..7, RB1, A pieces (2 per slot) from F8_DA0, B pieces from
+// F8_DB0, RB2, then the 8 F0 reads of the next k-tile
+#ifndef F8_RB1
+#define F8_RB1 9
+#endif
+#ifndef F8_DA0
+#define F8_DA0 10
+#endif
+#ifndef F8_DB0
+#define F8_DB0 15
+#endif
+#ifndef F8_RB2
+#define F8_RB2 23
+#endif
+static_assert(F8_RB1 >= 8 && F8_DA0 > F8_RB1 && F8_DB0 >= F8_DA0 + 4 && F8_RB2 >= F8_DB0 + 4 && F8_RB2 + 8 < 32,
+              "fp8 schedule knobs out of order");
+
 #define P4_FOR_ACC(BODY)                           \
   _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) \
   _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) { BODY; }
@@ -1387,10 +1444,10 @@ __device__ __forceinline__ void agpr_set(const f32x4& v) {
 // The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
 // template are also instantiated for the host, where the device-only helpers they call fail to substitute and
 // the kernel stub silently disappears.
-template <int LA, int LB>
+template <int LA, int LB, bool F8 = false>
 __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
                                            const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
-                                           const SKArgs& sk) {
+                                           const SKArgs& sk, const F8Scales& fs) {
   using namespace p4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t_in = threadIdx.x;
@@ -1462,6 +1519,85 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     P8_BARRIER();
+    using T = std::true_type;
+    using F = std::false_type;
+    auto run_loop = [&](auto&& ktile) {
+    int kt = kb;
+#if G4_STAMPS
+    const unsigned long long tl = __builtin_amdgcn_s_memtime();
+#endif
+    const int kfull = (int)(min(kvA, kvB) / BK);  // k-tiles [0, kfull) lie wholly inside both extents
+#pragma unroll 1
+    for (; kt + 2 < ke && kt + 3 <= kfull; ++kt) ktile(kt, T{}, T{}, T{});
+#pragma unroll 1
+    for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{}, F{});
+    if (kt + 1 < ke) {
+      ktile(kt, F{}, T{}, F{});
+      ++kt;
+    }
+    ktile(kt, F{}, F{}, F{});
+#if G4_STAMPS
+    stmp[3] += __builtin_amdgcn_s_memtime() - tl;
+    stmp[4] += tl - tm0;
+#endif
+    };
+    if constexpr (F8) {
+    const int s127 = 127;  // E8M0 unit block scale
+    FragF8 f0a[4], f1a[4], f0b[4], f1b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f0a[i].load(smem, 128 * wr + 32 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f0b[j].load(smem + OPB, 128 * wc + 32 * j, 0, lane);
+    auto ktile8 = [&](int kt, auto DMA, auto NEXT, auto FULLK) {
+      char* const cur = smem + ((kt - kb) & 1) * STAGE;
+      char* const nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
+      const int64_t k2 = (int64_t)(kt + 2) * BK;
+      const char* const rsa = abase + k2 * ksa;
+      const char* const rsb = bbase + k2 * ksb;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<0, 32>([&](auto XC) {
+        constexpr int x = decltype(XC)::value;
+        constexpr int y = x & 15, ii = y >> 2, jj = y & 3;
+        if constexpr (x < 16) agpr_mfma_f8<ii * 4 + jj>(f0a[ii].v, f0b[jj].v, s127);
+        else agpr_mfma_f8<ii * 4 + jj>(f1a[ii].v, f1b[jj].v, s127);
+        if constexpr (x < 4) f1a[x].load(cur, 128 * wr + 32 * x, 1, lane);
+        else if constexpr (x < 8) f1b[x - 4].load(cur + OPB, 128 * wc + 32 * (x - 4), 1, lane);
+        if constexpr (x == F8_RB1) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every F1 read of the tile landed, buffer free
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (decltype(DMA)::value) {
+          if constexpr (x >= F8_DA0 && x < F8_DA0 + 4) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if constexpr (decltype(FULLK)::value) pieceA_full(rsa, 2 * (x - F8_DA0) + u, cur);
+              else pieceA(rsa, kvA - k2, 2 * (x - F8_DA0) + u, cur);
+            }
+          }
+          if constexpr (x >= F8_DB0 && x < F8_DB0 + 4) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if constexpr (decltype(FULLK)::value) pieceB_full(rsb, 2 * (x - F8_DB0) + u, cur + OPB);
+              else pieceB(rsb, kvB - k2, 2 * (x - F8_DB0) + u, cur + OPB);
+            }
+          }
+        }
+        if constexpr (decltype(NEXT)::value) {
+          if constexpr (x == F8_RB2) {
+            if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+          }
+          constexpr int r = x - F8_RB2 - 1;
+          if constexpr (r >= 0 && r < 4) f0a[r].load(nxt, 128 * wr + 32 * r, 0, lane);
+          else if constexpr (r >= 4 && r < 8) f0b[r - 4].load(nxt + OPB, 128 * wc + 32 * (r - 4), 0, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    };
+    run_loop(ktile8);
+    } else {
     Frag<LA> f0a[8], f1a[8];
     Frag<LB> f0b[8], f1b[8];
 #pragma unroll
@@ -1539,26 +1675,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       });
       if (G4_PRIO) __builtin_amdgcn_s_setprio(0);
     };
-    using T = std::true_type;
-    using F = std::false_type;
-    int kt = kb;
-#if G4_STAMPS
-    const unsigned long long tl = __builtin_amdgcn_s_memtime();
-#endif
-    const int kfull = (int)(min(kvA, kvB) / BK);  // k-tiles [0, kfull) lie wholly inside both extents
-#pragma unroll 1
-    for (; kt + 2 < ke && kt + 3 <= kfull; ++kt) ktile(kt, T{}, T{}, T{});
-#pragma unroll 1
-    for (; kt + 2 < ke; ++kt) ktile(kt, T{}, T{}, F{});
-    if (kt + 1 < ke) {
-      ktile(kt, F{}, T{}, F{});
-      ++kt;
+    run_loop(ktile);
     }
-    ktile(kt, F{}, F{}, F{});
-#if G4_STAMPS
-    stmp[3] += __builtin_amdgcn_s_memtime() - tl;
-    stmp[4] += tl - tm0;
-#endif
+    if constexpr (F8) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: SVLA_AGPR_CLOBBERS);  // 16-pass XDL -> reads
     agpr_fence();  // MFMA results -> epilogue / slab readers
     __syncthreads();
   };
@@ -1582,11 +1701,50 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         else rows(std::integral_constant<int, 0>{});
       }
     };
+    // fp8: 32x32 blocks (block q = 4i + j in a[16q:16q+15]; register r of a block: row (r&3) + 8(r>>2) + 4(l>>5),
+    // column l&31), scaled by the row scales of A and B on the way into the image
+    auto wp8 = [&](int pass, float* Ei) {
+      if ((pass >> 1) == wr) {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc_n(fs.sa, fs.na * 4), rb = make_rsrc_n(fs.sb, fs.nb * 4);
+        float csc[4];
+        f32x4 rsc[2][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = 128 * wc + 32 * j + (lane & 31);
+          const int64_t n = fs.geglu_I ? ((c < 128) ? (n0 >> 1) + c : fs.geglu_I + (n0 >> 1) + (c - 128)) : n0 + c;
+          csc[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, (uint32_t)(n * 4), 0, 0));
+        }
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int64_t m = m0 + 64 * pass + 32 * ii + 8 * q + 4 * (lane >> 5);
+            rsc[ii][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (uint32_t)(m * 4), 0, 0));
+          }
+        auto rows = [&](auto H) {
+          static_for<0, 32>([&](auto IJ) {
+            constexpr int ii = decltype(IJ)::value >> 4, j = (decltype(IJ)::value >> 2) & 3, q4 = decltype(IJ)::value & 3;
+            constexpr int i = 2 * decltype(H)::value + ii;
+            const f32x4 v = agpr_get<(4 * i + j) * 4 + q4>();
+            const int col = 128 * wc + 32 * j + (lane & 31);
+            const int r = 32 * ii + 8 * q4 + 4 * (lane >> 5);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = v[q] * rsc[ii][q4][q] * csc[j];
+          });
+        };
+        if (pass & 1) rows(std::integral_constant<int, 1>{});
+        else rows(std::integral_constant<int, 0>{});
+      }
+    };
+    if constexpr (F8) {
+      tile_epilogue<BM, BN, NTH, decltype(wp8), true>(M, N, m0, n0, Cd, E, smem, t, wp8);
+    } else {
 #if G4_STAMPS
     tile_epilogue<BM, BN, NTH, decltype(wp), true>(M, N, m0, n0, Cd, E, smem, t, wp, stmp + 8);
 #else
     tile_epilogue<BM, BN, NTH, decltype(wp), true>(M, N, m0, n0, Cd, E, smem, t, wp);
 #endif
+    }
   };
 
   const int64_t I = sk.sk_iters, G = sk.grid;
@@ -1697,13 +1855,17 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #define SVLA_GEMM4_KERNEL(LA_, LB_)                                                                      \
   __global__ __launch_bounds__(256, 1) void gemm4_kernel_##LA_##LB_(                                     \
       int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) { \
-    gemm4_body<LA_, LB_>(M, N, K, A, B, Cd, E, sk);                                                      \
+    gemm4_body<LA_, LB_>(M, N, K, A, B, Cd, E, sk, F8Scales{});                                          \
   }
 SVLA_GEMM4_KERNEL(0, 0)
 SVLA_GEMM4_KERNEL(0, 1)
 SVLA_GEMM4_KERNEL(1, 0)
 SVLA_GEMM4_KERNEL(1, 1)
 #undef SVLA_GEMM4_KERNEL
+__global__ __launch_bounds__(256, 1) void gemm4f8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B,
+                                                         CDesc Cd, svla_epilogue E, SKArgs sk, F8Scales fs) {
+  gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, true>(M, N, K, A, B, Cd, E, sk, fs);
+}
 
 template <auto KERN>
 void set_lds_once(int bytes) {
@@ -2029,7 +2191,7 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
 }
 
 int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
-            const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s) {
+            const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s, const F8Scales* fs = nullptr) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   SKArgs sk;
   memset(&sk, 0, sizeof(sk));
@@ -2059,6 +2221,15 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
       lds_set = true;                                                                                \
     }                                                                                                \
     hipLaunchKernelGGL(gemm4_kernel_##LA_##LB_, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);   \
+  }
+  if (fs) {
+    static bool lds_set = false;
+    if (!lds_set) {
+      (void)hipFuncSetAttribute((const void*)gemm4f8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, p4::LDS);
+      lds_set = true;
+    }
+    hipLaunchKernelGGL(gemm4f8_kernel, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk, *fs);
+    return svla::check_launch("gemm4 fp8");
   }
   const int la = A.layout, lb = B.layout;
   if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(0, 0)
@@ -2278,3 +2449,77 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------------------------------------------------
+// fp8 e4m3 GEMM (BASELINE configs[4]): both operands KC fp8 with per-row fp32 scales, the 4-wave kernel in fp8 mode.
+// ------------------------------------------------------------------------------------------------------------
+extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const float* a_scale,
+                             const svla_operand* B, const float* b_scale, void* const* c_ptr,
+                             const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc, const svla_epilogue* epi,
+                             void* workspace, size_t ws_bytes, void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 16 == 0, "gemm_fp8: sizes M=%lld N=%lld K=%lld (K multiple of 16)",
+                 (long long)M, (long long)N, (long long)K);
+  SVLA_CHECK_ARG(A && B && epi && a_scale && b_scale, "gemm_fp8: NULL argument");
+  SVLA_CHECK_ARG(aligned16(a_scale) && aligned16(b_scale), "gemm_fp8: scales must be 16-B aligned");
+  SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
+  for (const svla_operand* op : {A, B}) {
+    SVLA_CHECK_ARG(op->layout == SVLA_LAYOUT_KC, "gemm_fp8: operands must be KC (reduction dim contiguous)");
+    SVLA_CHECK_ARG(op->ld > 0 && op->ld % 16 == 0, "gemm_fp8: ld %lld must be a positive multiple of 16",
+                   (long long)op->ld);
+    SVLA_CHECK_ARG((op->k_valid > 0 ? op->k_valid : K) % 16 == 0, "gemm_fp8: k_valid must be a multiple of 16");
+    for (int i = 0; i < op->nseg; ++i) SVLA_CHECK_ARG(op->ptr[i] && aligned16(op->ptr[i]), "gemm_fp8: operand ptr");
+  }
+  SVLA_CHECK_ARG(A->nseg == 1, "gemm_fp8: A has one segment");
+  const bool geglu = epi->kind == SVLA_EPI_GEGLU;
+  SVLA_CHECK_ARG(geglu ? (B->nseg == 2 && B->seg_dim == SVLA_SEG_GEGLU && B->seg_start[1] * 2 == N &&
+                          B->seg_start[1] % 128 == 0)
+                       : B->nseg == 1,
+                 "gemm_fp8: B is one segment, or two GEGLU segments of N/2 rows (multiple of 128) with EPI_GEGLU");
+  SVLA_CHECK_ARG(!epi->accumulate, "gemm_fp8: accumulate unsupported");
+  switch (epi->kind) {
+    case SVLA_EPI_STORE: break;
+    case SVLA_EPI_BIAS: SVLA_CHECK_ARG(epi->bias && aligned16(epi->bias), "gemm_fp8: bias"); break;
+    case SVLA_EPI_BIAS_RESID: SVLA_CHECK_ARG(epi->in0 && epi->ld_in0 % 8 == 0, "gemm_fp8: BIAS_RESID needs in0"); break;
+    case SVLA_EPI_GEGLU:
+      SVLA_CHECK_ARG(epi->out1 && epi->out2 && epi->ld_out1 % 8 == 0 && epi->ld_out2 % 8 == 0,
+                     "gemm_fp8: GEGLU needs out1,out2");
+      break;
+    case SVLA_EPI_ROPE:
+      SVLA_CHECK_ARG(epi->rope_cos && epi->rope_sin && epi->rope_L > 0 && epi->rope_D >= 16 && epi->rope_D % 16 == 0 &&
+                         epi->rope_D <= 256 && (256 % epi->rope_D) == 0 && epi->rope_ld % 8 == 0 &&
+                         epi->rope_cols % epi->rope_D == 0 && epi->rope_cols <= N,
+                     "gemm_fp8: ROPE tables / sizes");
+      SVLA_CHECK_ARG(c_nseg == 1, "gemm_fp8: ROPE writes one C matrix");
+      break;
+    default: SVLA_CHECK_ARG(false, "gemm_fp8: epilogue %d unsupported (STORE, BIAS, BIAS_RESID, GEGLU, ROPE)", epi->kind);
+  }
+  SVLA_CHECK_ARG(ldc % 8 == 0 && c_nseg >= 1 && c_nseg <= 4, "gemm_fp8: ldc / c_nseg");
+  CDesc C;
+  C.n = c_nseg;
+  C.ld = ldc;
+  for (int i = 0; i < 4; ++i) C.ptr[i] = nullptr;
+  for (int i = 0; i < 5; ++i) C.start[i] = 0;
+  for (int i = 0; i < c_nseg; ++i) {
+    C.ptr[i] = (bf16_t*)c_ptr[i];
+    C.start[i] = c_seg_start ? c_seg_start[i] : 0;
+    SVLA_CHECK_ARG(C.ptr[i] && aligned16(C.ptr[i]), "gemm_fp8: C ptr[%d] null or misaligned", i);
+    if (i > 0) SVLA_CHECK_ARG(C.start[i] % 256 == 0, "gemm_fp8: C segment start must be a multiple of 256");
+  }
+  // k units of two fp8 values: the bf16 staging machinery runs unchanged on them
+  svla_operand A2 = *A, B2 = *B;
+  A2.ld /= 2;
+  B2.ld /= 2;
+  A2.k_valid /= 2;
+  B2.k_valid /= 2;
+  F8Scales fs;
+  fs.sa = a_scale;
+  fs.sb = b_scale;
+  fs.na = A->r_valid > 0 ? A->r_valid : M;
+  fs.nb = geglu ? 2 * B->seg_start[1] : (B->r_valid > 0 ? B->r_valid : N);
+  fs.geglu_I = geglu ? B->seg_start[1] : 0;
+  GemmCtx ctx;
+  ctx.ws = workspace;
+  ctx.ws_bytes = workspace ? ws_bytes : 0;
+  ctx.variant = 0;
+  return launch4(M, N, K / 2, A2, B2, C, *epi, ctx, (hipStream_t)stream, &fs);
+}

@@ -316,6 +316,8 @@ class TrainEngine:
             torch.sum(self.sumsq_parts, 0, keepdim=True, out=self.sumsq)
             dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=ex.pg)
         Kx.clip_scale(self.sumsq, self.max_grad_norm, self.clip, self.gnorm)
+        from . import functional as Fn
+        Fn.WEIGHT_EPOCH[0] += 1  # AdamW below rewrites the bf16 weights behind torch's version counters
         if self.world == 1:
             Kx.adamw(self.master, self.flat_param, self.flat_grad, self.m, self.v, lr, self.betas[0], self.betas[1],
                     self.eps, self.wd, self.step_count, self.clip)

@@ -230,6 +230,43 @@ class LinearFn(torch.autograd.Function):
         return dx, retw, retb, dres, None
 
 
+# ------------------------------------------------------------------------------------ fp8 projections
+# Bumped by TrainEngine.optimizer_step: AdamW rewrites the bf16 weights through the C-ABI, which torch's version
+# counters do not see, so the fp8 weight copies compare this epoch as well.
+WEIGHT_EPOCH = [0]
+
+
+class FP8Weights:
+    """Row-wise e4m3 copies of one Gemma2 layer's projection weights (BASELINE configs[4]): q|k|v [4096, H],
+    o [H, 2048], gate|up [2I, H], down [H, I], each with its per-row fp32 scales (svla_quant_fp8_rows).  Rebuilt
+    lazily when a weight moved, was modified in place, or the optimizer stepped (WEIGHT_EPOCH)."""
+
+    def __init__(self):
+        self._key = None
+        self.mats = {}
+
+    @staticmethod
+    def _rows(mats):
+        mats = K._merge_rows(list(mats))
+        return mats[0] if len(mats) == 1 else torch.cat(mats, 0)
+
+    def get(self, name, mats):
+        key = (WEIGHT_EPOCH[0],) + tuple((m.data_ptr(), m._version) for m in mats)
+        hit = self.mats.get(name)
+        if hit is None or hit[0] != key:
+            q, s = K.quant_fp8_rows(self._rows(mats))
+            hit = (key, q, s)
+            self.mats[name] = hit
+        return hit[1], hit[2]
+
+
+def _fp8_linear(x, f8, name, mats, out, **kw):
+    """out = epi(x @ cat(mats)^T) with both operands quantised row-wise to e4m3 (x per call, weights cached)."""
+    xq, xs = K.quant_fp8_rows(x)
+    wq, ws = f8.get(name, mats)
+    K.gemm_fp8(xq, xs, wq, ws, out, **kw)
+
+
 # ------------------------------------------------------------------------------------ Gemma2 blocks
 @dataclass
 class GemmaAttnCfg:
@@ -251,19 +288,26 @@ class GemmaAttentionFn(torch.autograd.Function):
     pre-rotation q/k (RoPE transpose), which is what the projection backward needs."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg):
+    def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg, f8: Optional[FP8Weights] = None):
         x = _c(x)
         M, H = x.shape
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
-        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, cfg.L, cfg.D, qd + kd))
+        rope = (cos, sin, cfg.L, cfg.D, qd + kd)
+        if f8 is not None:
+            _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, kind=L.EPI_ROPE, rope=rope)
+        else:
+            K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=rope)
         attn = _empty(M, qd, like=x)
         lse = _empty(cfg.B, cfg.Hq, cfg.L, dtype=F32, like=x)
         a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window)
         K.attn_fwd(a, attn, lse)
         out = _empty(M, wo.shape[0], like=x)
-        K.linear_fwd(attn, [wo], out)
+        if f8 is not None:
+            _fp8_linear(attn, f8, "o", (wo,), out)
+        else:
+            K.linear_fwd(attn, [wo], out)
         ctx.save_for_backward(x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class)
         ctx.cfg = cfg
         return out
@@ -302,7 +346,7 @@ class GemmaAttentionFn(torch.autograd.Function):
                     K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
                 off += n
         rets = [d[2] for d in dests]
-        return (dx, *rets, ret_wo, None, None, None, None)
+        return (dx, *rets, ret_wo, None, None, None, None, None)
 
 
 @torch.no_grad()
@@ -345,16 +389,20 @@ class GemmaMLPFn(torch.autograd.Function):
     GEMM with the GeGLU in its epilogue; backward: dH GEMM, then the GeGLU derivative in one elementwise pass."""
 
     @staticmethod
-    def forward(ctx, x, wg, wu, wd):
+    def forward(ctx, x, wg, wu, wd, f8: Optional[FP8Weights] = None):
         x = _c(x)
         M = x.shape[0]
         I = wg.shape[0]
         h = _empty(M, I, like=x)
         g = _empty(M, I, like=x)
         u = _empty(M, I, like=x)
-        K.linear_geglu_fwd(x, wg, wu, h, g, u)
         out = _empty(M, wd.shape[0], like=x)
-        K.linear_fwd(h, [wd], out)
+        if f8 is not None:
+            _fp8_linear(x, f8, "gate_up", (wg, wu), h, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u)
+            _fp8_linear(h, f8, "down", (wd,), out)
+        else:
+            K.linear_geglu_fwd(x, wg, wu, h, g, u)
+            K.linear_fwd(h, [wd], out)
         ctx.save_for_backward(x, wg, wu, wd, g, u, h)
         return out
 
@@ -384,7 +432,7 @@ class GemmaMLPFn(torch.autograd.Function):
                 K.linear_wgrad(_c(dgu[:, :I]), x, [dg_], accumulate=accg)
             if du_ is not None:
                 K.linear_wgrad(_c(dgu[:, I:]), x, [du_], accumulate=accu)
-        return dx, retg, retu, ret_wd
+        return dx, retg, retu, ret_wd, None
 
 
 # ------------------------------------------------------------------------------------ SigLIP blocks

@@ -245,6 +245,68 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, outs: List[torch.Tensor], ac
     gemm(N, K, M, A, B, outs, starts, K, _epi(L.EPI_STORE, accumulate=accumulate))
 
 
+# ---------------------------------------------------------------------------------------- fp8 projections
+FP8 = torch.float8_e4m3fn
+
+
+def quant_fp8_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None):
+    """Row-wise OCP e4m3 quantisation (svla_quant_fp8_rows): q = e4m3(clamp(x * 448/amax_row)), scale = amax_row/448.
+    Returns (q [rows, K] float8_e4m3fn, scale [rows] fp32)."""
+    _chk_bf16(x, "quant_fp8_rows")
+    rows, K = x.shape
+    if q is None:
+        q = torch.empty(rows, K, dtype=FP8, device=x.device)
+    if scale is None:
+        scale = torch.empty(rows, dtype=torch.float32, device=x.device)
+    _req(q.dtype == FP8 and q.shape == (rows, K) and q.stride(1) == 1, "quant_fp8_rows: q must be [rows, K] e4m3")
+    _req(scale.dtype == torch.float32 and scale.numel() >= rows and scale.is_contiguous(), "quant_fp8_rows: scale")
+    L.check(L.lib().svla_quant_fp8_rows(rows, K, x.data_ptr(), _ld(x), q.data_ptr(), q.stride(0), scale.data_ptr(),
+                                        _stream()), "svla_quant_fp8_rows")
+    return q, scale
+
+
+def _operand_fp8(mats: Sequence[torch.Tensor], seg_dim: int = L.SEG_OUTER, starts=None) -> L.Operand:
+    op = L.Operand()
+    ld = mats[0].stride(0)
+    for i, m in enumerate(mats):
+        _req(m.is_cuda and m.dtype == FP8 and m.dim() == 2 and m.stride(1) == 1 and m.stride(0) == ld,
+             "gemm_fp8: operands are row-major e4m3 matrices with one leading dimension")
+        op.ptr[i] = m.data_ptr()
+    op.nseg, op.seg_dim, op.layout, op.ld = len(mats), seg_dim, L.LAYOUT_KC, ld
+    if starts is not None:
+        for i, s in enumerate(starts):
+            op.seg_start[i] = int(s)
+    return op
+
+
+def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, out: torch.Tensor,
+             kind=L.EPI_STORE, geglu_I: int = 0, **epi_kw):
+    """out = epi(xs[m] * ws[n] * (xq @ wq^T)) on the fp8 MFMA kernel (svla_gemm_fp8).  geglu_I > 0: wq holds the
+    gate rows [0, I) then the up rows [I, 2I), kind EPI_GEGLU, epi_kw out1=g, out2=u."""
+    M, K = xq.shape
+    N = wq.shape[0]
+    _req(wq.shape[1] == K, f"gemm_fp8: weight K {wq.shape[1]} != {K}")
+    _req(xs.numel() >= M and ws.numel() >= N and xs.dtype == ws.dtype == torch.float32, "gemm_fp8: scales")
+    A = _operand_fp8([xq])
+    if geglu_I:
+        B = _operand_fp8([wq[:geglu_I], wq[geglu_I:]], L.SEG_GEGLU, [0, geglu_I])
+    else:
+        B = _operand_fp8([wq])
+    cp = (ctypes.c_void_p * 4)(out.data_ptr(), None, None, None)
+    cs = (ctypes.c_int64 * 5)(0, 0, 0, 0, 0)
+    wsp = gemm_workspace()
+    e = _epi(kind, **epi_kw)
+    rec = launch_timer.get("geglu_fp8") if geglu_I else None
+    if rec is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+    L.check(L.lib().svla_gemm_fp8(M, N, K, ctypes.byref(A), xs.data_ptr(), ctypes.byref(B), ws.data_ptr(), cp, cs, 1,
+                                  _ld(out), ctypes.byref(e), wsp.data_ptr(), wsp.numel(), _stream()), "svla_gemm_fp8")
+    if rec is not None:
+        e1.record(torch.cuda.current_stream())
+        rec.append((e0, e1, M, N, K))
+
+
 # ---------------------------------------------------------------------------------------- norms
 def rmsnorm_fwd(x, w, eps, y, rstd):
     rows, N = x.shape

@@ -116,7 +116,7 @@ class Gemma2MLP(nn.Module):
     def forward(self, x):
         shp = x.shape
         out = Fn.GemmaMLPFn.apply(x.reshape(-1, shp[-1]), self.gate_proj.weight, self.up_proj.weight,
-                                  self.down_proj.weight)
+                                  self.down_proj.weight, getattr(self, "_svla_fp8", None))
         return out.view(*shp[:-1], self.hidden_size)
 
 
@@ -194,7 +194,7 @@ class Gemma2Attention(nn.Module):
             return out.view(B, Lq, H)
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
-                                        cfg)
+                                        cfg, getattr(self, "_svla_fp8", None))
         return out.view(B, Lq, H)
 
 
@@ -219,6 +219,14 @@ class Gemma2DecoderLayer(nn.Module):
         self.pre_feedforward_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.post_feedforward_layernorm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
         self.sliding_window = config.sliding_window
+
+    def set_fp8_projections(self, enabled: bool):
+        """BASELINE configs[4]: run the forward q|k|v, o, gate|up and down projections of this layer on the fp8
+        MFMA GEMM (row-wise e4m3 activations and weights, fp32 accumulation); the backward stays bf16.  Training
+        and the uncached forward only -- the KV-cached decode keeps the bf16 GEMV path."""
+        f8 = Fn.FP8Weights() if enabled else None
+        self.self_attn._svla_fp8 = f8
+        self.mlp._svla_fp8 = f8
 
     def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None):
         # reference :475-496 (sandwich norms + residuals)

@@ -458,6 +458,14 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
     DECODE_STATES_MAX = 2      # decode states (KV cache + captured graphs) kept per model, least recently used out
     DECODE_CAPACITY_STEP = 64  # cache capacities are bucketed: prompts of nearby lengths share one state
 
+    def enable_fp8_projections(self, enabled: bool = True):
+        """BASELINE configs[4]: the Gemma2 q|k|v, o, gate|up and down forward projections on the fp8 (OCP e4m3,
+        row-scaled) MFMA GEMM, the attention and every backward GEMM unchanged (bf16).  Tolerances: tests/
+        test_fp8_gpu.py; the captured prefill/decode graphs are dropped (the prefill changes)."""
+        for layer in self.language_model.model.layers:
+            layer.set_fp8_projections(enabled)
+        self.clear_decode_cache()
+
     def clear_decode_cache(self):
         """Drop every persistent decode state (KV caches, captured prefill/decode graphs and their memory pool).
         The graphs hold raw pointers to the weights they were captured with, so anything that rebinds parameter
