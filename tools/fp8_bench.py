@@ -41,6 +41,6 @@ for name, n, k, geglu in SHAPES:
     q = lambda: K.quant_fp8_rows(x, xq, xs)
     t8, t16, tq = timeit(f8), timeit(b16), timeit(q)
     fl = 2.0 * m * n * k
-    print(f"{name:10s} M={m} N={n} K={k}: fp8 {t8:.3f} ms {fl / t8 / 1e9:7.1f} TF ({fl / t8 / 5e9:.3f} of 5 PF)"
+    print(f"{name:10s} M={m} N={n} K={k}: fp8 {t8:.3f} ms {fl / t8 / 1e9:7.1f} TF ({fl / t8 / 5e12:.3f} of 5 PF)"
           f" | bf16 {t16:.3f} ms {fl / t16 / 1e9:7.1f} TF | act quant {tq * 1e3:.1f} us | speedup {t16 / t8:.2f}x",
           flush=True)
