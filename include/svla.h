@@ -149,7 +149,7 @@ int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
  * returned w.r.t. the pre-rotation q/k (the transpose of rotate_half RoPE applied to the gradients);
  * svla_attn_fwd rejects them.
  * bias (optional, forward only): an additive score bias shared by the batch, element (h, i, j) at
- * bias + (h*L + i)*bias_ld + j (bf16) — BEiT's relative position bias (transformers beit BeitLayer [3p], the
+ * bias + (h*L + i)*bias_ld + j (bf16; bias_ld >= round8(L), a multiple of 8) — BEiT's relative position bias (transformers beit BeitLayer [3p], the
  * ZoeDepth backbone called at model/modeling_spatialvla.py:314-323); not combined with softcap or kv_class.
  * head_dim D in {256, 72, 64}; L <= 8192.  lse: [B, Hq, L] fp32 (natural log of the softmax denominator).
  * ---------------------------------------------------------------------------------------- */

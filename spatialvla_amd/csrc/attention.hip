@@ -239,6 +239,21 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   const int nkt = (L + 63) / 64;
   glds_tile<RS, 64, NW>(smem, kbase, a.ldk, L, D, w, lane);
   glds_tile<RS, 64, NW>(smem + TB, vbase, a.ldv, L, D, w, lane);
+  // BIAS: this lane's bias row (its query) is read one key tile ahead into registers (keys 16nt + 4g .. +3 of the
+  // tile; 8 B per nt, zero beyond the padded row): the loads of tile kt+1 are in flight during tile kt
+  const bf16_t* brow = nullptr;
+  u32x2 bnext[4];
+  auto bias_fetch = [&](int kt_) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int k = kt_ * 64 + 16 * nt + 4 * g;
+      bnext[nt] = k < a.bias_ld ? *reinterpret_cast<const u32x2*>(brow + k) : u32x2{0u, 0u};
+    }
+  };
+  if constexpr (BIAS) {
+    brow = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid ? qi : 0)) * a.bias_ld;
+    bias_fetch(0);
+  }
 
   f32x4 acc[NDT];
 #pragma unroll
@@ -289,18 +304,13 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
       float mt = -INFINITY;
       float bb[4][4];  // additive score bias (BEiT relative position bias), row qi, keys 16nt + 4g + j of tile kt
       if constexpr (BIAS) {
-        const bf16_t* brow = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid ? qi : 0)) * a.bias_ld + kt * 64 + 4 * g;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          if (plain) {
-            const u32x2 w2 = *reinterpret_cast<const u32x2*>(brow + 16 * nt);
-            bb[nt][0] = __uint_as_float(w2[0] << 16); bb[nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
-            bb[nt][2] = __uint_as_float(w2[1] << 16); bb[nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bb[nt][j] = kt * 64 + 16 * nt + 4 * g + j < L ? bf2f(brow[16 * nt + j]) : 0.f;
-          }
+          const u32x2 w2 = bnext[nt];
+          bb[nt][0] = __uint_as_float(w2[0] << 16); bb[nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
+          bb[nt][2] = __uint_as_float(w2[1] << 16); bb[nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
         }
+        if (kt + 1 < nkt) bias_fetch(kt + 1);
       }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
@@ -347,13 +357,16 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   // natural-log lse of the scores (CAP: of p = exp(t) directly; else of the max-shifted log2-domain sum)
   if (qvalid && g == 0) lse[((int64_t)b * a.Hq + h) * L + qi] = CAP ? __logf(l) : (m + __log2f(l)) / LOG2E;
 
-  // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [16 q][DV] -> 16-B stores
+  // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [16 q][DV + 16] -> 16-B stores.
+  // The 16-element row pad puts the 16 query rows of one 8-B store 32 B apart (an unpadded DV = 256 row stride
+  // maps all 16 onto the same two banks: a 16-way conflict on every store).
+  constexpr int IS = DV + 16;
   __syncthreads();
-  bf16_t* img = (bf16_t*)(smem) + w * 16 * DV;
+  bf16_t* img = (bf16_t*)(smem) + w * 16 * IS;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) {
     uint32_t lo = pack2(acc[dt][0] * inv, acc[dt][1] * inv), hi = pack2(acc[dt][2] * inv, acc[dt][3] * inv);
-    *reinterpret_cast<u32x2*>(img + c * DV + 16 * dt + 4 * g) = u32x2{lo, hi};
+    *reinterpret_cast<u32x2*>(img + c * IS + 16 * dt + 4 * g) = u32x2{lo, hi};
   }
   __syncthreads();
   constexpr int CPR = D / 8;  // 16-B chunks per output row
@@ -362,7 +375,7 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
     const int q = qt * 64 + 16 * wq + r;
     if (q < L)
       *reinterpret_cast<u32x4*>(out + ((int64_t)b * L + q) * ldo + (int64_t)h * D + ch * 8) =
-          *reinterpret_cast<const u32x4*>(img + r * DV + ch * 8);
+          *reinterpret_cast<const u32x4*>(img + r * IS + ch * 8);
   }
 }
 
@@ -750,8 +763,8 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
     SVLA_CHECK_ARG(!cap && !a->kv_class && a->sliding_window <= 0 && a->Hq == a->Hkv,
                    "attn_fwd: head_dim 64 is the BEiT path (MHA, no softcap, kv_class or window)");
     if (a->bias) {
-      SVLA_CHECK_ARG(a->bias_ld >= a->L && a->bias_ld % 4 == 0 && ((uintptr_t)a->bias & 7) == 0,
-                     "attn_fwd: bias rows must hold L keys, ld a multiple of 4, 8-B aligned");
+      SVLA_CHECK_ARG(a->bias_ld >= (a->L + 7) / 8 * 8 && a->bias_ld % 8 == 0 && ((uintptr_t)a->bias & 15) == 0,
+                     "attn_fwd: bias rows must hold round8(L) keys (ld a multiple of 8), 16-B aligned");
       return fwd_launch<64, 1, false, true>(*a, o, ldo, lse, s);
     }
     return fwd_launch<64, 1, false>(*a, o, ldo, lse, s);

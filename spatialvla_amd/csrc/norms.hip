@@ -119,34 +119,61 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
 
 // ------------------------------------------------------------------ RMSNorm backward
 // dx = rstd*(g - xhat*mean(g*xhat)) + dres,  g = dy*(1+w), xhat = x*rstd;  dw += sum_rows dy*xhat
+// A block walks RPB rows; the next row's x / dy / dres (raw 16-B chunks) are loaded before the current row's
+// reduction barriers, so every row after the first finds its operands in registers (the row-serial version paid a
+// full HBM round trip per row: 40-63 us at [9984, 2304], ~3 TB/s).  MC = 16-B chunks per thread (N <= 256*8*MC).
+template <int MC>
 __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ w, const float* __restrict__ rstd,
                                                       const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dres,
                                                       bf16_t* __restrict__ dx, float* __restrict__ dw_partial) {
   __shared__ float red[16];
   const int nch = (int)(N >> 3);
-  float wf[MAXC][8], dwacc[MAXC][8];
+  float wf[MC][8], dwacc[MC][8];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
+  for (int c = 0; c < MC; ++c) {
     int ch = threadIdx.x + c * NTH;
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwacc[c][j] = 0.f;
     if (ch < nch) ld8(w + ch * 8, wf[c]);
   }
   const int64_t r0 = (int64_t)blockIdx.x * RPB;
-  for (int rr = 0; rr < RPB; ++rr) {
+  const int nr = (int)min<int64_t>(RPB, rows - r0);
+  u32x4 px[MC], pd[MC], pr[MC];
+  float prs = 0.f;
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      const int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        px[c] = *reinterpret_cast<const u32x4*>(x + row * N + ch * 8);
+        pd[c] = *reinterpret_cast<const u32x4*>(dy + row * N + ch * 8);
+        if (dres) pr[c] = *reinterpret_cast<const u32x4*>(dres + row * N + ch * 8);
+      }
+    }
+    prs = rstd[row];
+  };
+  fetch(r0);
+  for (int rr = 0; rr < nr; ++rr) {
     const int64_t row = r0 + rr;
-    if (row >= rows) break;
-    const float rs = rstd[row];
-    float xv[MAXC][8], gv[MAXC][8];
+    const float rs = prs;
+    u32x4 cx[MC], cd[MC], cr[MC];
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      cx[c] = px[c];
+      cd[c] = pd[c];
+      cr[c] = pr[c];
+    }
+    if (rr + 1 < nr) fetch(row + 1);
+    float xv[MC][8], gv[MC][8];
     float dot = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
+    for (int c = 0; c < MC; ++c) {
       int ch = threadIdx.x + c * NTH;
       if (ch < nch) {
         float d[8];
-        ld8(x + row * N + ch * 8, xv[c]);
-        ld8(dy + row * N + ch * 8, d);
+        unpack8(cx[c], xv[c]);
+        unpack8(cd[c], d);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float xh = xv[c][j] * rs;
@@ -159,7 +186,7 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
     }
     dot = block_sum(dot, red) / (float)N;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
+    for (int c = 0; c < MC; ++c) {
       int ch = threadIdx.x + c * NTH;
       if (ch < nch) {
         float o[8];
@@ -167,7 +194,7 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
         for (int j = 0; j < 8; ++j) o[j] = rs * (gv[c][j] - xv[c][j] * dot);
         if (dres) {
           float r[8];
-          ld8(dres + row * N + ch * 8, r);
+          unpack8(cr[c], r);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]) + r[j];
         }
@@ -176,7 +203,7 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
     }
   }
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
+  for (int c = 0; c < MC; ++c) {
     int ch = threadIdx.x + c * NTH;
     if (ch < nch) {
       float* p = dw_partial + (int64_t)blockIdx.x * N + ch * 8;
@@ -479,9 +506,14 @@ extern "C" int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const vo
                        (const bf16_t*)x, (const bf16_t*)w, (const float*)nullptr, rstd, (const bf16_t*)dy,
                        (const bf16_t*)dres, (bf16_t*)dx, dw_partial);
   } else {
-    hipLaunchKernelGGL(rms_bwd_kernel, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
-                       (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
-                       dw_partial);
+    if (N <= NTH * 8 * 2)
+      hipLaunchKernelGGL(rms_bwd_kernel<2>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                         (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                         dw_partial);
+    else
+      hipLaunchKernelGGL(rms_bwd_kernel<MAXC>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                         (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                         dw_partial);
   }
   return svla::check_launch("rmsnorm_bwd");
 }

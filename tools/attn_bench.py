@@ -14,6 +14,7 @@ BF = torch.bfloat16
 SHAPES = [  # name, B, L, Hq, Hkv, D, scale, softcap, prefix (None: no key classes)
     ("gemma2", 32, 312, 8, 4, 256, 1 / 16, 50.0, 299),
     ("siglip", 32, 256, 16, 16, 72, 72 ** -0.5, 0.0, None),
+    ("beit", 32, 577, 16, 16, 64, 0.125, 0.0, "bias"),  # ZoeDepth BEiT-L at 384^2: relative position bias, fwd only
 ]
 
 
@@ -27,8 +28,11 @@ def main():
         W = (Hq + 2 * Hkv) * D
         qkv = torch.randn(B * Lq, W, device=dev, generator=g).to(BF)
         q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
-        cls = None
-        if prefix is not None:
+        cls = bias = None
+        if prefix == "bias":
+            bias = torch.zeros(Hq, Lq, (Lq + 7) // 8 * 8, dtype=BF, device=dev)
+            bias[:, :, :Lq] = torch.randn(Hq, Lq, Lq, device=dev, generator=g).to(BF)
+        elif prefix is not None:
             cls = torch.zeros(B, Lq, dtype=torch.uint8, device=dev)
             cls[:, prefix:] = 1
         do = torch.randn(B * Lq, Hq * D, device=dev, generator=g).to(BF)
@@ -38,13 +42,13 @@ def main():
             for tag, cd in libs:
                 L._lib = cd
                 a = K.attn_args(B, Lq, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap,
-                                cls, 0)
+                                cls, 0, bias=bias)
                 out = torch.empty(B * Lq, Hq * D, dtype=BF, device=dev)
                 lse = torch.empty(B, Hq, Lq, device=dev)
-                dqkv = torch.empty_like(qkv)
+                dqkv = torch.zeros_like(qkv)
                 ld = dqkv.stride(0)
                 fwd = lambda: K.attn_fwd(a, out, lse)  # noqa: E731
-                bwd = lambda: K.attn_bwd(a, out, do, lse, dqkv[:, :Hq * D], ld,  # noqa: E731
+                bwd = (lambda: None) if bias is not None else lambda: K.attn_bwd(a, out, do, lse, dqkv[:, :Hq * D], ld,  # noqa: E731
                                          dqkv[:, Hq * D:(Hq + Hkv) * D], ld, dqkv[:, (Hq + Hkv) * D:], ld)
                 fwd(); bwd()
                 torch.cuda.synchronize()

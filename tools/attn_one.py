@@ -17,11 +17,15 @@ g = torch.Generator(device=dev).manual_seed(1)
 W = (Hq + 2 * Hkv) * D
 qkv = torch.randn(B * Lq, W, device=dev, generator=g).to(BF)
 q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
-cls = None
-if prefix is not None:
+cls = bias = None
+if prefix == "bias":
+    bias = torch.zeros(Hq, Lq, (Lq + 7) // 8 * 8, dtype=BF, device=dev)
+    bias[:, :, :Lq] = torch.randn(Hq, Lq, Lq, device=dev, generator=g).to(BF)
+elif prefix is not None:
     cls = torch.zeros(B, Lq, dtype=torch.uint8, device=dev)
     cls[:, prefix:] = 1
-a = K.attn_args(B, Lq, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap, cls, 0)
+a = K.attn_args(B, Lq, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap, cls, 0,
+                bias=bias)
 out = torch.empty(B * Lq, Hq * D, dtype=BF, device=dev)
 lse = torch.empty(B, Hq, Lq, device=dev)
 do = torch.randn(B * Lq, Hq * D, device=dev, generator=g).to(BF)
