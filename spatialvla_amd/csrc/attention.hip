@@ -115,24 +115,37 @@ __device__ __forceinline__ void tr_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// acc[dt] += A(dt) * B over NDT d-tiles, A read transposed from LDS in batches of 8 (32 VGPRs in flight);
+// acc[dt] += A(dt) * B over NDT d-tiles, A read transposed from LDS in batches of 4 fragments, double-buffered:
+// batch i+1's 8 transpose reads are issued before batch i's MFMAs (lgkmcnt(8) waits for batch i only), so the LDS
+// latency of a batch hides behind the previous batch's MFMAs instead of stalling every batch.
 // AT_A: the LDS operand is the MFMA A operand (else B)
 template <int RS, int NDT, bool AT_A>
 __device__ __forceinline__ void mfma_tr_sweep(f32x4 (&acc)[NDT], const char* lds, int rb, bf16x8 other, int lane) {
+  constexpr int CH = 4, NB = (NDT + CH - 1) / CH;
+  TrFrag f[2][CH];
 #pragma unroll
-  for (int d0 = 0; d0 < NDT; d0 += 8) {
-    constexpr int CH = NDT < 8 ? NDT : 8;
-    TrFrag f[CH];
+  for (int i = 0; i < CH; ++i)
+    if (i < NDT) f[0][i].template load<RS>(lds, rb, 16 * i, lane);
 #pragma unroll
-    for (int i = 0; i < CH; ++i)
-      if (d0 + i < NDT) f[i].template load<RS>(lds, rb, 16 * (d0 + i), lane);
-    tr_wait();
+  for (int bi = 0; bi < NB; ++bi) {
+    const int d0 = bi * CH;
+    if (bi + 1 < NB) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        if (d0 + CH + i < NDT) f[(bi + 1) & 1][i].template load<RS>(lds, rb, 16 * (d0 + CH + i), lane);
+      if (NDT - (d0 + CH) >= CH) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < CH; ++i)
       if (d0 + i < NDT) {
-        if (AT_A) acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[i].get(), other, acc[d0 + i], 0, 0, 0);
-        else acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(other, f[i].get(), acc[d0 + i], 0, 0, 0);
+        if (AT_A) acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[bi & 1][i].get(), other, acc[d0 + i], 0, 0, 0);
+        else acc[d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(other, f[bi & 1][i].get(), acc[d0 + i], 0, 0, 0);
       }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -275,12 +288,25 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
     }
     const bool plain = tile_plain(lcls, kt * 64, L, window_free, lane);
     f32x4 s[4];
+    {  // K fragments of k-step ks+1 are read while k-step ks multiplies (double-buffered, 32 VGPRs)
+      bf16x8 kb[2][4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < 4; ++nt) {
+        s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        kb[0][nt] = frag_row<RS>(ldsK, 16 * nt, 0, lane);
+      }
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsK, 16 * nt, ks, lane), qf[ks], s[nt], 0, 0, 0);
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks + 1 < NKS) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) kb[(ks + 1) & 1][nt] = frag_row<RS>(ldsK, 16 * nt, ks + 1, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[ks & 1][nt], qf[ks], s[nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     float p[4][4];
     if constexpr (CAP) {
@@ -456,11 +482,10 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
   constexpr int TB = tile_bytes<D>(64), QB = tile_bytes<D>(32);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ldsV = smem;
-  char* ldsQ = smem + TB;  // {Q [32][RS], dO [32][RS]}
-  char* ldsO = ldsQ + QB;
+  char* const ldsQ2 = smem + TB;  // two stages of {Q [32][RS], dO [32][RS]}: step+1 lands while step is consumed
   const int L = a.L, LP = (L + 35) / 32 * 32;  // lse/delta row stride: every 32-query tile in range
   const int grp = a.Hq / a.Hkv;
-  float* llse = (float*)(ldsO + QB);  // [grp][LP], log2 domain
+  float* llse = (float*)(ldsQ2 + 4 * QB);  // [grp][LP], log2 domain
   float* ldel = llse + grp * LP;
   uint8_t* lcls = (uint8_t*)(ldel + grp * LP);
 
@@ -504,23 +529,40 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
   for (int i = 0; i < NDT; ++i) adk[i] = adv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
 
+  issue_q(0, ldsQ2);
   for (int step = 0; step < nsteps; ++step) {
-    if (step) __syncthreads();  // every wave is done with the previous Q / dO tile
-    issue_q(step, ldsQ);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    __syncthreads();  // stage step&1 landed everywhere; every wave is done with step-1 (its stage is free)
+    if (step + 1 < nsteps) issue_q(step + 1, ldsQ2 + ((step + 1) & 1) * 2 * QB);
+    const char* const ldsQ = ldsQ2 + (step & 1) * 2 * QB;
+    const char* const ldsO = ldsQ + QB;
     const int hh = step / nqt, q0 = (step % nqt) * 32;
     const float* sl = llse + hh * LP;
     const float* sd = ldel + hh * LP;
     f32x4 s[2], dp[2];
+    {  // Q / dO / V fragments of k-step ks+1 are read while k-step ks multiplies (double-buffered)
+      bf16x8 qb[2][2], ob[2][2], vb[2];
+      auto ld = [&](int ks, int bf) {
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      s[mt] = dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < 2; ++mt) {
+          qb[bf][mt] = frag_row<RS>(ldsQ, 16 * mt, ks, lane);
+          ob[bf][mt] = frag_row<RS>(ldsO, 16 * mt, ks, lane);
+        }
+        vb[bf] = frag_row<RS>(ldsV, 16 * w, ks, lane);
+      };
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) s[mt] = dp[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ld(0, 0);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsQ, 16 * mt, ks, lane), kf[ks], s[mt], 0, 0, 0);
-        dp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row<RS>(ldsO, 16 * mt, ks, lane),
-                                                         frag_row<RS>(ldsV, 16 * w, ks, lane), dp[mt], 0, 0, 0);
+        if (ks + 1 < NKS) ld(ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          s[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks & 1][mt], kf[ks], s[mt], 0, 0, 0);
+          dp[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ob[ks & 1][mt], vb[ks & 1], dp[mt], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     // element (mt, j): query q0 + 16mt + 4g + j, key = lane col (kl)
@@ -731,7 +773,7 @@ int bwd_launch(const svla_attn_args& a, const bf16_t* dout, int64_t lddo, const 
                bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv, int64_t lddv, hipStream_t s) {
   const int grp = a.Hq / a.Hkv;
   const int LP = (a.L + 35) / 32 * 32;
-  const int lds_kv = tile_bytes<D>(64) + 2 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
+  const int lds_kv = tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
   SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
   const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
   const int nt = (a.L + 63) / 64;
