@@ -16,6 +16,9 @@ another order (tolerances in tests/test_model_gpu.py):
 * BEiT layers (BeitLayer.forward) in inference: LayerNorm, the q|k|v / o / fc1 / fc2 GEMMs with fused bias, exact
   GELU and layer-scale + residual epilogues, and the head_dim-64 attention with the additive relative position
   bias, all on libsvla (functional.beit_layer); the bias is copied once per layer into [heads, L, round8(L)] rows.
+* DPT readout projections (ZoeDepthReassembleStage.readout_projects[i] = Linear(2H, H) + exact GELU): one libsvla
+  GEMM with the BIAS_GELU_ERF epilogue (bf16(gelu_erf(bf16(acc + b))), the eager module's rounding points) instead
+  of the stock Linear (hipBLASLt) + elementwise GELU.
 * Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
   relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
   and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
@@ -140,11 +143,43 @@ def _beit_layer_forward(self, hidden_states, attention_mask=None, interpolate_po
     return Fn.beit_layer(self, hidden_states, bias)
 
 
-def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True) -> torch.nn.Module:
-    """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False keep the stock metric-head tail /
-    BEiT layers (the other paths are bitwise identical to the stock modules)."""
+def _readout_forward(self, x):
+    """nn.Sequential(Linear(2H, H), GELU(erf)) of ZoeDepthReassembleStage (transformers zoedepth [3p]) as one GEMM
+    with the fused bias + exact-GELU epilogue; other inputs (grad mode, fp32, CPU) keep the stock modules."""
+    lin = self[0]
+    if (not x.is_cuda or x.dtype != torch.bfloat16 or torch.is_grad_enabled() or lin.bias is None
+            or lin.weight.dtype != torch.bfloat16 or x.shape[-1] % 8 or lin.out_features % 8):
+        return torch.nn.Sequential.forward(self, x)
+    from . import _lib as L
+    from . import kernels as K
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    out = torch.empty(x2.shape[0], lin.out_features, dtype=x.dtype, device=x.device)
+    K.linear_fwd(x2, [lin.weight], out, kind=L.EPI_BIAS_GELU_ERF, bias=lin.bias)
+    return out.view(*shp[:-1], lin.out_features)
+
+
+def _is_exact_gelu(m) -> bool:
+    if isinstance(m, torch.nn.GELU):
+        return m.approximate == "none"
+    name = type(m).__name__
+    return name == "GELUActivation" and getattr(m, "act", None) in (torch.nn.functional.gelu,)
+
+
+def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout: bool = True) -> torch.nn.Module:
+    """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False / readout=False keep the stock
+    metric-head tail / BEiT layers / readout projections (the other paths are bitwise identical to the stock
+    modules)."""
     for m in zoe.modules():
         name = type(m).__name__
+        if name == "ZoeDepthReassembleStage" and readout and hasattr(m, "readout_projects"):
+            for seq in m.readout_projects:
+                if (not getattr(seq, "_svla_fast", False) and len(seq) == 2 and isinstance(seq[0], torch.nn.Linear)
+                        and _is_exact_gelu(seq[1])):
+                    seq.forward = types.MethodType(_readout_forward, seq)
+                    seq._svla_fast = True
         if name == "BeitRelativePositionBias" and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_cached_rel_pos_bias(m.forward), m)
             m._svla_fast = True

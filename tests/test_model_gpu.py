@@ -66,7 +66,7 @@ def test_zoe_fast_paths_bitwise(cuda):
     ref = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
     fast = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
     fast.load_state_dict(ref.state_dict())
-    zoe_fast.install(fast, tail=False, beit=False)
+    zoe_fast.install(fast, tail=False, beit=False, readout=False)
     x = torch.randn(2, 3, 384, 384, device=cuda).to(torch.bfloat16)
     with torch.no_grad():
         d0 = ref(pixel_values=x).predicted_depth
@@ -291,6 +291,22 @@ def test_image_token_mismatch_raises_deferred(cuda):
         batch["input_ids"] = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}["input_ids"]
         model(**batch)
         model.check_deferred()
+
+
+def test_zoe_readout_projection_fused(cuda):
+    """DPT readout projection (Linear(2H, H) + exact GELU, transformers ZoeDepthReassembleStage) as one GEMM with the
+    BIAS_GELU_ERF epilogue vs the stock modules: same rounding points, different accumulation order (rel-L2 1e-2)."""
+    import types
+    from spatialvla_amd import zoe_fast
+    from transformers.activations import ACT2FN
+    torch.manual_seed(4)
+    seq = torch.nn.Sequential(torch.nn.Linear(2048, 1024), ACT2FN["gelu"]).to(cuda).to(torch.bfloat16)
+    x = torch.randn(3, 576, 2048, device=cuda).to(torch.bfloat16)
+    with torch.no_grad():
+        ref = seq(x)
+        seq.forward = types.MethodType(zoe_fast._readout_forward, seq)
+        out = seq(x)
+    assert out.shape == ref.shape and H.rel_l2(out, ref) < 1e-2
 
 
 def _zoe_large(cuda, seed):
