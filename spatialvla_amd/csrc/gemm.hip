@@ -24,10 +24,31 @@
 #include "agpr.h"
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 #include "agpr_f8.h"
+#include "tanh_bf16_table.h"
 
 #include <type_traits>
 
 namespace {
+
+// Gemma2 final logit softcap (softcap_bf16 of svla_common.h) with tanh taken from a table: a = bf16(bf16(v) / cap) is
+// a bf16 value, and bf16(tanh(a)) is a for |a| < 2^-8, 1 for |a| >= 4, and a 1280-entry table in between
+// (tools/gen_tanh_table.py; a correctly rounded fp32 tanh cast to bf16, as the reference's bf16 tanh).  Replaces
+// the branch-free polynomial/exp tanh (~17 VALU ops and two transcendentals) of the lm_head epilogue.
+template <typename Tab>
+__device__ __forceinline__ float softcap_bf16_tab(float v, float cap, float icap, Tab tab) {
+  const float a = round_bf(round_bf(v) * icap);
+  const uint32_t u = __float_as_uint(a);
+  const uint32_t ab = (u >> 16) & 0x7fffu;
+  const uint32_t lo = (uint32_t)SVLA_TANH_TAB_E0 << 7, hi = (uint32_t)SVLA_TANH_TAB_E1 << 7;
+  const uint32_t idx = ab < lo ? 0u : (ab >= hi ? 0u : ab - lo);
+  const uint32_t tb = tab[idx];
+  uint32_t rb = ab < lo ? ab : (ab >= hi ? 0x3f80u : tb);
+  if (ab > 0x7f80u) rb = ab;  // NaN stays NaN
+  const float t = __uint_as_float(((u >> 16) & 0x8000u | rb) << 16);
+  return round_bf(t * cap);
+}
+constexpr int TANH_TAB_BYTES = sizeof(svla_tanh_bf16_tab);
+static_assert(TANH_TAB_BYTES % 16 == 0, "table copied in 16-B pieces");
 
 #ifndef G4_STAMPS
 #define G4_STAMPS 0
@@ -48,6 +69,7 @@ struct Cfg {
   static constexpr int EPI_ROWS = 64, EPI_LD = BN + 4;
   static constexpr int EPI_BYTES = EPI_ROWS * EPI_LD * 4;
   static constexpr int LDS = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  static_assert(EPI_BYTES + TANH_TAB_BYTES <= LDS, "epilogue image + tanh table must fit");
   static_assert(IA >= 1 && IB >= 1, "tile too small for the wave count");
 };
 using CfgBig = Cfg<256, 256, 2, 4>;
@@ -347,6 +369,55 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
       if (nv > 0) load8f((const bf16_t*)E.colscale + n, sc, nv);
     }
     if (nv <= 0) return;
+    if constexpr (KIND == SVLA_EPI_ROPE) {
+      // q/k columns: x = bf16(acc), partner chunk D/2 away in the same head (same tile image), reference rounding
+      // bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)); the cos/sin rows of the next row are loaded while this row
+      // is processed (the generic path waited one L2 round trip per row)
+      const bool rot = n < E.rope_cols;
+      const int hd = E.rope_D, half = hd >> 1;
+      const int d = (int)(n % hd);
+      const bool lo = d < half;
+      const int dd = lo ? d : d - half;
+      const int poff = lo ? half : -half;
+      const bf16_t* ctab = (const bf16_t*)E.rope_cos + dd;
+      const bf16_t* stab = (const bf16_t*)E.rope_sin + dd;
+      auto tab = [&](int it, u32x4& c4, u32x4& s4) {
+        const int64_t m = m0p + t / CPR + it * RPP;
+        const int64_t pos = (m < M ? m : m0p) % E.rope_L;
+        c4 = *reinterpret_cast<const u32x4*>(ctab + pos * E.rope_ld);
+        s4 = *reinterpret_cast<const u32x4*>(stab + pos * E.rope_ld);
+      };
+      u32x4 cn = {0u, 0u, 0u, 0u}, sn = {0u, 0u, 0u, 0u};
+      if (rot) tab(0, cn, sn);
+#pragma unroll 1
+      for (int it = 0; it < ITT; ++it) {
+        const u32x4 cc4 = cn, sc4 = sn;
+        if (rot && it + 1 < ITT) tab(it + 1, cn, sn);
+        const int row = t / CPR + it * RPP;
+        const int64_t m = m0p + row;
+        const float* pe = Ei + row * EPI_LD + 8 * cc;
+        float x[8];
+        {
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(pe), x1 = *reinterpret_cast<const f32x4*>(pe + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { x[j] = x0[j]; x[4 + j] = x1[j]; }
+        }
+        if (rot) {
+          const f32x4 y0 = *reinterpret_cast<const f32x4*>(pe + poff), y1 = *reinterpret_cast<const f32x4*>(pe + poff + 4);
+          float cf[8], sf[8];
+          unpack8(cc4, cf);
+          unpack8(sc4, sf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xv = round_bf(x[j]), yv = round_bf(j < 4 ? y0[j] : y1[j - 4]);
+            const float rv = lo ? -yv : yv;
+            x[j] = round_bf(xv * cf[j]) + round_bf(rv * sf[j]);
+          }
+        }
+        if (m < M) store8(cbase + (m - cm0) * ldc + n, x, nv);
+      }
+      return;
+    }
 #pragma unroll 1
     for (int ib = 0; ib < ITT; ib += IT) {
     float v[IT][8];
@@ -456,6 +527,11 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
   constexpr int CPR = BN / 8;     // 16-B chunks per row
   constexpr int RPP = NTH / CPR;  // rows per thread-pass
   const int cc = t % CPR;
+  // SOFTCAP_CE: the bf16 tanh table goes to LDS right after the image (every kernel's LDS has >= 2.5 KiB spare
+  // there); the first pass's barrier publishes it
+  const LDS_AS unsigned short* ltab = (const LDS_AS unsigned short*)(smem + 64 * EPI_LD * 4);
+  if (kind == SVLA_EPI_SOFTCAP_CE && t < TANH_TAB_BYTES / 16)
+    *(LDS_AS u32x4*)(smem + 64 * EPI_LD * 4 + 16 * t) = reinterpret_cast<const u32x4*>(svla_tanh_bf16_tab)[t];
 #pragma unroll 1
   for (int pass = 0; pass < BM / 64; ++pass) {
 #if G4_STAMPS
@@ -485,6 +561,7 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
         epi_pass_fast<SVLA_EPI_GEGLU_BWD, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
       case SVLA_EPI_GEGLU: epi_pass_fast<SVLA_EPI_GEGLU, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
+      case SVLA_EPI_ROPE: epi_pass_fast<SVLA_EPI_ROPE, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t); break;
       case SVLA_EPI_BIAS_GELU_ERF:
         epi_pass_fast<SVLA_EPI_BIAS_GELU_ERF, BN, NTH, ITMAX>(Ei, M, N, m0p, n0, cbase, cm0, Cd.ld, E, t);
         break;
@@ -535,26 +612,29 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           // softcap, round to bf16, per-(row, 128-column group) online-softmax partials (16 lanes share one)
           float mx = -INFINITY, se = 0.f;
           int am = 0x7fffffff;
-          const float cap = E.cap;
+          const float cap = E.cap, icap = 1.0f / E.cap;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = softcap_bf16(v[j], cap);
+            v[j] = softcap_bf16_tab(v[j], cap, icap, ltab);
             if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
           }
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             if (j < nv) se += __expf(v[j] - mx);
           if (mx == -INFINITY) se = 0.f;
+          // combine the 16 lanes of the group: the group max first, then each lane's sum rescaled to it (one exp
+          // per lane instead of two per butterfly step) and the lowest column index among the lanes at the max
+          float gm = mx;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) gm = fmaxf(gm, __shfl_xor(gm, o, 64));
+          se = (mx == -INFINITY) ? 0.f : se * __expf(mx - gm);
+          am = (mx == gm) ? am : 0x7fffffff;
 #pragma unroll
           for (int o = 1; o < 16; o <<= 1) {
-            float mx2 = __shfl_xor(mx, o, 64), se2 = __shfl_xor(se, o, 64);
-            int am2 = __shfl_xor(am, o, 64);
-            float mn = fmaxf(mx, mx2);
-            float s1 = (mx == -INFINITY) ? 0.f : se * __expf(mx - mn);
-            float s2 = (mx2 == -INFINITY) ? 0.f : se2 * __expf(mx2 - mn);
-            int a = (mx > mx2 || (mx == mx2 && am < am2)) ? am : am2;
-            mx = mn; se = s1 + s2; am = a;
+            se += __shfl_xor(se, o, 64);
+            am = min(am, __shfl_xor(am, o, 64));
           }
+          mx = gm;
           if (m < M) {
             if ((cc & 15) == 0 && n < N) {  // a 128-column group that starts beyond N has no stats slot
               const int64_t ntn = (N + 127) / 128;
@@ -715,7 +795,7 @@ constexpr int BM = 256, BN = 256, HALF = 128, NTH = 512;
 constexpr int HB = HALF * BK * 2;  // bytes per half-tile image (16 KiB)
 constexpr int STAGE = 4 * HB;      // A_h0 | A_h1 | B_h0 | B_h1
 constexpr int LDS = 2 * STAGE;     // 128 KiB (the 66.5 KiB epilogue image reuses it)
-static_assert(64 * (BN + 4) * 4 <= LDS, "epilogue image must fit");
+static_assert(64 * (BN + 4) * 4 + TANH_TAB_BYTES <= LDS, "epilogue image + tanh table must fit");
 }  // namespace p8
 
 template <int LAYOUT>
@@ -1184,7 +1264,7 @@ constexpr int BM = 256, BN = 256, NTH = 256;
 constexpr int OPB = BM * BK * 2;  // bytes per operand image per buffer (32 KiB)
 constexpr int STAGE = 2 * OPB;    // A | B
 constexpr int LDS = 2 * STAGE;    // 128 KiB (the 66.5 KiB epilogue image reuses it)
-static_assert(64 * (BN + 4) * 4 <= LDS, "epilogue image must fit");
+static_assert(64 * (BN + 4) * 4 + TANH_TAB_BYTES <= LDS, "epilogue image + tanh table must fit");
 static_assert(G4_RB1 >= 15 * G4_RS && G4_DA0 > G4_RB1 && G4_DB0 >= G4_DA0 + 8 * G4_DST &&
                   G4_RB2 >= G4_DB0 + 8 * G4_DST - 1 && G4_RB2 + 1 + 15 * G4_RS < 128,
               "gemm4 schedule knobs out of order");
@@ -2058,7 +2138,7 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
           const int64_t n = r0 + r;
-          const float v = softcap_bf16(wave_sum(acc[r][m]), cap);
+          const float v = softcap_bf16_tab(wave_sum(acc[r][m]), cap, 1.0f / cap, svla_tanh_bf16_tab);
           if (n < nend) {
             if (lane == 0) c[m * ldc + n] = f2bf(v);
             if (v > mx[m]) {
@@ -2427,7 +2507,10 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
     }
   }
   const int64_t t256 = tiles(256, 256);
-  const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU;
+  // ROPE's fast-path epilogue (cos/sin prefetched a row ahead) runs as well on the 4-wave kernel: q|k|v 233 -> 225 us
+  // (tools/gemm_epi_bench.py, bitwise equal)
+  const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU ||
+                         epi->kind == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
                     (variant == 3 || ((variant == 0 || variant == 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
                                         (t256 >= 512 || K >= 4096) &&

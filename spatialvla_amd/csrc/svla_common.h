@@ -67,10 +67,12 @@ __device__ __forceinline__ float fast_tanh(float x) {
 }
 // transformers "gelu_pytorch_tanh" == torch.nn.functional.gelu(approximate="tanh")
 // Gemma2 final logit softcap on a bf16 tensor, op by op as the reference (modeling_gemma2.py:994-997):
-// logits / cap, tanh, * cap, each rounded to bf16 (true division; fast_tanh's 4e-7 error only matters at a bf16
-// rounding tie of tanh, which the argmax margin gate of the tests covers).
-__device__ __forceinline__ float softcap_bf16(float v, float cap) {
-  const float a = round_bf(round_bf(v) / cap);
+// logits / cap, tanh, * cap, each rounded to bf16 (fast_tanh's 4e-7 error only matters at a bf16 rounding tie of
+// tanh, which the argmax margin gate of the tests covers).  The division is a multiply by RN(1/cap): for every
+// finite bf16 input, bf16(x * RN(1/cap)) == bf16(x / cap) at cap 30 and 50 (checked exhaustively over all 65536
+// bf16 values, tools/check_softcap_recip.py), and it saves the ~10-instruction correctly rounded divide per logit.
+__device__ __forceinline__ float softcap_bf16(float v, float cap, float icap) {
+  const float a = round_bf(round_bf(v) * icap);
   return round_bf(round_bf(fast_tanh(a)) * cap);
 }
 __device__ __forceinline__ float gelu_tanh(float x) {

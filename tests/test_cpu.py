@@ -295,3 +295,10 @@ def test_kv_cache_layout_and_capacity():
     c.seen_tokens = 10
     with pytest.raises(ValueError):
         c.append_classes(torch.ones(2, 1, dtype=torch.uint8))
+
+
+def test_softcap_reciprocal_multiply_exact_on_bf16():
+    """The GEMM/GEMV softcap epilogues divide by the cap as a multiply by RN(1/cap) (svla_common.h softcap_bf16):
+    exact at bf16 for every finite bf16 input at caps 30 and 50 (exhaustive)."""
+    import runpy
+    runpy.run_path(os.path.join(REPO, "tools", "check_softcap_recip.py"))

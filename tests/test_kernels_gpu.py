@@ -354,6 +354,31 @@ def test_gemm_softcap_ce(cuda, M):
     assert d[:, V:].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("M", [256, 4])  # 256: MFMA tile epilogue; 4: the decode GEMV path
+def test_softcap_every_bf16_logit(cuda, M):
+    """Every finite bf16 logit value through the SOFTCAP_CE epilogue (reciprocal-multiply divide, table tanh) against
+    the reference's op-by-op bf16 softcap (modeling_gemma2.py:994-997: /cap, tanh, *cap, each cast to bf16) computed
+    by torch in float64: bit-exact.  A = e_0 rows and B[n, 0] = value n, so C[m, n] = value n exactly."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    vals = torch.arange(-32768, 32768, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    vals = vals[torch.isfinite(vals.float())]
+    V = vals.numel()
+    ldv = Kn.round_up(V, 64)
+    A = torch.zeros(M, 16, dtype=BF, device=cuda)
+    A[:, 0] = 1.0
+    B = torch.zeros(V, 16, dtype=BF, device=cuda)
+    B[:, 0] = vals.to(cuda)
+    buf = torch.empty(M, ldv, dtype=BF, device=cuda)
+    stats = torch.empty(M, Kn.ceil_div(V, 128), 3, dtype=torch.float32, device=cuda)
+    Kn.linear_fwd(A, [B], buf[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=stats, cap=30.0)
+    x = vals.double() + 0.0  # the GEMM forms 0 + 1 * (-0.0) = +0.0
+    ref = ((x / 30.0).to(torch.bfloat16).double().tanh().to(torch.bfloat16).double() * 30.0).to(torch.bfloat16)
+    got = buf[:, :V].cpu()
+    same = got.view(torch.int16) == ref.view(torch.int16)[None, :]
+    assert bool(same.all()), (f"{int((~same).sum())} mismatches, e.g. {vals[~same[0]][:5].tolist()} -> "
+                              f"{got[0][~same[0]][:5].tolist()} vs {ref[~same[0]][:5].tolist()}")
+
+
 @pytest.mark.parametrize("M,H,V,every", [(300, 256, 1000, 7), (9984 // 8, 2304, 4099, 24), (64, 128, 300, 0)])
 def test_lm_head_ce_fn_label_rows(cuda, M, H, V, every):
     """LMHeadCEFn's backward runs the softmax gradient and both lm_head GEMMs over the labelled rows only;
