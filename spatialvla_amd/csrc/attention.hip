@@ -22,6 +22,10 @@
 
 #include "svla_common.h"
 
+#ifndef SVLA_ATT_QW
+#define SVLA_ATT_QW 2  // query sub-tiles per wave of the forward at head_dim 64 / 72 (variant builds: 1)
+#endif
+
 namespace {
 
 constexpr float MASKVAL = -3.3895313892515355e38f;  // torch.finfo(bfloat16).min
@@ -220,26 +224,68 @@ __device__ __forceinline__ void block_coords(int nqt, int nhg, int& qt, int& hg,
 }
 
 // ================================================================== forward
-// Block = (query tile of 64, NH query heads sharing one kv head, batch); 4 waves per head, 16 queries per wave.
+// Block = (query tile of 64*QW, NH query heads sharing one kv head, batch); 4 waves per head, each wave QW sub-tiles
+// of 16 queries (sub-tile u: queries 64u + 16wq + c of the block's tile).  Every K / V fragment read from LDS feeds
+// QW MFMAs (QW = 2 for the short head dims, where one fragment per MFMA left the kernel LDS-bound).
 // K/V tiles stream through two LDS stages by LDS-DMA: tile kt+1 lands while tile kt is consumed.
-template <int D, int NH, bool CAP, bool BIAS = false>
+// acc[u][dt] += V(dt)^T * P_u^T over NDT d-tiles: the V fragment (transpose read, batches of 4 double-buffered as
+// mfma_tr_sweep) is loaded once and multiplied into every sub-tile.
+template <int RS, int NDT, int QW>
+__device__ __forceinline__ void mfma_tr_sweep_q(f32x4 (&acc)[QW][NDT], const char* lds, int rb, const bf16x8 (&pb)[QW],
+                                                int lane) {
+  constexpr int CH = 4, NB = (NDT + CH - 1) / CH;
+  TrFrag f[2][CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i)
+    if (i < NDT) f[0][i].template load<RS>(lds, rb, 16 * i, lane);
+#pragma unroll
+  for (int bi = 0; bi < NB; ++bi) {
+    const int d0 = bi * CH;
+    if (bi + 1 < NB) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        if (d0 + CH + i < NDT) f[(bi + 1) & 1][i].template load<RS>(lds, rb, 16 * (d0 + CH + i), lane);
+      if (NDT - (d0 + CH) >= CH) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (d0 + i < NDT) {
+        const bf16x8 v = f[bi & 1][i].get();
+#pragma unroll
+        for (int u = 0; u < QW; ++u)
+          acc[u][d0 + i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v, pb[u], acc[u][d0 + i], 0, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int D, int NH, bool CAP, bool BIAS = false, int QW = 1>
 __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
                                                                int64_t ldo, float* __restrict__ lse) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
-  constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH;
+  constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH, QT = 64 * QW;
   constexpr int TB = tile_bytes<D>(64), STAGE = 2 * TB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
 
   const int L = a.L;
   int qt, hg, b;
-  block_coords((L + 63) / 64, a.Hq / NH, qt, hg, b);
+  block_coords((L + QT - 1) / QT, a.Hq / NH, qt, hg, b);
   const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int h = hg * NH + (w >> 2), wq = w & 3;
   const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int qi = qt * 64 + 16 * wq + c;
-  const bool qvalid = qi < L;
+  int qi[QW];
+  bool qvalid[QW];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    qi[u] = qt * QT + 64 * u + 16 * wq + c;
+    qvalid[u] = qi[u] < L;
+  }
   const bool window_free = a.sliding_window <= 0 || a.sliding_window >= L;
 
   const bf16_t* qbase = (const bf16_t*)a.q + (int64_t)b * L * a.ldq + (int64_t)h * D;
@@ -247,31 +293,41 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
 
   load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 64 * NW);
-  bf16x8 qf[NKS];
-  load_row_frags<D>(qf, qbase + (int64_t)qi * a.ldq, qvalid, lane);
+  bf16x8 qf[QW][NKS];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) load_row_frags<D>(qf[u], qbase + (int64_t)qi[u] * a.ldq, qvalid[u], lane);
   const int nkt = (L + 63) / 64;
   glds_tile<RS, 64, NW>(smem, kbase, a.ldk, L, D, w, lane);
   glds_tile<RS, 64, NW>(smem + TB, vbase, a.ldv, L, D, w, lane);
-  // BIAS: this lane's bias row (its query) is read one key tile ahead into registers (keys 16nt + 4g .. +3 of the
-  // tile; 8 B per nt, zero beyond the padded row): the loads of tile kt+1 are in flight during tile kt
-  const bf16_t* brow = nullptr;
-  u32x2 bnext[4];
+  // BIAS: this lane's bias rows (its queries) are read one key tile ahead into registers (keys 16nt + 4g .. +3 of
+  // the tile; 8 B per nt, zero beyond the padded row): the loads of tile kt+1 are in flight during tile kt
+  const bf16_t* brow[QW];
+  u32x2 bnext[QW][4];
   auto bias_fetch = [&](int kt_) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int k = kt_ * 64 + 16 * nt + 4 * g;
-      bnext[nt] = k < a.bias_ld ? *reinterpret_cast<const u32x2*>(brow + k) : u32x2{0u, 0u};
-    }
+    for (int u = 0; u < QW; ++u)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int k = kt_ * 64 + 16 * nt + 4 * g;
+        bnext[u][nt] = k < a.bias_ld ? *reinterpret_cast<const u32x2*>(brow[u] + k) : u32x2{0u, 0u};
+      }
   };
   if constexpr (BIAS) {
-    brow = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid ? qi : 0)) * a.bias_ld;
+#pragma unroll
+    for (int u = 0; u < QW; ++u)
+      brow[u] = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid[u] ? qi[u] : 0)) * a.bias_ld;
     bias_fetch(0);
   }
 
-  f32x4 acc[NDT];
+  f32x4 acc[QW][NDT];
+  float m[QW], l[QW];
 #pragma unroll
-  for (int i = 0; i < NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int u = 0; u < QW; ++u) {
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) acc[u][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+  }
   const float LOG2E = 1.4426950408889634f;
   const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
 
@@ -287,12 +343,13 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
       glds_tile<RS, 64, NW>(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
     }
     const bool plain = tile_plain(lcls, kt * 64, L, window_free, lane);
-    f32x4 s[4];
-    {  // K fragments of k-step ks+1 are read while k-step ks multiplies (double-buffered, 32 VGPRs)
+    f32x4 s[QW][4];
+    {  // K fragments of k-step ks+1 are read while k-step ks multiplies (double-buffered)
       bf16x8 kb[2][4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        s[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < QW; ++u) s[u][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
         kb[0][nt] = frag_row<RS>(ldsK, 16 * nt, 0, lane);
       }
 #pragma unroll
@@ -304,101 +361,113 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
-          s[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[ks & 1][nt], qf[ks], s[nt], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < QW; ++u)
+            s[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kb[ks & 1][nt], qf[u][ks], s[u][nt], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    float p[4][4];
-    if constexpr (CAP) {
-      float ps = 0.f;
+    float bb[QW][4][4];  // additive score bias (BEiT relative position bias), rows qi[u], keys 16nt + 4g + j
+    if constexpr (BIAS) {
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float e = ce.lg2p(ce.r(s[nt][j]));
-          if (!plain) {
-            const int kj = kt * 64 + 16 * nt + 4 * g + j;
-            if (!visible(lcls[kj], kj, qi, a.sliding_window)) e = MASKED_LG2P;
-            if (kj >= L) e = -INFINITY;
-          }
-          p[nt][j] = __builtin_amdgcn_exp2f(e);
-          ps += p[nt][j];
-        }
-      l += ps;
-    } else {
-      float x[4][4];
-      float mt = -INFINITY;
-      float bb[4][4];  // additive score bias (BEiT relative position bias), row qi, keys 16nt + 4g + j of tile kt
-      if constexpr (BIAS) {
+      for (int u = 0; u < QW; ++u)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const u32x2 w2 = bnext[nt];
-          bb[nt][0] = __uint_as_float(w2[0] << 16); bb[nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
-          bb[nt][2] = __uint_as_float(w2[1] << 16); bb[nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
+          const u32x2 w2 = bnext[u][nt];
+          bb[u][nt][0] = __uint_as_float(w2[0] << 16); bb[u][nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
+          bb[u][nt][2] = __uint_as_float(w2[1] << 16); bb[u][nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
         }
-        if (kt + 1 < nkt) bias_fetch(kt + 1);
+      if (kt + 1 < nkt) bias_fetch(kt + 1);
+    }
+    bf16x8 pb[2][QW];  // P of key halves 0 / 1 (the B operands of the PV products)
+#pragma unroll
+    for (int u = 0; u < QW; ++u) {
+      float p[4][4];
+      if constexpr (CAP) {
+        float ps = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float e = ce.lg2p(ce.r(s[u][nt][j]));
+            if (!plain) {
+              const int kj = kt * 64 + 16 * nt + 4 * g + j;
+              if (!visible(lcls[kj], kj, qi[u], a.sliding_window)) e = MASKED_LG2P;
+              if (kj >= L) e = -INFINITY;
+            }
+            p[nt][j] = __builtin_amdgcn_exp2f(e);
+            ps += p[nt][j];
+          }
+        l[u] += ps;
+      } else {
+        float x[4][4];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = s[u][nt][j] * (a.scale * LOG2E);  // log2 domain
+            if constexpr (BIAS) v = fmaf(bb[u][nt][j], LOG2E, v);
+            if (!plain) {
+              const int kj = kt * 64 + 16 * nt + 4 * g + j;
+              if (kj >= L) v = -INFINITY;
+              else if (!visible(lcls[kj], kj, qi[u], a.sliding_window)) v = MASKVAL;
+            }
+            x[nt][j] = v;
+            mt = fmaxf(mt, v);
+          }
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float mnew = fmaxf(m[u], mt);
+        const float alpha = __builtin_amdgcn_exp2f(m[u] - mnew);  // m=-inf -> 0
+        float ps = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            p[nt][j] = __builtin_amdgcn_exp2f(x[nt][j] - mnew);
+            ps += p[nt][j];
+          }
+        l[u] = l[u] * alpha + ps;
+        m[u] = mnew;
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) acc[u][i] *= alpha;
       }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = s[nt][j] * (a.scale * LOG2E);  // log2 domain
-          if constexpr (BIAS) v = fmaf(bb[nt][j], LOG2E, v);
-          if (!plain) {
-            const int kj = kt * 64 + 16 * nt + 4 * g + j;
-            if (kj >= L) v = -INFINITY;
-            else if (!visible(lcls[kj], kj, qi, a.sliding_window)) v = MASKVAL;
-          }
-          x[nt][j] = v;
-          mt = fmaxf(mt, v);
-        }
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mnew = fmaxf(m, mt);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m=-inf -> 0
-      float ps = 0.f;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          p[nt][j] = __builtin_amdgcn_exp2f(x[nt][j] - mnew);
-          ps += p[nt][j];
-        }
-      l = l * alpha + ps;
-      m = mnew;
-#pragma unroll
-      for (int i = 0; i < NDT; ++i) acc[i] *= alpha;
+      for (int ks = 0; ks < 2; ++ks) {
+        float pv[8] = {p[2 * ks][0], p[2 * ks][1], p[2 * ks][2], p[2 * ks][3],
+                       p[2 * ks + 1][0], p[2 * ks + 1][1], p[2 * ks + 1][2], p[2 * ks + 1][3]};
+        pb[ks][u] = pack_frag(pv);
+      }
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      float pv[8] = {p[2 * ks][0], p[2 * ks][1], p[2 * ks][2], p[2 * ks][3],
-                     p[2 * ks + 1][0], p[2 * ks + 1][1], p[2 * ks + 1][2], p[2 * ks + 1][3]};
-      const bf16x8 pb = pack_frag(pv);
-      mfma_tr_sweep<RS, NDT, true>(acc, ldsV, 32 * ks, pb, lane);
-    }
+    for (int ks = 0; ks < 2; ++ks) mfma_tr_sweep_q<RS, NDT, QW>(acc, ldsV, 32 * ks, pb[ks], lane);
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  const float inv = 1.0f / l;
-  // natural-log lse of the scores (CAP: of p = exp(t) directly; else of the max-shifted log2-domain sum)
-  if (qvalid && g == 0) lse[((int64_t)b * a.Hq + h) * L + qi] = CAP ? __logf(l) : (m + __log2f(l)) / LOG2E;
-
-  // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [16 q][DV + 16] -> 16-B stores.
+  // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [QW*16 q][DV + 16] -> 16-B stores.
   // The 16-element row pad puts the 16 query rows of one 8-B store 32 B apart (an unpadded DV = 256 row stride
   // maps all 16 onto the same two banks: a 16-way conflict on every store).
   constexpr int IS = DV + 16;
   __syncthreads();
-  bf16_t* img = (bf16_t*)(smem) + w * 16 * IS;
+  bf16_t* img = (bf16_t*)(smem) + w * QW * 16 * IS;
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) {
-    uint32_t lo = pack2(acc[dt][0] * inv, acc[dt][1] * inv), hi = pack2(acc[dt][2] * inv, acc[dt][3] * inv);
-    *reinterpret_cast<u32x2*>(img + c * IS + 16 * dt + 4 * g) = u32x2{lo, hi};
+  for (int u = 0; u < QW; ++u) {
+    float lu = l[u];
+    lu += __shfl_xor(lu, 16, 64);
+    lu += __shfl_xor(lu, 32, 64);
+    const float inv = 1.0f / lu;
+    // natural-log lse of the scores (CAP: of p = exp(t) directly; else of the max-shifted log2-domain sum)
+    if (qvalid[u] && g == 0) lse[((int64_t)b * a.Hq + h) * L + qi[u]] = CAP ? __logf(lu) : (m[u] + __log2f(lu)) / LOG2E;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      uint32_t lo = pack2(acc[u][dt][0] * inv, acc[u][dt][1] * inv), hi = pack2(acc[u][dt][2] * inv, acc[u][dt][3] * inv);
+      *reinterpret_cast<u32x2*>(img + (16 * u + c) * IS + 16 * dt + 4 * g) = u32x2{lo, hi};
+    }
   }
   __syncthreads();
   constexpr int CPR = D / 8;  // 16-B chunks per output row
-  for (int idx = lane; idx < 16 * CPR; idx += 64) {
+  for (int idx = lane; idx < QW * 16 * CPR; idx += 64) {
     const int r = idx / CPR, ch = idx % CPR;
-    const int q = qt * 64 + 16 * wq + r;
+    const int q = qt * QT + 64 * (r >> 4) + 16 * wq + (r & 15);
     if (q < L)
       *reinterpret_cast<u32x4*>(out + ((int64_t)b * L + q) * ldo + (int64_t)h * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(img + r * IS + ch * 8);
@@ -757,14 +826,16 @@ int check_args(const svla_attn_args* a) {
 
 int round16(int x) { return (x + 15) & ~15; }
 
-template <int D, int NH, bool CAP, bool BIAS = false>
+template <int D, int NH, bool CAP, bool BIAS = false, int QW = 1>
 int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
   const int lds = 4 * tile_bytes<D>(64) + round16(a.L);
+  static_assert(4 * NH * QW * 16 * (Cfg<D>::DV + 16) * 2 <= 4 * tile_bytes<D>(64), "output image must fit");
   SVLA_CHECK_ARG(lds <= 160 * 1024, "attn_fwd: L too large for the LDS-resident key classes");
-  const int64_t nblk = (int64_t)((a.L + 63) / 64) * (a.Hq / NH) * a.B;
+  const int64_t nblk = (int64_t)((a.L + 64 * QW - 1) / (64 * QW)) * (a.Hq / NH) * a.B;
   SVLA_CHECK_ARG(nblk < (1LL << 31), "attn_fwd: grid too large");
-  set_lds_once<attn_fwd_kernel<D, NH, CAP, BIAS>>(lds);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NH, CAP, BIAS>), dim3((unsigned)nblk), dim3(256 * NH), lds, s, a, out, ldo, lse);
+  set_lds_once<attn_fwd_kernel<D, NH, CAP, BIAS, QW>>(lds);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NH, CAP, BIAS, QW>), dim3((unsigned)nblk), dim3(256 * NH), lds, s, a, out, ldo,
+                     lse);
   return svla::check_launch("attn_fwd");
 }
 
@@ -807,11 +878,12 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
     if (a->bias) {
       SVLA_CHECK_ARG(a->bias_ld >= (a->L + 7) / 8 * 8 && a->bias_ld % 8 == 0 && ((uintptr_t)a->bias & 15) == 0,
                      "attn_fwd: bias rows must hold round8(L) keys (ld a multiple of 8), 16-B aligned");
-      return fwd_launch<64, 1, false, true>(*a, o, ldo, lse, s);
+      return fwd_launch<64, 1, false, true, SVLA_ATT_QW>(*a, o, ldo, lse, s);
     }
-    return fwd_launch<64, 1, false>(*a, o, ldo, lse, s);
+    return fwd_launch<64, 1, false, false, SVLA_ATT_QW>(*a, o, ldo, lse, s);
   }
-  return cap ? fwd_launch<72, 1, true>(*a, o, ldo, lse, s) : fwd_launch<72, 1, false>(*a, o, ldo, lse, s);
+  return cap ? fwd_launch<72, 1, true, false, SVLA_ATT_QW>(*a, o, ldo, lse, s)
+             : fwd_launch<72, 1, false, false, SVLA_ATT_QW>(*a, o, ldo, lse, s);
 }
 
 template <int D, int NH>

@@ -247,8 +247,10 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         if pwait is not None:
             pwait("pre")
 
-    def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor, kinv=None):
-        """Reference :308-333 -> [B, np, H_text]."""
+    def get_image_features(self, pixel_values: torch.FloatTensor, intrinsic: torch.FloatTensor, kinv=None,
+                           depth=None):
+        """Reference :308-333 -> [B, np, H_text].  depth: a precomputed Zoe depth (predict_action computes it outside
+        its prefill graph); None = predict it here."""
         self._wait_params()
         dt = self.multi_modal_projector.linear.weight.dtype
         pv = pixel_values.to(dt).contiguous()
@@ -259,7 +261,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         Hv = feats.shape[-1]
         sel = feats.reshape(-1, Hv)
         if self.config.use_vision_zoe:
-            depth = self.predict_depth(pixel_values.to(dt))
+            if depth is None:
+                depth = self.predict_depth(pixel_values.to(dt))
             enc = self.ego3d_features(intrinsic, depth, kinv)  # kinv: precomputed outside a graph capture
             sel = self.position_embedding_3d.forward_residual(enc, sel)
         lin = self.multi_modal_projector.linear
@@ -513,7 +516,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
     def _prefill_body(self, st, x):
         """Vision tower + Ego3D/Zoe + Gemma2 prefill over the prompt (filling the cache) + the first greedy token."""
         ids, cache = x["ids"], st["cache"]
-        feats = self.get_image_features(x["pv"], x["intr"], x["kinv"]) if x["pv"] is not None else None
+        feats = (self.get_image_features(x["pv"], x["intr"], x["kinv"], x.get("depth")) if x["pv"] is not None
+                 else None)
         pos = (torch.arange(ids.shape[1], device=ids.device) + 1)[None]
         strict, self.strict_checks = self.strict_checks, False  # checked on the host by predict_action
         try:
@@ -545,7 +549,9 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(graph, pool=st["pool"]):
+                # captured on the warm-up stream: the per-stream handles of the libraries the frozen Zoe forward still
+                # calls (MIOpen and the GEMM back end it uses at B=1) exist there, none is created under capture
+                with torch.cuda.graph(graph, pool=st["pool"], stream=side):
                     out = self._prefill_body(st, static)
             except RuntimeError as e:  # an op of the prefill cannot be captured: run this shape eagerly from now on
                 cache.seen_tokens = 0
@@ -589,7 +595,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             cache.seen_tokens = p0
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, pool=st["pool"]):
+            with torch.cuda.graph(graph, pool=st["pool"], stream=side):  # on the warm-up stream, as the prefill
                 out = self._decode_body(st, p0)
             cache.seen_tokens = p0
             g = st["graphs"][p0] = (graph, out)
@@ -623,6 +629,11 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         # inv(K) (reference :221): the closed-form HIP inverse, captured into the prefill graph with the rest
         kinv = None
         prefill = {"ids": ids, "pv": pv, "intr": intr, "cls": cls, "kinv": kinv}
+        if graphs and pv is not None and self.config.use_vision_zoe:
+            # the frozen Zoe forward runs eagerly, ahead of the prefill graph: its DPT neck is still MIOpen
+            # convolutions, whose B=1 solvers create vendor-library handles lazily -- not capturable
+            dt = self.multi_modal_projector.linear.weight.dtype
+            prefill["depth"] = self.predict_depth(pv.to(dt))
         first = self._prefill_graph(st, prefill) if graphs else self._prefill_body(st, prefill)
         cache.seen_tokens = P
         finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
