@@ -25,6 +25,9 @@
 #ifndef SVLA_ATT_QW
 #define SVLA_ATT_QW 2  // query sub-tiles per wave of the forward at head_dim 64 / 72 (variant builds: 1)
 #endif
+#ifndef SVLA_ATT_QW256
+#define SVLA_ATT_QW256 1  // head_dim 256 forward: 1 = head pairs (NH 2), 16 queries per wave; 2 = one head, 32 per wave
+#endif
 
 namespace {
 
@@ -869,6 +872,9 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
   bf16_t* o = (bf16_t*)out;
   SVLA_CHECK_ARG(!a->bias || a->D == 64, "attn_fwd: an additive bias is only supported with head_dim 64");
   if (a->D == 256) {
+    if (SVLA_ATT_QW256 == 2)
+      return cap ? fwd_launch<256, 1, true, false, 2>(*a, o, ldo, lse, s)
+                 : fwd_launch<256, 1, false, false, 2>(*a, o, ldo, lse, s);
     if (pair) return cap ? fwd_launch<256, 2, true>(*a, o, ldo, lse, s) : fwd_launch<256, 2, false>(*a, o, ldo, lse, s);
     return cap ? fwd_launch<256, 1, true>(*a, o, ldo, lse, s) : fwd_launch<256, 1, false>(*a, o, ldo, lse, s);
   }
