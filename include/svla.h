@@ -121,10 +121,15 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
  * scales, fp32 accumulate).  Replaces the bf16 forward nn.Linear of Gemma2 q/k/v/o and gate/up/down
  * (model/modeling_gemma2.py:86-92, 351-354, 376-408) when fp8 projections are enabled; the backward stays bf16.
  * ---------------------------------------------------------------------------------------- */
-/* Row-wise quantisation: scale[r] = amax_r/448, q[r,k] = e4m3(clamp(x[r,k]*448/amax_r, +-448)) (RNE; a zero row
- * gives q = 0, scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0, K <= 9216. */
-int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq, float* scale,
-                        void* stream);
+/* Row-wise quantisation: x'[r,k] = x[r,k] * colscale[k] (colscale fp32 [K], 16-B aligned, or NULL = 1);
+ * scale[r] = amax_r(x')/448, q[r,k] = e4m3(clamp(x'[r,k]*448/amax_r, +-448)) (RNE; a zero row gives q = 0,
+ * scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0, K <= 18432 (the dgrad GEMMs quantise dY with
+ * colscale = the row scales of the forward fp8 weight, so the weight's transposed e4m3 copy is reused as is). */
+int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, const float* colscale, void* q,
+                        int64_t ldq, float* scale, void* stream);
+/* Byte transpose out[c][r] = in[r][c] of an R x C matrix (the e4m3 weight copies for the dgrad GEMMs).
+ * ldi % 16 == 0, ldo % 4 == 0, 16-B aligned input. */
+int svla_transpose_u8(int64_t R, int64_t C, const void* in, int64_t ldi, void* out, int64_t ldo, void* stream);
 /* C[M,N] = epilogue( a_scale[m] * b_scale[n] * sum_k A(m,k) B(n,k) ) with A, B e4m3 KC operands (ld in bytes, a
  * multiple of 16; K and k_valid multiples of 16; A one segment; B one segment, or two SVLA_SEG_GEGLU segments of
  * N/2 rows with SVLA_EPI_GEGLU, b_scale then [N]: gate rows then up rows).  Scales fp32, 16-B aligned.  Epilogues

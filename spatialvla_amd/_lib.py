@@ -65,7 +65,8 @@ SIGNATURES = {
     "svla_gemm_bf16_ex": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), ctypes.POINTER(Operand),
                                   ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64,
                                   ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t, c_i32, c_vp]),
-    "svla_quant_fp8_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "svla_quant_fp8_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "svla_transpose_u8": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "svla_gemm_fp8": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), c_vp, ctypes.POINTER(Operand), c_vp,
                               ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64, ctypes.POINTER(Epilogue), c_vp,
                               ctypes.c_size_t, c_vp]),

@@ -15,7 +15,8 @@ __device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
 
 template <int NCH>
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(int64_t rows, int64_t K, const bf16_t* __restrict__ x,
-                                                             int64_t ldx, uint8_t* __restrict__ q, int64_t ldq,
+                                                             int64_t ldx, const float* __restrict__ colscale,
+                                                             uint8_t* __restrict__ q, int64_t ldq,
                                                              float* __restrict__ scale) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -30,6 +31,11 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(int64_t rows, int64
     v[c] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xr + k)) : u32x4{0, 0, 0, 0};
     float f[8];
     unpack8(v[c], f);
+    if (colscale && k < K) {
+      const f32x4 s0 = *reinterpret_cast<const f32x4*>(colscale + k), s1 = *reinterpret_cast<const f32x4*>(colscale + k + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] *= s0[j]; f[4 + j] *= s1[j]; }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(f[j]));
   }
@@ -42,6 +48,11 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(int64_t rows, int64
     if (k < K) {
       float f[8];
       unpack8(v[c], f);
+      if (colscale) {
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(colscale + k), s1 = *reinterpret_cast<const f32x4*>(colscale + k + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { f[j] *= s0[j]; f[4 + j] *= s1[j]; }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -448.f), 448.f);
       const u32x2 o = {cvt4(f[0], f[1], f[2], f[3]), cvt4(f[4], f[5], f[6], f[7])};
@@ -50,22 +61,78 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(int64_t rows, int64
   }
 }
 
+// Byte transpose out[c][r] = in[r][c] through a 64x64 LDS tile (fp8 weight copies for the dgrad GEMMs): 16-B
+// row-chunk loads, 4-B column-chunk stores; the tile's LDS rows are padded by 4 B against bank conflicts.
+__global__ __launch_bounds__(256) void transpose_u8_kernel(int64_t R, int64_t C, const uint8_t* __restrict__ in,
+                                                           int64_t ldi, uint8_t* __restrict__ out, int64_t ldo) {
+  __shared__ uint8_t tile[64][68];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x;
+  {  // 64 rows x 4 chunks of 16 B
+    const int r = t >> 2, ch = t & 3;
+    const int64_t gr = r0 + r, gc = c0 + 16 * ch;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (gr < R && gc + 16 <= C) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(in + gr * ldi + gc);
+      w[0] = v[0]; w[1] = v[1]; w[2] = v[2]; w[3] = v[3];
+    } else if (gr < R) {
+      for (int j = 0; j < 16; ++j)
+        if (gc + j < C) w[j >> 2] |= (uint32_t)in[gr * ldi + gc + j] << (8 * (j & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint32_t*>(&tile[r][16 * ch + 4 * j]) = w[j];
+  }
+  __syncthreads();
+  {  // 64 output rows (input columns) x 16 chunks of 4 B (input rows)
+    const int c = t >> 2;
+#pragma unroll
+    for (int part = 0; part < 4; ++part) {
+      const int rq = (t & 3) * 4 + part;  // 4-row group 0..15
+      const int64_t oc = c0 + c, orr = r0 + 4 * rq;
+      if (oc < C) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)tile[4 * rq + j][c] << (8 * j);
+        if (orr + 4 <= R) *reinterpret_cast<uint32_t*>(out + oc * ldo + orr) = w;
+        else
+          for (int j = 0; j < 4; ++j)
+            if (orr + j < R) out[oc * ldo + orr + j] = (uint8_t)(w >> (8 * j));
+      }
+    }
+  }
+}
+
 }  // namespace
 
-extern "C" int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq,
-                                   float* scale, void* stream) {
-  SVLA_CHECK_ARG(rows > 0 && K > 0 && K % 8 == 0 && K <= 64 * 8 * 18, "quant_fp8_rows: K=%lld (multiple of 8, <= 9216)",
+extern "C" int svla_transpose_u8(int64_t R, int64_t C, const void* in, int64_t ldi, void* out, int64_t ldo,
+                                 void* stream) {
+  SVLA_CHECK_ARG(R > 0 && C > 0 && in && out && ldi >= C && ldo >= R && ldi % 16 == 0 && ldo % 4 == 0 &&
+                     ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 3) == 0,
+                 "transpose_u8: sizes / pointers (ldi % 16, ldo % 4, 16-B aligned input)");
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64)), block(256);
+  hipLaunchKernelGGL(transpose_u8_kernel, grid, block, 0, (hipStream_t)stream, R, C, (const uint8_t*)in, ldi,
+                     (uint8_t*)out, ldo);
+  return svla::check_launch("transpose_u8");
+}
+
+extern "C" int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, const float* colscale,
+                                   void* q, int64_t ldq, float* scale, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && K > 0 && K % 8 == 0 && K <= 64 * 8 * 36, "quant_fp8_rows: K=%lld (multiple of 8, <= 18432)",
                  (long long)K);
   SVLA_CHECK_ARG(x && q && scale && ldx >= K && ldq >= K && ldx % 8 == 0 && ldq % 8 == 0 &&
                      ((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 7) == 0,
                  "quant_fp8_rows: pointers / leading dimensions");
+  SVLA_CHECK_ARG(!colscale || ((uintptr_t)colscale & 15) == 0, "quant_fp8_rows: colscale must be 16-B aligned");
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   hipStream_t s = (hipStream_t)stream;
   if (K <= 64 * 8 * 5)
-    hipLaunchKernelGGL(quant_fp8_rows_kernel<5>, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, (uint8_t*)q, ldq,
-                       scale);
+    hipLaunchKernelGGL(quant_fp8_rows_kernel<5>, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, colscale,
+                       (uint8_t*)q, ldq, scale);
+  else if (K <= 64 * 8 * 18)
+    hipLaunchKernelGGL(quant_fp8_rows_kernel<18>, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, colscale,
+                       (uint8_t*)q, ldq, scale);
   else
-    hipLaunchKernelGGL(quant_fp8_rows_kernel<18>, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, (uint8_t*)q, ldq,
-                       scale);
+    hipLaunchKernelGGL(quant_fp8_rows_kernel<36>, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, colscale,
+                       (uint8_t*)q, ldq, scale);
   return svla::check_launch("quant_fp8_rows");
 }

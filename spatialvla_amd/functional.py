@@ -234,6 +234,8 @@ class LinearFn(torch.autograd.Function):
 # Bumped by TrainEngine.optimizer_step: AdamW rewrites the bf16 weights through the C-ABI, which torch's version
 # counters do not see, so the fp8 weight copies compare this epoch as well.
 WEIGHT_EPOCH = [0]
+# fp8 projections: the input-gradient (dgrad) GEMMs run in e4m3 too (the weight-gradient GEMMs stay bf16)
+FP8_DGRAD = [True]
 
 
 class FP8Weights:
@@ -255,9 +257,24 @@ class FP8Weights:
         hit = self.mats.get(name)
         if hit is None or hit[0] != key:
             q, s = K.quant_fp8_rows(self._rows(mats))
-            hit = (key, q, s)
+            hit = (key, q, s, None)
             self.mats[name] = hit
         return hit[1], hit[2]
+
+    def get_t(self, name, mats):
+        """(W_q^T [K, N] e4m3, the row scales s [N] of W_q): the byte transpose of the forward copy, for dgrad."""
+        self.get(name, mats)
+        key, q, s, qt = self.mats[name]
+        if qt is None:
+            qt = K.transpose_u8(q)
+            self.mats[name] = (key, q, s, qt)
+        return qt, s
+
+    def ones(self, n, device):
+        o = self.mats.get(("ones", n))
+        if o is None:
+            o = self.mats[("ones", n)] = torch.ones(n, dtype=torch.float32, device=device)
+        return o
 
 
 def _fp8_linear(x, f8, name, mats, out, **kw):
@@ -265,6 +282,15 @@ def _fp8_linear(x, f8, name, mats, out, **kw):
     xq, xs = K.quant_fp8_rows(x)
     wq, ws = f8.get(name, mats)
     K.gemm_fp8(xq, xs, wq, ws, out, **kw)
+
+
+def _fp8_dgrad(dy, f8, name, mats, out):
+    """out[M, K] = dy[M, N] @ cat(mats)[N, K] on the fp8 GEMM.  The forward's e4m3 weight W ~ diag(s_w) W_q is
+    reused transposed: dy's columns are scaled by s_w before dy is quantised per row, so
+    out = s_dy[m] * sum_n q_dy[m, n] W_q[n, k] -- one e4m3 GEMM against the byte-transposed W_q."""
+    wt, sw = f8.get_t(name, mats)
+    dq, ds = K.quant_fp8_rows(dy, colscale=sw)
+    K.gemm_fp8(dq, ds, wt, f8.ones(wt.shape[0], dy.device), out)
 
 
 # ------------------------------------------------------------------------------------ Gemma2 blocks
@@ -310,6 +336,7 @@ class GemmaAttentionFn(torch.autograd.Function):
             K.linear_fwd(attn, [wo], out)
         ctx.save_for_backward(x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class)
         ctx.cfg = cfg
+        ctx.f8 = f8
         return out
 
     @staticmethod
@@ -320,7 +347,11 @@ class GemmaAttentionFn(torch.autograd.Function):
         M = x.shape[0]
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         dattn = _empty(M, qd, like=x)
-        K.linear_dgrad(dout, [wo], dattn)
+        f8 = ctx.f8 if FP8_DGRAD[0] else None
+        if f8 is not None:
+            _fp8_dgrad(dout, f8, "o", (wo,), dattn)
+        else:
+            K.linear_dgrad(dout, [wo], dattn)
         dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
         if dwo is not None:
             K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
@@ -333,7 +364,10 @@ class GemmaAttentionFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            K.linear_dgrad(dqkv, [wq, wk, wv], dx)
+            if f8 is not None:
+                _fp8_dgrad(dqkv, f8, "qkv", (wq, wk, wv), dx)
+            else:
+                K.linear_dgrad(dqkv, [wq, wk, wv], dx)
         rets = []
         dests = [_grad_dest(w, ctx.needs_input_grad[1 + i]) for i, w in enumerate((wq, wk, wv))]
         if all(d[0] is not None for d in dests) and len({d[1] for d in dests}) == 1:
@@ -404,6 +438,7 @@ class GemmaMLPFn(torch.autograd.Function):
             K.linear_geglu_fwd(x, wg, wu, h, g, u)
             K.linear_fwd(h, [wd], out)
         ctx.save_for_backward(x, wg, wu, wd, g, u, h)
+        ctx.f8 = f8
         return out
 
     @staticmethod
@@ -417,12 +452,19 @@ class GemmaMLPFn(torch.autograd.Function):
         dgu = _empty(M, 2 * I, like=x)
         # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (measured in the training
         # step: the GEGLU_BWD GEMM epilogue cost +60% over the plain dgrad, the separate pass ~0.17 ms)
-        K.linear_dgrad(dout, [wd], dgu[:, :I])
+        f8 = ctx.f8 if FP8_DGRAD[0] else None
+        if f8 is not None:
+            _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
+        else:
+            K.linear_dgrad(dout, [wd], dgu[:, :I])
         K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            K.linear_dgrad(dgu, [wg, wu], dx)
+            if f8 is not None:
+                _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx)
+            else:
+                K.linear_dgrad(dgu, [wg, wu], dx)
         dg_, accg, retg = _grad_dest(wg, ctx.needs_input_grad[1])
         du_, accu, retu = _grad_dest(wu, ctx.needs_input_grad[2])
         if dg_ is not None and du_ is not None and accg == accu:

@@ -249,9 +249,10 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, outs: List[torch.Tensor], ac
 FP8 = torch.float8_e4m3fn
 
 
-def quant_fp8_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None):
-    """Row-wise OCP e4m3 quantisation (svla_quant_fp8_rows): q = e4m3(clamp(x * 448/amax_row)), scale = amax_row/448.
-    Returns (q [rows, K] float8_e4m3fn, scale [rows] fp32)."""
+def quant_fp8_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+                   colscale: Optional[torch.Tensor] = None):
+    """Row-wise OCP e4m3 quantisation (svla_quant_fp8_rows) of x * colscale (colscale fp32 [K] or None):
+    q = e4m3(clamp(x' * 448/amax_row)), scale = amax_row/448.  Returns (q [rows, K] float8_e4m3fn, scale [rows])."""
     _chk_bf16(x, "quant_fp8_rows")
     rows, K = x.shape
     if q is None:
@@ -260,9 +261,24 @@ def quant_fp8_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Opt
         scale = torch.empty(rows, dtype=torch.float32, device=x.device)
     _req(q.dtype == FP8 and q.shape == (rows, K) and q.stride(1) == 1, "quant_fp8_rows: q must be [rows, K] e4m3")
     _req(scale.dtype == torch.float32 and scale.numel() >= rows and scale.is_contiguous(), "quant_fp8_rows: scale")
-    L.check(L.lib().svla_quant_fp8_rows(rows, K, x.data_ptr(), _ld(x), q.data_ptr(), q.stride(0), scale.data_ptr(),
-                                        _stream()), "svla_quant_fp8_rows")
+    if colscale is not None:
+        _req(colscale.dtype == torch.float32 and colscale.is_contiguous() and colscale.numel() >= K,
+             "quant_fp8_rows: colscale must be a contiguous fp32 [K]")
+    L.check(L.lib().svla_quant_fp8_rows(rows, K, x.data_ptr(), _ld(x), _ptr(colscale), q.data_ptr(), q.stride(0),
+                                        scale.data_ptr(), _stream()), "svla_quant_fp8_rows")
     return q, scale
+
+
+def transpose_u8(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[c, r] = x[r, c] for a 1-byte-element matrix (e4m3 weight copies), svla_transpose_u8."""
+    _req(x.is_cuda and x.element_size() == 1 and x.dim() == 2 and x.stride(1) == 1, "transpose_u8: 1-byte matrix")
+    R, C = x.shape
+    if out is None:
+        out = torch.empty(C, R, dtype=x.dtype, device=x.device)
+    _req(out.shape == (C, R) and out.stride(1) == 1 and out.element_size() == 1, "transpose_u8: out must be [C, R]")
+    L.check(L.lib().svla_transpose_u8(R, C, x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), _stream()),
+            "svla_transpose_u8")
+    return out
 
 
 def _operand_fp8(mats: Sequence[torch.Tensor], seg_dim: int = L.SEG_OUTER, starts=None) -> L.Operand:

@@ -44,6 +44,44 @@ def test_quant_fp8_rows_bitexact(cuda, rows, k):
     assert torch.equal(s.cpu(), sr)
 
 
+def test_quant_fp8_rows_colscale_and_transpose(cuda):
+    """Quantiser with column scales (the dgrad operand) bit-exact to torch; byte transpose exact."""
+    g = torch.Generator(device=cuda).manual_seed(5)
+    for rows, k in ((300, 18432), (37, 4096)):
+        x = torch.randn(rows, k, device=cuda, generator=g).to(BF)
+        cs = torch.rand(k, device=cuda, generator=g) * 0.01 + 1e-4
+        q, s = K.quant_fp8_rows(x, colscale=cs)
+        xr = (x.float() * cs[None, :]).cpu()
+        amax = xr.abs().amax(1)
+        inv = torch.where(amax > 0, torch.tensor(448.0) / amax, torch.zeros_like(amax))
+        qr = (xr * inv[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+        assert torch.equal(q.view(torch.uint8).cpu(), qr.view(torch.uint8)) and torch.equal(s.cpu(), amax / 448.0)
+    for r_, c_ in ((4096, 2304), (2304, 18432), (100, 48)):
+        m = torch.randint(0, 256, (r_, c_), dtype=torch.uint8, device=cuda)
+        assert torch.equal(K.transpose_u8(m), m.t().contiguous())
+
+
+def test_fp8_dgrad_gemm(cuda):
+    """dX = dY @ W on the fp8 path (functional._fp8_dgrad): dY scaled by the forward weight copy's row scales and
+    quantised per row, against the byte-transposed e4m3 weight.  Within 4e-3 of the exact product of the
+    quantised operands, within 6e-2 of the bf16 product."""
+    from spatialvla_amd import functional as Fn
+    g = torch.Generator(device=cuda).manual_seed(8)
+    M, N, Kd = 2000, 18432, 2304
+    dy = torch.randn(M, N, device=cuda, generator=g).to(BF)
+    w = (torch.randn(N, Kd, device=cuda, generator=g) * 0.02).to(BF)
+    f8 = Fn.FP8Weights()
+    out = torch.empty(M, Kd, dtype=BF, device=cuda)
+    Fn._fp8_dgrad(dy, f8, "w", (w,), out)
+    wq, ws = f8.get("w", (w,))
+    dq, ds = K.quant_fp8_rows(dy, colscale=ws)
+    exact = (dq.float() * ds[:, None]) @ wq.float()
+    bf = dy.float() @ w.float()
+    e_k, e_q = rel(out, exact), rel(out, bf)
+    print(f"fp8 dgrad: vs quantised-operand product {e_k:.2e}, vs bf16 {e_q:.2e}")
+    assert e_k < 4e-3 and e_q < 6e-2
+
+
 def _dequant(q, s):
     return q.float() * s[:, None]
 
