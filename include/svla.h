@@ -123,7 +123,7 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
  * ---------------------------------------------------------------------------------------- */
 /* Row-wise quantisation: x'[r,k] = x[r,k] * colscale[k] (colscale fp32 [K], 16-B aligned, or NULL = 1);
  * scale[r] = amax_r(x')/448, q[r,k] = e4m3(clamp(x'[r,k]*448/amax_r, +-448)) (RNE; a zero row gives q = 0,
- * scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0, K <= 18432 (the dgrad GEMMs quantise dY with
+ * scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0 (the dgrad GEMMs quantise dY with
  * colscale = the row scales of the forward fp8 weight, so the weight's transposed e4m3 copy is reused as is). */
 int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, const float* colscale, void* q,
                         int64_t ldq, float* scale, void* stream);

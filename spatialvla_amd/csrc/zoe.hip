@@ -110,19 +110,16 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   const int b = (int)(pix / ((int64_t)a.W * a.H));
   const Tap ty = tap(y, a.h, a.H), tx = tap(x, a.w, a.W);
 
-  // hidden pre-activations as 40 pairs: one v_pk_fma_f32 per two outputs (same per-output fma chain as scalar code)
-  f32x2 h2[HID / 2];
+  float h[HID];
 #pragma unroll
-  for (int o = 0; o < HID / 2; ++o) h2[o] = f32x2{pb1[2 * o], pb1[2 * o + 1]};
-  auto accum1 = [&](float vj, int c) {
-    const f32x2* wr = reinterpret_cast<const f32x2*>(pw1 + c * HID);
-    const f32x2 vv = {vj, vj};
-#pragma unroll
-    for (int o = 0; o < HID / 2; ++o) h2[o] = __builtin_elementwise_fma(wr[o], vv, h2[o]);
-  };
+  for (int o = 0; o < HID; ++o) h[o] = pb1[o];
   auto accum8 = [&](const float* v, int c0) {  // channels c0..c0+7
 #pragma unroll
-    for (int j = 0; j < 8; ++j) accum1(v[j], c0 + j);
+    for (int j = 0; j < 8; ++j) {
+      const float* wr = pw1 + (c0 + j) * HID;
+#pragma unroll
+      for (int o = 0; o < HID; ++o) h[o] += wr[o] * v[j];
+    }
   };
   // main feature (CF channels, CF % 8 == 0) and the relative depth
   {
@@ -135,7 +132,9 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
       accum8(v, c);
     }
     const float r = bf2f(a.rel[(int64_t)b * a.rs[0] + y * a.rs[1] + x * a.rs[2]]);
-    accum1(r, a.CF);
+    const float* wr = pw1 + a.CF * HID;
+#pragma unroll
+    for (int o = 0; o < HID; ++o) h[o] += wr[o] * r;
   }
   // bilinear-upsampled bin embedding (CE channels, CE % 8 == 0)
   {
@@ -160,7 +159,7 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   float s4[4] = {pb2[0], pb2[1], pb2[2], pb2[3]};
 #pragma unroll
   for (int o = 0; o < HID; ++o) {
-    const float g = round_bf(gelu_erf(round_bf(h2[o >> 1][o & 1])));
+    const float g = round_bf(gelu_erf(round_bf(h[o])));
 #pragma unroll
     for (int q = 0; q < 4; ++q) s4[q] += pw2[q * HID + o] * g;
   }

@@ -37,6 +37,8 @@ g = torch.Generator(device=dev).manual_seed(5)
 x = torch.randn(B, L, cfg.hidden_size, device=dev, generator=g).to(torch.bfloat16).requires_grad_(True)
 gy = torch.randn(B, L, cfg.hidden_size, device=dev, generator=g).to(torch.bfloat16)
 Slot = Fn.ResidualSlot
+if os.environ.get("SVLA_BLOCK_FP8"):  # BASELINE configs[4]: fp8 projections (forward + dgrad)
+    layer.set_fp8_projections(True)
 
 
 def run(use_slot, iters=10):

@@ -18,6 +18,6 @@ tot = 0
 for r in it:
     dd = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     tot += dd
-    n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", ""))[:70]
+    n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", ""))[:70]
     print(f"{dd:9.1f} us  grid={int(r['Grid_Size_X']):>9} wg={r['Workgroup_Size_X']:>4}  {n}")
 print(f"iteration: {P} kernels, wall {(t1 - t0) / 1e3:.1f} us, kernel sum {tot:.1f} us")
