@@ -95,66 +95,116 @@ __device__ __forceinline__ void load8(const bf16_t* p, int64_t stride, bool vec,
   }
 }
 
+// The hidden layer (CF+1+CE -> 80 1x1 conv, 98 % of the tail's FLOPs) runs on MFMA: a block owns 256 output pixels,
+// each wave 64 of them as 4 groups of 16; the conv's input channels are permuted (feat 0..CF-1, emb CF.., rel last,
+// zero pad to 192 = 6 k-steps of 32) on both operands, the weights are staged once per block in LDS in fragment
+// order (bf16, exact: the module's weights are bf16), and every lane gathers the 8 channels of its (pixel, k-step)
+// A fragment straight from the inputs (16-B loads, the bin embedding bilinearly interpolated and rounded to bf16 as
+// the reference's upsampled tensor).  bf16(h + b1) goes through LDS back to one thread per pixel for the rest.
+constexpr int KP = 192, KS = KP / 32, NT = HID / 16, HS_LD = HID + 8;
+constexpr int ZT_LDS = KS * NT * 64 * 16 + 256 * HS_LD * 2;
+
 __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const float* __restrict__ prm) {
+  extern __shared__ __attribute__((aligned(16))) char zsm[];
+  bf16_t* wl = (bf16_t*)zsm;                              // [KS][NT][64 lanes][8] B fragments
+  bf16_t* hs = (bf16_t*)(zsm + KS * NT * 64 * 16);         // [256 pixels][HS_LD] bf16(h + b1)
   const int CIN = a.CF + 1 + a.CE;
   const float* __restrict__ pw1 = prm;
   const float* __restrict__ pw2 = pw1 + CIN * HID;
   const float* __restrict__ pb1 = pw2 + 4 * HID;
   const float* __restrict__ pb2 = pb1 + HID;
   const float* __restrict__ plb = pb2 + 4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t npix = (int64_t)a.B * a.H * a.W;
+  const int64_t pix0 = (int64_t)blockIdx.x * 256;
 
-  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (pix >= (int64_t)a.B * a.H * a.W) return;
+  // permuted channel kk -> row of W1^T (-1: zero pad)
+  auto wrow = [&](int kk) {
+    if (kk < a.CF) return kk;
+    if (kk < a.CF + a.CE) return kk + 1;
+    if (kk == a.CF + a.CE) return a.CF;
+    return -1;
+  };
+  for (int i = t; i < KS * NT * 64; i += 256) {  // fragment (ks, nt, lane): B[k = 32ks + 8(l>>4) + j][o = 16nt + (l&15)]
+    const int l = i & 63, nt = (i >> 6) % NT, ks = (i >> 6) / NT;
+    const int o = 16 * nt + (l & 15);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = wrow(32 * ks + 8 * (l >> 4) + j);
+      v[j] = r >= 0 ? pw1[r * HID + o] : 0.f;
+    }
+    *reinterpret_cast<u32x4*>(wl + i * 8) = pack8(v);
+  }
+  __syncthreads();
+
+  f32x4 hacc[4][NT];
+#pragma unroll
+  for (int pg = 0; pg < 4; ++pg)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) hacc[pg][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g4 = lane >> 4;
+#pragma unroll
+  for (int pg = 0; pg < 4; ++pg) {
+    int64_t pix = pix0 + 64 * w + 16 * pg + (lane & 15);
+    const bool pv = pix < npix;
+    if (!pv) pix = npix - 1;
+    const int x = (int)(pix % a.W), y = (int)((pix / a.W) % a.H), b = (int)(pix / ((int64_t)a.W * a.H));
+    const Tap ty = tap(y, a.h, a.H), tx = tap(x, a.w, a.W);
+    const Taps2 te = taps2(a.es, ty, tx);
+    const bf16_t* fp = a.feat + (int64_t)b * a.fs[0] + y * a.fs[2] + x * a.fs[3];
+    const bf16_t* eb = a.emb + (int64_t)b * a.es[0];
+    const bool vf = a.fs[1] == 1, ve = a.es[1] == 1;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kk = 32 * ks + 8 * g4;  // first permuted channel of this lane's 8
+      float v[8];
+      if (kk < a.CF) {
+        load8(fp + kk * a.fs[1], a.fs[1], vf, v);
+      } else if (kk < a.CF + a.CE) {
+        float q00[8], q01[8], q10[8], q11[8];
+        const bf16_t* pc = eb + (kk - a.CF) * a.es[1];
+        load8(pc + te.o00, a.es[1], ve, q00);
+        load8(pc + te.o01, a.es[1], ve, q01);
+        load8(pc + te.o10, a.es[1], ve, q10);
+        load8(pc + te.o11, a.es[1], ve, q11);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = round_bf(te.ly0 * (te.lx0 * q00[j] + te.lx1 * q01[j]) + te.ly1 * (te.lx0 * q10[j] + te.lx1 * q11[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+        if (kk == a.CF + a.CE) v[0] = bf2f(a.rel[(int64_t)b * a.rs[0] + y * a.rs[1] + x * a.rs[2]]);
+      }
+      const bf16x8 af = __builtin_bit_cast(bf16x8, pack8(v));
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(wl + ((ks * NT + nt) * 64 + lane) * 8);
+        hacc[pg][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, hacc[pg][nt], 0, 0, 0);
+      }
+    }
+  }
+  // C[pixel row 4(l>>4)+i][output 16nt + (l&15)] -> hs[pixel][o] = bf16(h + b1)
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int o = 16 * nt + (lane & 15);
+    const float bias = pb1[o];
+#pragma unroll
+    for (int pg = 0; pg < 4; ++pg)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hs[(64 * w + 16 * pg + 4 * g4 + i) * HS_LD + o] = f2bf(hacc[pg][nt][i] + bias);
+  }
+  __syncthreads();
+
+  const int64_t pix = pix0 + t;
+  if (pix >= npix) return;
   const int x = (int)(pix % a.W);
   const int y = (int)((pix / a.W) % a.H);
   const int b = (int)(pix / ((int64_t)a.W * a.H));
   const Tap ty = tap(y, a.h, a.H), tx = tap(x, a.w, a.W);
-
   float h[HID];
 #pragma unroll
-  for (int o = 0; o < HID; ++o) h[o] = pb1[o];
-  auto accum8 = [&](const float* v, int c0) {  // channels c0..c0+7
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float* wr = pw1 + (c0 + j) * HID;
-#pragma unroll
-      for (int o = 0; o < HID; ++o) h[o] += wr[o] * v[j];
-    }
-  };
-  // main feature (CF channels, CF % 8 == 0) and the relative depth
-  {
-    const bf16_t* fp = a.feat + (int64_t)b * a.fs[0] + y * a.fs[2] + x * a.fs[3];
-    const bool vec = a.fs[1] == 1;
-#pragma unroll 1
-    for (int c = 0; c < a.CF; c += 8) {
-      float v[8];
-      load8(fp + c * a.fs[1], a.fs[1], vec, v);
-      accum8(v, c);
-    }
-    const float r = bf2f(a.rel[(int64_t)b * a.rs[0] + y * a.rs[1] + x * a.rs[2]]);
-    const float* wr = pw1 + a.CF * HID;
-#pragma unroll
-    for (int o = 0; o < HID; ++o) h[o] += wr[o] * r;
-  }
-  // bilinear-upsampled bin embedding (CE channels, CE % 8 == 0)
-  {
-    const Taps2 te = taps2(a.es, ty, tx);
-    const bf16_t* eb = a.emb + (int64_t)b * a.es[0];
-    const bool vec = a.es[1] == 1;
-#pragma unroll 1
-    for (int c = 0; c < a.CE; c += 8) {
-      float q00[8], q01[8], q10[8], q11[8], v[8];
-      const bf16_t* pc = eb + c * a.es[1];
-      load8(pc + te.o00, a.es[1], vec, q00);
-      load8(pc + te.o01, a.es[1], vec, q01);
-      load8(pc + te.o10, a.es[1], vec, q10);
-      load8(pc + te.o11, a.es[1], vec, q11);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = round_bf(te.ly0 * (te.lx0 * q00[j] + te.lx1 * q01[j]) + te.ly1 * (te.lx0 * q10[j] + te.lx1 * q11[j]));
-      accum8(v, a.CF + 1 + c);
-    }
-  }
+  for (int o8 = 0; o8 < HID / 8; ++o8) unpack8(*reinterpret_cast<const u32x4*>(hs + t * HS_LD + 8 * o8), h + 8 * o8);
 
   float s4[4] = {pb2[0], pb2[1], pb2[2], pb2[3]};
 #pragma unroll
@@ -286,8 +336,14 @@ extern "C" int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, i
   for (int i = 0; i < 3; ++i) a.rs[i] = rel_strides[i];
   a.p_eps = p_eps; a.max_t = max_t; a.min_t = min_t; a.clamp_eps = clamp_eps; a.out = out;
   const int64_t npix = (int64_t)B * H * W;
-  hipLaunchKernelGGL(zoe_tail_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a,
-                     params);
+  SVLA_CHECK_ARG(CF + 1 + CE <= KP, "zoe_tail: at most %d input channels", KP);
+  static bool lds_set = false;
+  if (!lds_set) {
+    (void)hipFuncSetAttribute((const void*)zoe_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ZT_LDS);
+    lds_set = true;
+  }
+  hipLaunchKernelGGL(zoe_tail_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), ZT_LDS, (hipStream_t)stream,
+                     a, params);
   return svla::check_launch("zoe_metric_tail");
 }
 
