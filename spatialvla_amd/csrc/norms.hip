@@ -314,6 +314,60 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(int64_t rows, int64_
 }
 
 // ------------------------------------------------------------------ LayerNorm
+// Wave-per-row forward for rows up to 64*8*WC elements (SigLIP 1152, BEiT 1024): four rows per block, the mean and
+// variance are wave reductions (no block barrier); the block-per-row kernel below left 112 of 256 threads idle at
+// N = 1152 and paid four barriers per row (19.9 us for [8192, 1152], 1.9 TB/s).
+template <int WC>
+__global__ __launch_bounds__(256) void ln_fwd_wave_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                          float eps, bf16_t* __restrict__ y, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int nch = (int)(N >> 3);
+  float v[WC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < WC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      ld8(x + row * N + ch * 8, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    }
+  }
+  const float mean = wave_sum(s) / (float)N;
+  float s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < WC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[c][j] - mean;
+        s2 += d * d;
+      }
+  }
+  const float rstd = rsqrtf(wave_sum(s2) / (float)N + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < WC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float wf[8], bf[8], o[8];
+      ld8(w + ch * 8, wf);
+      ld8(b + ch * 8, bf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wf[j] + bf[j];
+      st8(y + row * N + ch * 8, o);
+    }
+  }
+}
+
 __global__ __launch_bounds__(NTH) void ln_fwd_kernel(int64_t N, const bf16_t* __restrict__ x,
                                                      const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
                                                      float eps, bf16_t* __restrict__ y, float* __restrict__ mean_out,
@@ -522,8 +576,12 @@ extern "C" int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const 
                                   void* y, float* mean, float* rstd, void* stream) {
   SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "layernorm: bad N");
   SVLA_CHECK_ARG(x && w && b && y && mean && rstd, "layernorm: null pointer");
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N, (const bf16_t*)x,
-                     (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)y, mean, rstd);
+  if (N <= 64 * 8 * 3)
+    hipLaunchKernelGGL(ln_fwd_wave_kernel<3>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, rows,
+                       N, (const bf16_t*)x, (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)y, mean, rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N, (const bf16_t*)x,
+                       (const bf16_t*)w, (const bf16_t*)b, eps, (bf16_t*)y, mean, rstd);
   return svla::check_launch("layernorm_fwd");
 }
 
