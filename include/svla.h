@@ -111,7 +111,8 @@ int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const
 size_t svla_gemm_workspace_bytes(void);
 /* svla_gemm_bf16 with an explicit kernel choice (tests / tuning tools, not a reference interface): 0 = auto (as
  * svla_gemm_bf16), 1 = two-barrier tiles, 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case,
- * 4 = never the 4-wave kernel, 5 = auto without the small-M GEMV path. */
+ * 4 = never the 4-wave kernel, 5 = auto without the small-M GEMV path, 6 = small-M GEMVs without the prefetching
+ * kernel, 7 = the prefetching GEMV with two rows per wave. */
 int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                       void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                       const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant, void* stream);
@@ -199,6 +200,17 @@ typedef struct {
 size_t svla_attn_decode_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32_t Lk, int32_t D);
 int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, float* workspace, size_t ws_bytes,
                      void* stream);
+
+/* The decode step's attention in ONE launch: svla_qkv_rope_append + svla_attn_decode fused (same results, bitwise).
+ * a->q / a->ldq point at the raw q|k|v projection rows (row b*Lq+t: Hq q heads, Hkv k heads, Hkv v heads, not yet
+ * rotated); the new tokens sit at positions p0 = Lk-Lq .. Lk-1 and use RoPE table row t (rope_cos/rope_sin [Lq,
+ * >=D/2], rope_ld).  The rotated k and the v rows are appended to cache rows p0+t; q is not written back.
+ * workspace: >= svla_attn_decode_rope_workspace_bytes(...) bytes, 256-B aligned, ZEROED ONCE by the caller (its
+ * head holds arrival counters that every launch returns to zero; one workspace per stream).
+ * Replaces modeling_gemma2.py:123-154 (RoPE), :387-395 (HybridCache update) and :169-195 (eager attention). */
+size_t svla_attn_decode_rope_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t Lk, int32_t D);
+int svla_attn_decode_rope(const svla_attn_decode_args* a, const void* rope_cos, const void* rope_sin, int64_t rope_ld,
+                          void* out, int64_t ldo, void* workspace, size_t ws_bytes, void* stream);
 
 /* Decode-step q|k|v epilogue: rotate_half RoPE on q in place (rows b*Lq+t of qkv, position table row t) and on
  * k, rotated k and plain v written to cache rows p0+t (k/v cache element (b, j, h, d) at base + b*bs + j*ld + h*D + d).

@@ -75,6 +75,9 @@ SIGNATURES = {
                               c_vp, c_i64, c_vp, c_vp]),
     "svla_attn_decode_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "svla_attn_decode": (c_i32, [ctypes.POINTER(AttnDecodeArgs), c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
+    "svla_attn_decode_rope_workspace_bytes": (ctypes.c_size_t, [c_i32] * 6),
+    "svla_attn_decode_rope": (c_i32, [ctypes.POINTER(AttnDecodeArgs), c_vp, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                      ctypes.c_size_t, c_vp]),
     "svla_qkv_rope_append": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                                      c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "svla_add_rmsnorm2_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),

@@ -7,6 +7,7 @@ view as `param._svla_grad` — straight into that view (accumulating when `param
 in which case autograd receives None for that parameter (no extra copy, no autograd add).
 """
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -383,6 +384,11 @@ class GemmaAttentionFn(torch.autograd.Function):
         return (dx, *rets, ret_wo, None, None, None, None, None)
 
 
+# decode steps run RoPE + cache append + attention as one launch (svla_attn_decode_rope); False = the two-launch
+# form (svla_qkv_rope_append, then svla_attn_decode), kept for the bitwise A/B test
+DECODE_FUSED = [os.environ.get("SVLA_DECODE_FUSED", "1") != "0"]
+
+
 @torch.no_grad()
 def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_class, p0, cfg: GemmaAttnCfg):
     """Gemma2Attention.forward with a KV cache (modeling_gemma2.py:364-413, cache update :387-395), inference
@@ -397,9 +403,15 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     qkv = _empty(M, qd + 2 * kd, like=x)
     attn = _empty(M, qd, like=x)
     if p0 > 0:
-        # decode step: plain projection, then one pass rotates q in place and appends rotated k / v to the cache
+        # decode step: plain projection, then one launch rotates q / k, appends k / v to the cache and attends
         K.linear_fwd(x, [wq, wk, wv], qkv)
-        K.qkv_rope_append(qkv, B, Lq, cfg.Hq, cfg.Hkv, cfg.D, cos, sin, k_cache, v_cache, p0)
+        if DECODE_FUSED[0]:
+            K.attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
+                               cfg.softcap, kv_class, cfg.window, attn)
+        else:
+            K.qkv_rope_append(qkv, B, Lq, cfg.Hq, cfg.Hkv, cfg.D, cos, sin, k_cache, v_cache, p0)
+            K.attn_decode(qkv[:, :qd], Lq, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
+                          cfg.softcap, kv_class, cfg.window, attn)
     else:
         K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, Lq, cfg.D, qd + kd))
         k_cache[:, :Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
@@ -410,9 +422,6 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         a = K.attn_args(B, Lq, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, cls, cfg.window)
         K.attn_fwd(a, attn, lse)
-    else:
-        K.attn_decode(qkv[:, :qd], Lq, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale, cfg.softcap,
-                      kv_class, cfg.window, attn)
     out = _empty(M, wo.shape[0], like=x)
     K.linear_fwd(attn, [wo], out)
     return out

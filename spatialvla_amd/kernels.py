@@ -446,6 +446,50 @@ def attn_decode(q, Lq, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_clas
             "attn_decode")
 
 
+# svla_attn_decode_rope workspaces: zeroed once, one per (device, stream) -- the arrival counters at their head
+# return to zero after every launch, so a buffer is reused by every later call (and by captured graph replays)
+_DECODE_WS = {}
+
+
+def _decode_rope_ws(nbytes, device):
+    key = (device.index, _stream())
+    ws = _DECODE_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(max(nbytes, 8 << 20), dtype=torch.uint8, device=device)
+        _DECODE_WS[key] = ws
+    return ws
+
+
+def attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_class, window, out):
+    """The decode step's attention in one launch: q|k|v projection rows (b*Lq+t, unrotated) -> RoPE (table row t),
+    rotated k / v appended to cache rows Lk-Lq.., attention of the Lq new queries over the first Lk cache rows."""
+    B = k_cache.shape[0]
+    _req(qkv.shape[0] == B * Lq and out.shape[0] == B * Lq and qkv.stride(1) == 1 and out.stride(1) == 1,
+         "attn_decode_rope: qkv/out rows != B*Lq or not contiguous")
+    _req(qkv.shape[1] >= (Hq + 2 * Hkv) * D, "attn_decode_rope: qkv narrower than q|k|v")
+    _req(k_cache.shape[1] >= Lk and v_cache.shape[1] >= Lk and Lk > Lq, "attn_decode_rope: cache / Lk")
+    _req(k_cache.stride(2) == 1 and v_cache.stride(2) == 1, "attn_decode_rope: cache rows must be contiguous")
+    _req(cos.shape[0] >= Lq and cos.shape == sin.shape and cos.stride(1) == 1 and cos.stride(0) == sin.stride(0),
+         "attn_decode_rope: tables")
+    _req(kv_class is None or (kv_class.dtype == torch.uint8 and kv_class.shape[0] == B and kv_class.stride(1) == 1),
+         "attn_decode_rope: kv_class must be uint8 [B, >=Lk]")
+    for t, n in ((qkv, "qkv"), (k_cache, "k"), (v_cache, "v"), (out, "out"), (cos, "cos"), (sin, "sin")):
+        _chk_bf16(t, n)
+    a = L.AttnDecodeArgs()
+    a.B, a.Lq, a.Lk, a.Hq, a.Hkv, a.D = B, Lq, Lk, Hq, Hkv, D
+    a.sliding_window, a.scale, a.softcap = int(window or 0), float(scale), float(softcap or 0.0)
+    a.q, a.ldq = qkv.data_ptr(), qkv.stride(0)
+    a.k, a.ldk, a.bsk = k_cache.data_ptr(), k_cache.stride(1), k_cache.stride(0)
+    a.v, a.ldv, a.bsv = v_cache.data_ptr(), v_cache.stride(1), v_cache.stride(0)
+    a.kv_class = _ptr(kv_class)
+    a.ldc = kv_class.stride(0) if kv_class is not None else 0
+    nb = L.lib().svla_attn_decode_rope_workspace_bytes(B, Lq, Hq, Hkv, Lk, D)
+    ws = _decode_rope_ws(nb, qkv.device)
+    L.check(L.lib().svla_attn_decode_rope(ctypes.byref(a), cos.data_ptr(), sin.data_ptr(), cos.stride(0),
+                                          out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), _stream()),
+            "attn_decode_rope")
+
+
 def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
     """RoPE q in place, rotated k and v into cache rows p0.. (the decode step's q|k|v epilogue)."""
     _req(qkv.shape[0] == B * Lq and qkv.stride(1) == 1, "qkv_rope_append: qkv rows")

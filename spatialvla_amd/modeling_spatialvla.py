@@ -460,6 +460,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
 
     DECODE_STATES_MAX = 2      # decode states (KV cache + captured graphs) kept per model, least recently used out
     DECODE_CAPACITY_STEP = 64  # cache capacities are bucketed: prompts of nearby lengths share one state
+    EOS_CHECK_EVERY = 8        # predict_action reads the device's finished flags once per this many decode steps
 
     def enable_fp8_projections(self, enabled: bool = True):
         """BASELINE configs[4]: the Gemma2 q|k|v, o, gate|up and down forward projections on the fp8 (OCP e4m3,
@@ -506,6 +507,12 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                 states.popitem(last=False)
             st = {"cache": self.new_cache(B, cap), "graphs": {}, "prefill": {}, "wptr": wptr,
                   "tok": torch.zeros(B, 1, dtype=torch.int64, device=dev),
+                  # greedy bookkeeping read / written inside the step graphs: finished rows, eos / pad ids (-1 = no
+                  # eos), every generated token at its cache position
+                  "fin": torch.zeros(B, 1, dtype=torch.bool, device=dev),
+                  "eos": torch.full((1, 1), -1, dtype=torch.int64, device=dev),
+                  "pad": torch.zeros(1, 1, dtype=torch.int64, device=dev),
+                  "toks": torch.zeros(B, cap + 1, dtype=torch.int64, device=dev),
                   "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev)),
                   "pool": torch.cuda.graph_pool_handle() if dev.type == "cuda" else None,
                   "side": torch.cuda.Stream(device=dev) if dev.type == "cuda" else None}
@@ -581,6 +588,15 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         self.language_model.head(h[:, -1:].contiguous(), tgt, stash)
         return stash["argmax"]
 
+    def _greedy_bookkeep(self, st, p0, am):
+        """The greedy loop's per-token update on the device (so a run of steps needs no host round trip): rows that
+        already emitted eos get pad, newly finished rows are marked, the token is fed to the next step and kept at
+        its cache position p0 + 1 (reference generate: unfinished_sequences / pad_token_id handling)."""
+        nxt = torch.where(st["fin"], st["pad"], am.view(-1, 1))
+        st["fin"].logical_or_(nxt == st["eos"])
+        st["tok"].copy_(nxt)
+        st["toks"][:, p0 + 1:p0 + 2].copy_(nxt)
+
     def _decode_step_graph(self, st, p0):
         """The decode step as a HIP graph (torch.cuda.CUDAGraph on ROCm), captured once per cache position: a
         B=1 step is ~300 small launches whose host-side cost exceeds their GPU time, and a graph replays them
@@ -591,12 +607,16 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             side = st["side"]
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):  # eager warm-up (lazy kernel attributes); rewrites row p0 identically
-                self._decode_body(st, p0)
+                saved = (st["tok"].clone(), st["fin"].clone())
+                self._greedy_bookkeep(st, p0, self._decode_body(st, p0))
+                st["tok"].copy_(saved[0])
+                st["fin"].copy_(saved[1])
             cache.seen_tokens = p0
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, pool=st["pool"], stream=side):  # on the warm-up stream, as the prefill
                 out = self._decode_body(st, p0)
+                self._greedy_bookkeep(st, p0, out)
             cache.seen_tokens = p0
             g = st["graphs"][p0] = (graph, out)
         g[0].replay()
@@ -636,26 +656,34 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             prefill["depth"] = self.predict_depth(pv.to(dt))
         first = self._prefill_graph(st, prefill) if graphs else self._prefill_body(st, prefill)
         cache.seen_tokens = P
-        finished = torch.zeros(B, 1, dtype=torch.bool, device=dev)
-        nxt = first.view(B, 1).clone()
-        if eos is not None:
-            finished = nxt == eos
-        out = [nxt]
-        pad = torch.full_like(nxt, max(self.pad_token_id, 0))
-        for _ in range(max_new_tokens - 1):
-            if eos is not None and bool(finished.all()):
+        # the per-token update runs on the device (_greedy_bookkeep); the host reads the finished flags only every
+        # EOS_CHECK_EVERY steps and cuts the output where the last row finished -- the tokens and the length are the
+        # step-by-step loop's
+        st["eos"].fill_(-1 if eos is None else int(eos))
+        st["pad"].fill_(max(self.pad_token_id, 0))
+        nxt = first.view(B, 1)
+        st["fin"].copy_(nxt == st["eos"])
+        st["tok"].copy_(nxt)
+        st["toks"][:, P:P + 1].copy_(nxt)
+        steps = 0
+        while steps < max_new_tokens - 1:
+            if eos is not None and steps % self.EOS_CHECK_EVERY == 0 and bool(st["fin"].all()):
                 break
-            st["tok"].copy_(nxt)
             p0 = cache.seen_tokens
-            am_ = self._decode_step_graph(st, p0) if graphs else self._decode_body(st, p0)
-            if not graphs:
+            if graphs:
+                self._decode_step_graph(st, p0)
+            else:
+                self._greedy_bookkeep(st, p0, self._decode_body(st, p0))
                 cache.seen_tokens = p0 + 1
-            nxt = am_.view(B, 1).clone()
-            if eos is not None:
-                nxt = torch.where(finished, pad, nxt)
-                finished = finished | (nxt == eos)
-            out.append(nxt)
-        return torch.cat(out, 1)
+            steps += 1
+        toks = st["toks"][:, P:P + steps + 1].clone()
+        if eos is not None:  # the step-by-step loop's length: up to the token where the last row finished
+            hit = toks == eos
+            if bool(hit.any(1).all()):
+                n = toks.shape[1]
+                first_eos = torch.where(hit, torch.arange(n, device=dev), n).min(1).values
+                toks = toks[:, :int(first_eos.max()) + 1]
+        return toks
 
     @torch.no_grad()
     def predict_action_uncached(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):

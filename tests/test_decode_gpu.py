@@ -114,6 +114,18 @@ def test_predict_action_eos_pads_finished(cuda):
     ref = model.predict_action_uncached(inputs, max_new_tokens=4, eos_token_id=eos)
     assert torch.equal(out, ref)
     assert out[0, 1] == eos and bool((out[0, 2:] == max(model.pad_token_id, 0)).all())
+    # every row finished: the output stops at the token where the last row finished, as the step-by-step loop,
+    # although the device-side loop only looks at the finished flags every EOS_CHECK_EVERY steps
+    one = {k: v[:1] for k, v in inputs.items()}
+    free1 = model.predict_action(one, max_new_tokens=12, eos_token_id=-1)
+    eos1 = int(free1[0, 1])
+    ref1 = model.predict_action_uncached(one, max_new_tokens=12, eos_token_id=eos1)
+    assert ref1.shape[1] <= 2
+    for graphs in (True, False):
+        model.decode_graphs = graphs
+        out1 = model.predict_action(one, max_new_tokens=12, eos_token_id=eos1)
+        assert torch.equal(out1, ref1), (graphs, out1, ref1)
+    model.decode_graphs = True
 
 
 def test_forward_past_key_values_matches_reforward(cuda):
@@ -225,6 +237,56 @@ def test_qkv_rope_append(cuda, B, Lq, p0):
     assert torch.equal(kc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, Hq * D:nrot])
     assert torch.equal(vc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, nrot:])
     assert kc[:, :p0].abs().sum() == 0 and kc[:, p0 + Lq:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("B,Lq,p0,Hq,Hkv,D,window,use_cls", [
+    (1, 1, 299, 8, 4, 256, 0, True), (2, 3, 61, 8, 4, 256, 0, True), (1, 1, 64, 8, 4, 256, 4096, True),
+    (2, 2, 130, 4, 4, 128, 50, False), (1, 1, 7, 8, 2, 64, 0, False)])
+def test_attn_decode_rope_fused_bitwise(cuda, B, Lq, p0, Hq, Hkv, D, window, use_cls):
+    """svla_attn_decode_rope (one launch: RoPE + cache append + split + in-launch combine) equals
+    svla_qkv_rope_append + svla_attn_decode bit for bit: output and both caches; repeated launches reuse the
+    zeroed-once workspace (its counters come back to zero)."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(10)
+    kd, Lk = Hkv * D, p0 + Lq
+    cap = Lk + 9
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    f = (torch.arange(p0, p0 + Lq, device=cuda).float() + 1)[:, None] * inv[None]
+    emb = torch.cat([f, f], -1)  # HF layout [Lq, D] (the kernels read the first D/2 columns)
+    cos, sin = emb.cos().to(BF).contiguous(), emb.sin().to(BF).contiguous()
+    kc0 = _r(B, cap, kd)
+    vc0 = _r(B, cap, kd)
+    cls = None
+    if use_cls:
+        cls = torch.zeros(B, cap, dtype=torch.uint8, device=cuda)
+        cls[:, p0 - 3:] = 1
+        cls[-1, 5:9] = 2
+    for rep in range(3):
+        qkv = _r(B * Lq, (Hq + 2 * Hkv) * D, scale=2.0)
+        kc1, vc1, kc2, vc2 = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
+        ref, out = torch.empty(B * Lq, Hq * D, dtype=BF, device=cuda), torch.empty(B * Lq, Hq * D, dtype=BF, device=cuda)
+        q2 = qkv.clone()
+        Kn.qkv_rope_append(q2, B, Lq, Hq, Hkv, D, cos, sin, kc1, vc1, p0)
+        Kn.attn_decode(q2[:, :Hq * D], Lq, kc1, vc1, Lk, Hq, Hkv, D, 1 / 16, 50.0, cls, window, ref)
+        Kn.attn_decode_rope(qkv, Lq, cos, sin, kc2, vc2, Lk, Hq, Hkv, D, 1 / 16, 50.0, cls, window, out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), rep
+        assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1), rep
+    ws = Kn._DECODE_WS[(qkv.device.index, Kn._stream())]
+    assert int(ws[:256].count_nonzero()) == 0  # the arrival counters are back to zero
+
+
+def test_attn_decode_rope_rejects_bad_args(cuda):
+    from spatialvla_amd import kernels as Kn
+    qkv = _r(1, 16 * 256)
+    kc = _r(1, 32, 4 * 256)
+    cos = _r(1, 256)
+    with pytest.raises(Exception):  # Lk must exceed Lq (a cached prefix)
+        Kn.attn_decode_rope(qkv, 1, cos, cos, kc, kc, 1, 8, 4, 256, 1 / 16, 50.0, None, 0, _r(1, 8 * 256))
+    with pytest.raises(Exception):  # GQA group 3
+        kc3 = _r(1, 32, 3 * 256)
+        Kn.attn_decode_rope(_r(1, 15 * 256), 1, cos, cos, kc3, kc3, 10, 9, 3, 256, 1 / 16, 50.0, None, 0,
+                            _r(1, 9 * 256))
 
 
 @pytest.mark.parametrize("rows", [1, 3, 299])
