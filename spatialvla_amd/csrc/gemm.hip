@@ -44,7 +44,7 @@ __device__ __forceinline__ float softcap_bf16_tab(float v, float cap, float icap
   const uint32_t tb = tab[idx];
   uint32_t rb = ab < lo ? ab : (ab >= hi ? 0x3f80u : tb);
   if (ab > 0x7f80u) rb = ab;  // NaN stays NaN
-  const float t = __uint_as_float(((u >> 16) & 0x8000u | rb) << 16);
+  const float t = __uint_as_float((((u >> 16) & 0x8000u) | rb) << 16);
   return round_bf(t * cap);
 }
 constexpr int TANH_TAB_BYTES = sizeof(svla_tanh_bf16_tab);
@@ -2089,24 +2089,36 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
   }
 }
 
-// SOFTCAP_CE at small M (the lm_head of a decode step): one wave per 128-column tile of the vocab walks its
-// rows four at a time and keeps the tile's online-softmax partials {max, sumexp, argmax} per activation row in
-// registers — the row_stats layout of the MFMA epilogue (logits rounded to bf16, softcapped, rounded again).
+// SOFTCAP_CE at small M (the lm_head of a decode step): one workgroup per 128-column tile of the vocab, each of
+// its four waves walks 32 of the tile's rows four at a time and keeps online-softmax partials {max, sumexp,
+// argmax} per activation row in registers (logits rounded to bf16, softcapped, rounded again); the four partials
+// merge through LDS in wave order into the row_stats record of the MFMA epilogue's layout.  Four waves per tile
+// (2073 tiles -> 8292 waves) keep ~4x the weight loads in flight of one wave per tile.
+__device__ __forceinline__ void gemv_ce_merge(float& mx, float& se, int& am, float m2, float s2, int a2) {
+  if (m2 == -INFINITY) return;
+  const float mn = fmaxf(mx, m2);
+  se = (mx == -INFINITY ? 0.f : se * __expf(mx - mn)) + s2 * __expf(m2 - mn);
+  if (m2 > mx || (m2 == mx && a2 < am)) am = a2;
+  mx = mn;
+}
+
 __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int64_t K, const bf16_t* __restrict__ x,
                                                            int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
                                                            bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
   constexpr int RW = 4;
-  const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float part[4][GEMV_MAXM][3];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t tile = blockIdx.x;
   const int64_t ntn = (N + 127) / 128;
-  if (tile >= ntn) return;
   const float cap = E.cap;
   float mx[GEMV_MAXM], se[GEMV_MAXM];
   int am[GEMV_MAXM];
 #pragma unroll
   for (int m = 0; m < GEMV_MAXM; ++m) { mx[m] = -INFINITY; se[m] = 0.f; am[m] = 0x7fffffff; }
-  const int64_t nend = (tile + 1) * 128 < N ? (tile + 1) * 128 : N;
-  for (int64_t r0 = tile * 128; r0 < nend; r0 += RW) {
+  const int64_t tend = (tile + 1) * 128 < N ? (tile + 1) * 128 : N;
+  const int64_t wbeg = tile * 128 + wv * 32;
+  const int64_t nend = wbeg + 32 < tend ? wbeg + 32 : tend;
+  for (int64_t r0 = wbeg; r0 < nend; r0 += RW) {
     float acc[RW][GEMV_MAXM];
 #pragma unroll
     for (int r = 0; r < RW; ++r)
@@ -2156,13 +2168,21 @@ __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int
   if (lane == 0) {
 #pragma unroll
     for (int m = 0; m < GEMV_MAXM; ++m) {
-      if (m < M) {
-        float* rs = E.row_stats + (m * ntn + tile) * 3;
-        rs[0] = mx[m];
-        rs[1] = se[m];
-        rs[2] = __int_as_float(am[m]);
-      }
+      part[wv][m][0] = mx[m];
+      part[wv][m][1] = se[m];
+      part[wv][m][2] = __int_as_float(am[m]);
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < M) {
+    const int m = threadIdx.x;
+    float tm = -INFINITY, ts = 0.f;
+    int ta = 0x7fffffff;
+    for (int q = 0; q < 4; ++q) gemv_ce_merge(tm, ts, ta, part[q][m][0], part[q][m][1], __float_as_int(part[q][m][2]));
+    float* rs = E.row_stats + (m * ntn + tile) * 3;
+    rs[0] = tm;
+    rs[1] = ts;
+    rs[2] = __int_as_float(ta);
   }
 }
 
@@ -2207,6 +2227,125 @@ __global__ __launch_bounds__(256) void gemv_splitk_kernel(int M, int64_t rows, i
   }
 }
 
+// Prefetching GEMV: a lane's whole K range (KCH 16-B chunks per weight row, K <= KCH*512) is loaded before the
+// first FMA, so a wave has RW*NW*KCH loads in flight instead of the runtime loop's unroll-bounded few -- the
+// decode GEMVs are HBM-latency bound (a few MB per launch).  Same products and summation order per lane as
+// gemv_kernel, so the results are bitwise equal.
+template <int KCH, int RW, bool GEGLU>
+__global__ __launch_bounds__(256) void gemv_pf_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ x,
+                                                      int64_t ldx, svla_operand B, bf16_t* __restrict__ c,
+                                                      int64_t ldc, svla_epilogue E) {
+  constexpr int NW = GEGLU ? 2 : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = wave * RW;
+  if (r0 >= rows) return;
+  u32x4 wv[RW][NW][KCH];
+#pragma unroll
+  for (int r = 0; r < RW; ++r) {
+    const int64_t n = r0 + r < rows ? r0 + r : rows - 1;
+    const bf16_t* wr[NW];
+    if constexpr (GEGLU) {
+      wr[0] = (const bf16_t*)B.ptr[0] + n * B.ld;
+      wr[NW - 1] = (const bf16_t*)B.ptr[1] + n * B.ld;
+    } else {
+      wr[0] = gemv_row(B, n);
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int i = 0; i < KCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        wv[r][q][i] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + k)) : u32x4{0, 0, 0, 0};
+      }
+  }
+  float acc[RW][NW][GEMV_MAXM];
+#pragma unroll
+  for (int r = 0; r < RW; ++r)
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) acc[r][q][m] = 0.f;
+#pragma unroll
+  for (int i = 0; i < KCH; ++i) {
+    const int64_t k = (int64_t)lane * 8 + i * 512;
+    if (k < K) {
+      float wf[RW][NW][8];
+#pragma unroll
+      for (int r = 0; r < RW; ++r)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) unpack8(wv[r][q][i], wf[r][q]);
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) {
+        if (m < M) {
+          float xf[8];
+          unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+#pragma unroll
+          for (int r = 0; r < RW; ++r)
+#pragma unroll
+            for (int q = 0; q < NW; ++q)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[r][q][m] = fmaf(wf[r][q][j], xf[j], acc[r][q][m]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) {
+    if (m < M) {
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        float v[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v[q] = wave_sum(acc[r][q][m]);
+        const int64_t n = r0 + r;
+        if (lane == 0 && n < rows) {
+          if constexpr (GEGLU) {
+            const float g = round_bf(v[0]), u = round_bf(v[1]);
+            c[m * ldc + n] = f2bf(round_bf(gelu_tanh(g)) * u);
+            ((bf16_t*)E.out1)[m * E.ld_out1 + n] = f2bf(g);
+            ((bf16_t*)E.out2)[m * E.ld_out2 + n] = f2bf(u);
+          } else {
+            c[m * ldc + n] = f2bf(v[0]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int KCH, int RW, bool GEGLU>
+void launch_gemv_pf(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
+                    int64_t ldc, const svla_epilogue& E, hipStream_t s) {
+  const int64_t waves = (rows + RW - 1) / RW;
+  hipLaunchKernelGGL((gemv_pf_kernel<KCH, RW, GEGLU>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, M, rows,
+                     K, (const bf16_t*)A.ptr[0], A.ld, B, c, ldc, E);
+}
+
+// K chunk count of the prefetching GEMV for this K (0 = no instance: the runtime-loop kernels)
+inline int gemv_pf_kch(int64_t K) {
+  const int64_t kch = (K + 511) / 512;
+  return (kch == 4 || kch == 5) ? (int)kch : 0;  // K = 9216 (down): the split-K kernel stays ahead (11.7 vs 13.2 us)
+}
+
+template <bool GEGLU>
+bool try_gemv_pf(int variant, int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B,
+                 bf16_t* c, int64_t ldc, const svla_epilogue& E, hipStream_t s) {
+  const int kch = gemv_pf_kch(K);
+  if (kch == 0 || variant == 6) return false;
+  const bool rw2 = variant == 7;
+#define SVLA_GEMV_PF(KC)                                                                   \
+  if (kch == KC) {                                                                         \
+    if (rw2) launch_gemv_pf<KC, 2, GEGLU>(M, rows, K, A, B, c, ldc, E, s);                 \
+    else launch_gemv_pf<KC, 1, GEGLU>(M, rows, K, A, B, c, ldc, E, s);                     \
+    return true;                                                                           \
+  }
+  SVLA_GEMV_PF(4)
+  SVLA_GEMV_PF(5)
+#undef SVLA_GEMV_PF
+  return false;
+}
+
 template <int RW, bool GEGLU>
 int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
                 int64_t ldc, const svla_epilogue& E, hipStream_t s) {
@@ -2219,7 +2358,8 @@ int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svl
 // Per-call dispatch context (no process state: the library is re-entrant across threads and streams).
 // variant (tests / tools only, svla_gemm_bf16_ex): 0 = auto (the 4-wave kernel for long-K GEMMs with more than a
 // wave of tiles, else 8-phase + stream-K, else the 2-barrier tiles), 1 = 2-barrier kernel, 2 = 8-phase without
-// stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = no small-M GEMV path.
+// stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = no small-M GEMV path,
+// 6 = small-M GEMVs without the prefetching kernel, 7 = the prefetching kernel with two rows per wave.
 struct GemmCtx {
   void* ws;          // caller-owned stream-K workspace (slabs + arrival counters), NULL = no stream-K
   size_t ws_bytes;
@@ -2381,7 +2521,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
                                  void* stream) {
-  SVLA_CHECK_ARG(variant >= 0 && variant <= 5, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 7, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   GemmCtx ctx;
   ctx.ws = workspace;
@@ -2486,10 +2626,12 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
       bf16_t* c0 = C.ptr[0];
       if (epi->kind == SVLA_EPI_SOFTCAP_CE) {
         const int64_t ntn = (N + 127) / 128;
-        hipLaunchKernelGGL(gemv_softcap_kernel, dim3((unsigned)((ntn + 3) / 4)), dim3(256), 0, s, (int)M, N, K,
+        hipLaunchKernelGGL(gemv_softcap_kernel, dim3((unsigned)ntn), dim3(256), 0, s, (int)M, N, K,
                            (const bf16_t*)A->ptr[0], A->ld, (const bf16_t*)B->ptr[0], B->ld, c0, ldc, *epi);
       } else if (epi->kind == SVLA_EPI_GEGLU) {
-        launch_gemv<1, true>((int)M, N / 2, K, *A, *B, c0, ldc, *epi, s);
+        if (!try_gemv_pf<true>(variant, (int)M, N / 2, K, *A, *B, c0, ldc, *epi, s))
+          launch_gemv<1, true>((int)M, N / 2, K, *A, *B, c0, ldc, *epi, s);
+      } else if (try_gemv_pf<false>(variant, (int)M, N, K, *A, *B, c0, ldc, *epi, s)) {
       } else if (K > 4096) {
         hipLaunchKernelGGL(gemv_splitk_kernel, dim3((unsigned)N), dim3(256), 0, s, (int)M, N, K,
                            (const bf16_t*)A->ptr[0], A->ld, *B, c0, ldc);
@@ -2512,7 +2654,7 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU ||
                          epi->kind == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (variant == 3 || ((variant == 0 || variant == 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
+                    (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
                                         (t256 >= 512 || K >= 4096) &&
                                         (B->layout == SVLA_LAYOUT_KC || K >= 4096)));  // short-K x RC B: +4%
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile

@@ -527,6 +527,11 @@ def embed_merge_bwd(ids, img_index, sorted_rows, offsets, na, dout, normalizer, 
 
 def ego3d_encode(depth, kinv, uv_h, patch, reso, n_freqs, feat, xyz_out=None):
     B, _, Hd, Wd = depth.shape
+    _req(kinv.numel() == B * 9 and kinv.dtype == torch.float32 and kinv.is_contiguous(),
+         f"ego3d_encode: inv(K) must be [{B}, 3, 3] fp32 (one per depth map), got {tuple(kinv.shape)}")
+    _req(feat.shape[0] >= B * (Hd // patch) * (Wd // patch), "ego3d_encode: feat has fewer rows than B * patches")
+    _req(xyz_out is None or xyz_out.numel() >= B * (Hd // patch) * (Wd // patch) * 3 * reso * reso,
+         "ego3d_encode: xyz_out too small")
     L.check(L.lib().svla_ego3d_encode(B, Hd, Wd, depth.data_ptr(), kinv.data_ptr(), uv_h.data_ptr(), patch, reso,
                                       n_freqs, feat.data_ptr(), _ld(feat), _ptr(xyz_out), _stream()), "ego3d_encode")
 
