@@ -2105,7 +2105,11 @@ __device__ __forceinline__ void gemv_ce_merge(float& mx, float& se, int& am, flo
 __global__ __launch_bounds__(256) void gemv_softcap_kernel(int M, int64_t N, int64_t K, const bf16_t* __restrict__ x,
                                                            int64_t ldx, const bf16_t* __restrict__ w, int64_t ldw,
                                                            bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E) {
-  constexpr int RW = 4;
+#ifndef SVLA_LMHEAD_RW
+#define SVLA_LMHEAD_RW 4  // 8: 272.7 us vs 259.9 us per lm_head launch (profiles/r2q_dec*)
+#endif
+  constexpr int RW = SVLA_LMHEAD_RW;  // vocab rows per step of a wave (32 % RW == 0)
+  static_assert(32 % RW == 0, "a wave's 32 rows split into steps of RW");
   __shared__ float part[4][GEMV_MAXM][3];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
@@ -2199,17 +2203,44 @@ __global__ __launch_bounds__(256) void gemv_splitk_kernel(int M, int64_t rows, i
   float acc[GEMV_MAXM];
 #pragma unroll
   for (int m = 0; m < GEMV_MAXM; ++m) acc[m] = 0.f;
+  if (K <= 5 * 2048) {  // the down projection (K = 9216): every chunk of the lane's K range in flight at once
+    constexpr int KCH = 5;
+    u32x4 wv[KCH];
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int64_t k = (int64_t)threadIdx.x * 8 + i * 2048;
+      if (k < K) wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + k));
+    }
+#pragma unroll
+    for (int i = 0; i < KCH; ++i) {
+      const int64_t k = (int64_t)threadIdx.x * 8 + i * 2048;
+      if (k < K) {
+        float wf[8];
+        unpack8(wv[i], wf);
+#pragma unroll
+        for (int m = 0; m < GEMV_MAXM; ++m) {
+          if (m < M) {
+            float xf[8];
+            unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+          }
+        }
+      }
+    }
+  } else {
 #pragma unroll 4
-  for (int64_t k = (int64_t)threadIdx.x * 8; k < K; k += 2048) {
-    float wf[8];
-    unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + k)), wf);
+    for (int64_t k = (int64_t)threadIdx.x * 8; k < K; k += 2048) {
+      float wf[8];
+      unpack8(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + k)), wf);
 #pragma unroll
-    for (int m = 0; m < GEMV_MAXM; ++m) {
-      if (m < M) {
-        float xf[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
+      for (int m = 0; m < GEMV_MAXM; ++m) {
+        if (m < M) {
+          float xf[8];
+          unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + k), xf);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+          for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+        }
       }
     }
   }
