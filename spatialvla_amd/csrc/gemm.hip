@@ -2390,7 +2390,8 @@ int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svl
 // variant (tests / tools only, svla_gemm_bf16_ex): 0 = auto (the 4-wave kernel for long-K GEMMs with more than a
 // wave of tiles, else 8-phase + stream-K, else the 2-barrier tiles), 1 = 2-barrier kernel, 2 = 8-phase without
 // stream-K, 3 = 4-wave kernel for every 256x256 case, 4 = never the 4-wave kernel, 5 = no small-M GEMV path,
-// 6 = small-M GEMVs without the prefetching kernel, 7 = the prefetching kernel with two rows per wave.
+// 6 = small-M GEMVs without the prefetching kernel, 7 = the prefetching kernel with two rows per wave,
+// 8 = 8-phase + stream-K for every sub-wave grid (tools/prefill_gemm_bench.py).
 struct GemmCtx {
   void* ws;          // caller-owned stream-K workspace (slabs + arrival counters), NULL = no stream-K
   size_t ws_bytes;
@@ -2552,7 +2553,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
                                  void* stream) {
-  SVLA_CHECK_ARG(variant >= 0 && variant <= 7, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 8, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   GemmCtx ctx;
   ctx.ws = workspace;
@@ -2696,7 +2697,7 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   }
   if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);
   if (variant != 1 && !kseg && seg_ok(256, 256) &&
-      (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus())))
+      (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus()) || (variant == 8 && sk_ok)))
     return launch8(M, N, K, *A, *B, C, *epi, ctx, s);
   if (tiles(256, 256) >= 512 && seg_ok(256, 256)) return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   if (tiles(256, 128) >= 256 && seg_ok(256, 128)) return launch<CfgMid>(M, N, K, *A, *B, C, *epi, s);
