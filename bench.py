@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-decode", action="store_true", help="skip the B=1 decode-latency leg")
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-fp8-leg", action="store_true", help="skip the configs[4] fp8 leg of the N=1 line")
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE configs[4]: Gemma2 q|k|v, o, gate|up, down forward projections on the fp8 MFMA GEMM")
     return ap.parse_args()
@@ -122,6 +123,34 @@ def dominant_kernel_roofline(records, fp8=False):
             "frac": round(ach / peak, 4), "traffic": None if fp8 else pmc_traffic(), "avg_launch_ms": round(avg, 4),
             "launches_timed": len(ms), "algorithmic_flops_per_launch": flops,
             "algorithmic_bytes_per_launch": bytes_alg}
+
+
+def fp8_leg(model, engine, batches, args):
+    """BASELINE configs[4] beside the bf16 line (N=1, after the timed region, same model and batches): the training
+    step with the Gemma2 q|k|v, o, gate|up and down projections on the fp8 (e4m3, row-scaled) MFMA GEMM, forward and
+    dgrad, weight copies re-quantised after every optimizer step; timed like the main line (barrier-free: one rank).
+    roofline: the fp8 gate/up GeGLU launches inside the timed steps vs the dense fp8 peak (5 PFLOP/s)."""
+    from spatialvla_amd import kernels as K
+    model.enable_fp8_projections(True)
+    try:
+        n = len(batches)
+        for s in range(min(2, args.warmup)):
+            engine.train_step(batches[s % n])
+        torch.cuda.synchronize()
+        ev = K.launch_timer["geglu_fp8"] = []
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            loss = engine.train_step(batches[s % n])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        K.launch_timer.pop("geglu_fp8")
+    finally:
+        model.enable_fp8_projections(False)
+    B = args.batch
+    return {"what": "BASELINE configs[4] at N=1: fwd+bwd+AdamW with fp8 Gemma2 projections (fwd + dgrad), B=%d" % B,
+            "value": round(B * args.steps / dt, 3), "unit": "episodes/s", "ms_per_step": round(dt / args.steps * 1e3, 2),
+            "steps": args.steps, "final_loss": round(float(loss.item()), 4),
+            "roofline": dominant_kernel_roofline(ev, fp8=True)}
 
 
 def gemma2_block_roofline(model, B, L, device, iters=20):
@@ -350,6 +379,8 @@ def main():
         "mfu_model_flops": round(eps * GFLOP_PER_EPISODE / 1e3 / (world * PEAK_BF16_TFLOPS), 4),
         "final_loss": round(final_loss, 4),
     }
+    if world == 1 and not args.fp8 and not args.no_fp8_leg and args.config == "spatialvla_4b":
+        result["fp8"] = fp8_leg(model, engine, batches, args)
     if rank == 0:
         result["roofline"] = dominant_kernel_roofline(geglu_events, fp8=args.fp8)
         if args.config == "spatialvla_4b":

@@ -308,6 +308,13 @@ int svla_ce_finalize(int64_t M, int64_t N, int64_t ntiles, const float* row_stat
  * target < 0 get 0; columns in [N, ldd) zeroed.  scale = grad_loss / n_valid (device scalar). */
 int svla_ce_bwd(int64_t M, int64_t N, const void* logits, int64_t ldl, const float* lse, const int64_t* target,
                 float cap, const float* grad_scale, void* dlogits, int64_t ldd, void* stream);
+/* Action-token accuracy of one training step (train/monkey_patch.py:267-309): pred [B, >=L-1] int64 argmax ids
+ * (row stride ldp; pred[b,t] = argmax of logits[b,t]), labels [B, L] int64 (row stride ldl); gt[b,t] =
+ * labels[b,t+1].  ranges: HOST array of 6 inclusive token-id bounds {translation lo, hi, rotation lo, hi,
+ * gripper lo, hi}.  counts[8] (device, int64) = {n, correct} for {all action rows, translation, rotation,
+ * gripper}; acc[4] (device, fp32) = correct / n per class, computed as torch's float32 division (0/0 -> nan). */
+int svla_action_accuracy(int64_t B, int64_t L, const int64_t* pred, int64_t ldp, const int64_t* labels, int64_t ldl,
+                         const int64_t* ranges, int64_t* counts, float* acc, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Optimizer (DeepSpeed FusedAdam / torch AdamW semantics, scripts/zero1.json:23-34).

@@ -12,8 +12,9 @@ It restates, op for op and with the same bf16 rounding points, the reference eag
   * prefix-LM mask (:258-306), Gemma2 layers (model/modeling_gemma2.py:60-506), normalizer (:741-742),
     lm_head + softcap (:993-997), shifted masked CE (modeling_spatialvla.py:415-430).
   * ZoeDepth itself is the transformers module (3p), run frozen under no_grad as in the reference.
-Pinned by tests/test_oracle_cpu.py against tests/golden/*.safetensors, which oracle/gen_golden.py
-produced by running the reference's own code.
+  * the per-step action metrics of the patched Trainer.compute_loss (train/monkey_patch.py:267-324).
+Pinned by tests/test_cpu.py (and tests/test_action_tokenizer.py) against tests/golden/*, which
+oracle/gen_golden.py, gen_action_golden.py and gen_metrics_golden.py produced by running the reference's own code.
 """
 import math
 from typing import Dict, Optional
@@ -380,3 +381,26 @@ def build_params_random(cfg: dict, seed: int, dtype=BF16):
             t.requires_grad_(True)
         P[n] = t
     return P
+
+
+# ---------------------------------------------------------------------------------------- action metrics
+def action_metrics(pred: torch.Tensor, labels: torch.Tensor, ranges, actions=None, decode=None) -> Dict[str, float]:
+    """train/monkey_patch.py:267-324: pred [B, >= L-1] argmax ids of logits[:, :-1], labels [B, L]; ranges = (trans lo,
+    hi, rot lo, hi, grip lo, hi) inclusive token ids.  Accuracies as float32 divisions; with `actions` [B, n, 7] and
+    `decode` (SpatialActionTokenizer.decode_token_ids_to_actions), the L1 loss of the decoded predictions."""
+    t_lo, t_hi, r_lo, r_hi, g_lo, g_hi = (int(v) for v in ranges)
+    L = labels.shape[1]
+    shift_pred = pred[:, :L - 1]
+    shift_labels = labels[:, 1:]
+    mask = (shift_labels >= t_lo) & (shift_labels <= g_hi)                                     # :270-272
+    gt, pr = shift_labels[mask], shift_pred[mask]
+    ok = gt == pr
+    out = {"accuracy": float(ok.sum().float() / mask.sum().float())}                          # :275
+    for name, lo, hi in (("translation", t_lo, t_hi), ("rotation", r_lo, r_hi), ("gripper", g_lo, g_hi)):
+        m = (gt >= lo) & (gt <= hi)                                                             # :282, :288, :294
+        out[name + "_accuracy"] = float((gt[m] == pr[m]).sum().float() / m.sum().float())       # :304-306
+    if actions is not None and decode is not None:                                              # :308-311
+        gt_a = actions.reshape(-1, 7).to(device="cpu", dtype=torch.float32)
+        pa = decode(pr.cpu().numpy().reshape(-1, 3))
+        out["l1_loss"] = float(F.l1_loss(torch.tensor(pa), gt_a))
+    return out

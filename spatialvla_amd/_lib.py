@@ -101,6 +101,8 @@ SIGNATURES = {
     "svla_add_bf16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "svla_ce_finalize": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "svla_ce_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp]),
+    "svla_action_accuracy": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(c_i64), c_vp, c_vp,
+                                     c_vp]),
     "svla_sumsq_bf16": (c_i32, [c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "svla_adamw": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32,
                            c_vp, c_vp]),

@@ -260,14 +260,16 @@ __global__ __launch_bounds__(NT) void attn_decode_split_kernel(svla_attn_decode_
     __syncthreads();
     if (tid == 0) {
       int* cnt = f.cnt + (int64_t)bq * a.Hkv + hk;
-      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // agent-scope release (the barrier above orders every wave's partial stores before it) / acquire pair:
+      // the ordering the combine relies on is the memory model's, not only the sc1 ISA behaviour
+      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = old == nch - 1;
       if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sc[0][0] = last ? 1.f : 0.f;  // broadcast through the existing LDS array
     }
     __syncthreads();
     if (sc[0][0] == 0.f) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the sc1 loads stay below
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread: the partials of other XCDs are visible
     // combine (attn_decode_combine_kernel's arithmetic and order), chunks in batches of CB whose sc1 loads are all
     // issued before the first use
     constexpr int CB = 8;

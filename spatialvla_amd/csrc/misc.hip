@@ -553,3 +553,60 @@ extern "C" int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh,
                      (bf16_t*)du, lddu);
   return svla::check_launch("geglu_bwd");
 }
+
+// ---------------------------------------------------------------- action-token accuracy (integer, bit-exact)
+// train/monkey_patch.py:267-309: pred[b,t] = argmax over V of logits[b,t] (t < L-1), gt[b,t] = labels[b,t+1];
+// rows with gt in [trans_lo, grip_hi] count; correct = gt == pred, split by the translation / rotation / gripper id
+// ranges.  One workgroup (a step has ~10^4 rows); integer sums, so the result is order-independent.
+__global__ __launch_bounds__(1024) void action_accuracy_kernel(int64_t B, int64_t L, const int64_t* pred,
+                                                               int64_t ldp, const int64_t* labels, int64_t ldl,
+                                                               int64_t t_lo, int64_t t_hi, int64_t r_lo,
+                                                               int64_t r_hi, int64_t g_lo, int64_t g_hi,
+                                                               int64_t* counts, float* acc) {
+  __shared__ int64_t red[8][1024 / 64];
+  int64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // {n, ok} x {all, translation, rotation, gripper}
+  const int64_t rows = B * (L - 1);
+  for (int64_t i = threadIdx.x; i < rows; i += blockDim.x) {
+    const int64_t b = i / (L - 1), t = i % (L - 1);
+    const int64_t gt = labels[b * ldl + t + 1];
+    if (gt < t_lo || gt > g_hi) continue;
+    const int64_t ok = pred[b * ldp + t] == gt ? 1 : 0;
+    c[0] += 1;
+    c[1] += ok;
+    const int k = (gt >= t_lo && gt <= t_hi) ? 1 : (gt >= r_lo && gt <= r_hi) ? 2 : (gt >= g_lo && gt <= g_hi) ? 3 : 0;
+    if (k) {
+      c[2 * k] += 1;
+      c[2 * k + 1] += ok;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int64_t v = c[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[j][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    int64_t v = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[threadIdx.x][k];
+    counts[threadIdx.x] = v;
+    red[threadIdx.x][0] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4)  // torch: correct.sum().float() / mask.sum().float() (0/0 -> nan)
+    acc[threadIdx.x] = (float)red[2 * threadIdx.x + 1][0] / (float)red[2 * threadIdx.x][0];
+}
+
+extern "C" int svla_action_accuracy(int64_t B, int64_t L, const int64_t* pred, int64_t ldp, const int64_t* labels,
+                                    int64_t ldl, const int64_t* ranges, int64_t* counts, float* acc, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && L > 1 && pred && labels && ranges && counts && acc && ldp >= L - 1 && ldl >= L,
+                 "action_accuracy: bad args");
+  SVLA_CHECK_ARG(ranges[0] <= ranges[1] && ranges[1] < ranges[2] && ranges[2] <= ranges[3] && ranges[3] < ranges[4] &&
+                     ranges[4] <= ranges[5],
+                 "action_accuracy: token ranges must be ordered translation < rotation < gripper");
+  hipLaunchKernelGGL(action_accuracy_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, L, pred, ldp, labels,
+                     ldl, ranges[0], ranges[1], ranges[2], ranges[3], ranges[4], ranges[5], counts, acc);
+  return svla::check_launch("action_accuracy");
+}

@@ -103,10 +103,9 @@ class ZeroExchange:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
-        self.nccl = self.world > 1 and dist.get_backend(process_group) == "nccl"
         self.chunk = [(e - s) // self.world for s, e in buckets]
-        self._rs = {}        # bucket -> pending reduce-scatter (work, out-of-place buffer or None)
-        self._ag = {}        # bucket -> pending all-gather (work, out-of-place buffer or None)
+        self._rs = {}        # bucket -> pending reduce-scatter work
+        self._ag = {}        # bucket -> pending all-gather work
         self.ready_end: Dict[object, int] = {}  # grad hook point -> flat index below which every grad is written
         self.wait_buckets: Dict[object, List[int]] = {}  # parameter wait point -> buckets to wait for
 
@@ -126,16 +125,13 @@ class ZeroExchange:
                 self._reduce_scatter(b)
 
     def _reduce_scatter(self, b):
+        """In place: the output is this rank's chunk of the input bucket (NCCL's in-place form).  The same call on
+        every backend -- RCCL on the GPUs, gloo in the CPU tests -- so the tests run the code path of the 8-GPU
+        run.  AVG on bf16: RCCL rounds to bf16 at every ring hop (DESIGN.md §6 states the bound)."""
         s, e = self.buckets[b]
         o, c = self.owned(b)
-        src = self.fg[s:e]
-        if self.nccl:  # in place: the output is this rank's chunk of the input (NCCL's in-place form)
-            w = dist.reduce_scatter_tensor(self.fg[o:o + c], src, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
-            self._rs[b] = (w, None)
-        else:  # gloo (CPU tests, shared-GPU rehearsals): sum-all-reduce a copy, keep this rank's chunk
-            tmp = src.float()
-            w = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            self._rs[b] = (w, tmp)
+        self._rs[b] = dist.reduce_scatter_tensor(self.fg[o:o + c], self.fg[s:e], op=dist.ReduceOp.AVG,
+                                                 group=self.pg, async_op=True)
 
     def finish_reduce(self):
         """Launch the buckets no hook covered and wait for every reduce-scatter (stream-ordered on nccl)."""
@@ -144,33 +140,27 @@ class ZeroExchange:
         for b in range(len(self.buckets)):
             if b not in self._rs:
                 self._reduce_scatter(b)
-        for b, (w, out) in self._rs.items():
+        for w in self._rs.values():
             w.wait()
-            if out is not None:
-                o, c = self.owned(b)
-                r = o - self.buckets[b][0]
-                self.fg[o:o + c].copy_(out[r:r + c] / self.world)
         self._rs.clear()
 
     # ---------------------------------------------------------------- step: all-gather
     def all_gather(self, b):
+        """In place: the input is this rank's chunk of the output bucket.  Left in flight; the forward's parameter
+        wait points (or land_before_update) complete it."""
         if self.world == 1:
             return
         s, e = self.buckets[b]
         o, c = self.owned(b)
-        if self.nccl:  # in place: the input is this rank's chunk of the output
-            self._ag[b] = (dist.all_gather_into_tensor(self.fp[s:e], self.fp[o:o + c], group=self.pg, async_op=True),
-                           None)
-        else:
-            parts = [torch.empty(c, dtype=self.fp.dtype, device=self.fp.device) for _ in range(self.world)]
-            self._ag[b] = (dist.all_gather(parts, self.fp[o:o + c].clone(), group=self.pg, async_op=True), parts)
+        self._ag[b] = dist.all_gather_into_tensor(self.fp[s:e], self.fp[o:o + c], group=self.pg, async_op=True)
 
     def _land(self, b):
-        w, parts = self._ag.pop(b)
-        w.wait()
-        if parts is not None:
-            s, e = self.buckets[b]
-            self.fp[s:e].copy_(torch.cat(parts))
+        self._ag.pop(b).wait()
+
+    def land(self, b):
+        """Complete bucket b's all-gather if one is in flight (before AdamW rewrites its send buffer)."""
+        if b in self._ag:
+            self._land(b)
 
     def wait_params(self, point):
         for b in self.wait_buckets.get(point, ()):
@@ -229,6 +219,12 @@ class TrainEngine:
                 bstart = n
         self.params = [e[0] for e in entries]
         self.offsets = offs
+        vision = set()
+        for mod in (getattr(model, "vision_tower", None), getattr(model, "multi_modal_projector", None),
+                    getattr(model, "position_embedding_3d", None)):
+            if mod is not None:
+                vision.update(id(p) for p in mod.parameters())
+        self.vision_slices = [(o, p.numel()) for p, o in zip(self.params, offs) if id(p) in vision]
         self.numel = n
         self.buckets = buckets
         self.flat_param = torch.zeros(n, dtype=BF16, device=dev)
@@ -290,6 +286,8 @@ class TrainEngine:
                 vt._svla_layer_grad_hook = lambda i: ex.on_grads_ready(("siglip", i))
             for mod in (model, model.language_model, lm, vt):  # wait points: "pre", ("siglip", i), ("gemma", i), "head"
                 mod._svla_param_wait = ex.wait_params
+            # inference entry points (predict_action) replay captured graphs that contain no wait points
+            model._svla_param_wait_all = ex.wait_all_params
 
     # ------------------------------------------------------------------ optimizer
     def lr_at(self, step: int) -> float:
@@ -323,6 +321,9 @@ class TrainEngine:
                     self.eps, self.wd, self.step_count, self.clip)
             return
         for b in self.gather_order:
+            # a bucket no forward wait point landed (e.g. SigLIP's after a text-only batch) still has last step's
+            # gather in flight, reading the chunk AdamW is about to rewrite
+            ex.land(b)
             o, c = ex.owned(b)
             so = self.shard_offsets[b]
             Kx.adamw(self.master[so:so + c], self.flat_param[o:o + c], self.flat_grad[o:o + c], self.m[so:so + c],
@@ -330,9 +331,14 @@ class TrainEngine:
             ex.all_gather(b)
 
     def train_step(self, batch: Dict[str, torch.Tensor]):
-        """forward + backward + ZeRO-1 exchange + clip + AdamW; returns the loss tensor (no host sync)."""
+        """forward + backward + ZeRO-1 exchange + clip + AdamW; returns the loss tensor (no host sync).
+        A batch without pixel_values leaves the vision-side gradients unwritten: they are zeroed (an unused
+        parameter's gradient is zero, as in the reference's DeepSpeed step), not left at the previous step's."""
         out = self.model(**batch, return_dict=True)
         out.loss.backward()
+        if batch.get("pixel_values") is None:
+            for o, n in self.vision_slices:
+                self.flat_grad[o:o + n].zero_()
         self.exchange.finish_reduce()
         self.optimizer_step()
         return out.loss.detach()

@@ -449,12 +449,17 @@ def attn_decode(q, Lq, k_cache, v_cache, Lk, Hq, Hkv, D, scale, softcap, kv_clas
 # svla_attn_decode_rope workspaces: zeroed once, one per (device, stream) -- the arrival counters at their head
 # return to zero after every launch, so a buffer is reused by every later call (and by captured graph replays)
 _DECODE_WS = {}
+# every workspace ever handed out stays allocated: a graph captured against a smaller one keeps its raw pointer
+# (and its zeroed arrival counters), so a replacement must never return the old buffer to the caching allocator
+_DECODE_WS_RETIRED = []
 
 
 def _decode_rope_ws(nbytes, device):
     key = (device.index, _stream())
     ws = _DECODE_WS.get(key)
     if ws is None or ws.numel() < nbytes:
+        if ws is not None:
+            _DECODE_WS_RETIRED.append(ws)
         ws = torch.zeros(max(nbytes, 8 << 20), dtype=torch.uint8, device=device)
         _DECODE_WS[key] = ws
     return ws
@@ -578,6 +583,25 @@ def ce_bwd(N, logits, lse, target, cap, grad_scale, dlogits):
     M = logits.shape[0]
     L.check(L.lib().svla_ce_bwd(M, N, logits.data_ptr(), _ld(logits), lse.data_ptr(), target.data_ptr(), cap,
                                 grad_scale.data_ptr(), dlogits.data_ptr(), _ld(dlogits), _stream()), "ce_bwd")
+
+
+def action_accuracy(pred: torch.Tensor, labels: torch.Tensor, ranges, counts=None, acc=None):
+    """svla_action_accuracy: pred [B, >= L-1] int64 argmax ids (pred[b, t] for logits[b, t]), labels [B, L] int64,
+    ranges = 6 inclusive token-id bounds (translation, rotation, gripper).  Returns (counts int64 [8], acc fp32 [4])
+    on the device: {overall, translation, rotation, gripper} accuracy (train/monkey_patch.py:267-309)."""
+    B, Lp = pred.shape
+    _req(labels.dim() == 2 and labels.shape[0] == B and Lp >= labels.shape[1] - 1, "action_accuracy: shapes")
+    _req(pred.dtype == labels.dtype == torch.int64 and pred.is_cuda and labels.is_cuda, "action_accuracy: int64 CUDA")
+    _req(pred.stride(1) == 1 and labels.stride(1) == 1, "action_accuracy: rows must be contiguous")
+    if counts is None:
+        counts = torch.empty(8, dtype=torch.int64, device=pred.device)
+    if acc is None:
+        acc = torch.empty(4, dtype=torch.float32, device=pred.device)
+    rg = (ctypes.c_int64 * 6)(*[int(v) for v in ranges])
+    L.check(L.lib().svla_action_accuracy(B, labels.shape[1], pred.data_ptr(), pred.stride(0), labels.data_ptr(),
+                                         labels.stride(0), rg, counts.data_ptr(), acc.data_ptr(), _stream()),
+            "svla_action_accuracy")
+    return counts, acc
 
 
 def sumsq(x_flat, out, n_partial=4096):

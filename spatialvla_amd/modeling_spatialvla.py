@@ -242,6 +242,13 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                        self.uv_h.float().contiguous(), patch_size, reso, self.config.n_freqs, feat, xyz)
         return xyz
 
+    def _wait_all_params(self):
+        """ZeRO-1: land every parameter all-gather still in flight (TrainEngine leaves them to the next forward's
+        wait points, which a replayed inference graph does not contain)."""
+        wait_all = getattr(self, "_svla_param_wait_all", None)
+        if wait_all is not None:
+            wait_all()
+
     def _wait_params(self):
         pwait = getattr(self, "_svla_param_wait", None)  # ZeRO-1: embeddings / projector / Ego3D all-gathered
         if pwait is not None:
@@ -425,6 +432,44 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         (train/monkey_patch.py:267 uses logits[..., :-1, :].argmax(-1))."""
         return self.last_stash.get("argmax")
 
+    def action_token_ranges(self, action_tokenizer=None):
+        """Inclusive token-id bounds (translation lo, hi, rotation lo, hi, gripper lo, hi) of the spatial action
+        tokens: from `action_tokenizer` (or self.action_tokenizer, as train/monkey_patch.py:270-297 reads them) when
+        given, else the canonical 4096 / 4096 / 2 split of the spatial_token_num tokens at action_token_begin_idx
+        (scripts/action_config.json)."""
+        at = action_tokenizer if action_tokenizer is not None else getattr(self, "action_tokenizer", None)
+        if at is not None:
+            return tuple(int(v) for t in (at.translation_tokenizer, at.rotation_tokenizer, at.gripper_tokenizer)
+                         for v in (t.token_start_idx, t.token_end_idx))
+        a0, n = int(self.config.action_token_begin_idx), int(self.config.spatial_token_num)
+        if n != 8194:
+            raise ValueError("action_token_ranges: pass the action tokenizer (non-canonical spatial_token_num)")
+        return (a0, a0 + 4095, a0 + 4096, a0 + 8191, a0 + 8192, a0 + 8193)
+
+    def action_metrics(self, labels: torch.Tensor, actions: Optional[torch.Tensor] = None, action_tokenizer=None,
+                       argmax: Optional[torch.Tensor] = None):
+        """The per-step metrics of the reference's compute_loss (train/monkey_patch.py:267-324) for the last
+        training forward: accuracy, translation_accuracy, rotation_accuracy, gripper_accuracy as device fp32
+        scalars, from the argmax the lm_head epilogue already produced (no [B, L, V] argmax pass, no host sync);
+        with `actions` and an action tokenizer also l1_loss, decoded on the host as the reference does (:308-311)."""
+        B, Lq = labels.shape
+        am = argmax if argmax is not None else self.action_argmax()
+        if am is None:
+            raise ValueError("action_metrics: no argmax of a previous forward (run a training forward first)")
+        am = am.view(B, -1)
+        ranges = self.action_token_ranges(action_tokenizer)
+        _counts, acc = K.action_accuracy(am, labels.contiguous(), ranges)
+        out = {"accuracy": acc[0], "translation_accuracy": acc[1], "rotation_accuracy": acc[2],
+               "gripper_accuracy": acc[3]}
+        at = action_tokenizer if action_tokenizer is not None else getattr(self, "action_tokenizer", None)
+        if actions is not None and at is not None:
+            sl = labels[:, 1:]
+            mask = (sl >= ranges[0]) & (sl <= ranges[5])
+            pred_ids = am[:, :Lq - 1][mask].cpu().numpy().reshape(-1, 3)
+            gt = actions.reshape(-1, 7).to(device="cpu", dtype=torch.float32)
+            out["l1_loss"] = F.l1_loss(torch.tensor(at.decode_token_ids_to_actions(pred_ids)), gt)
+        return out
+
     # ------------------------------------------------------------------ inference
     def new_cache(self, batch_size: int, capacity: int) -> Gemma2KVCache:
         """An empty KV cache for `capacity` tokens per sequence (prompt + generated)."""
@@ -498,7 +543,10 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         cap = -(-capacity // self.DECODE_CAPACITY_STEP) * self.DECODE_CAPACITY_STEP
         key = (B, cap, str(dev))
         st = states.get(key)
-        wptr = self.language_model.lm_head.weight.data_ptr()
+        # the graphs hold raw pointers: to the weights (rebound by TrainEngine) and, with fp8 projections, to the
+        # e4m3 weight copies, which the next eager forward after an optimizer step (WEIGHT_EPOCH) frees and rebuilds
+        fp8 = any(getattr(l.mlp, "_svla_fp8", None) is not None for l in self.language_model.model.layers)
+        wptr = (self.language_model.lm_head.weight.data_ptr(), Fn.WEIGHT_EPOCH[0] if fp8 else -1)
         if st is not None and st["wptr"] != wptr:  # weights were rebound since capture: the graphs are stale
             states.pop(key)
             st = None
@@ -630,6 +678,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         (:294) and fills the cache; decode: one token per step at position P+i+1 (:473-474), no pixel values
         after step 0 (:475-476), attending to the prompt and every earlier generated token.  Stops when every
         sequence has emitted eos or after max_new_tokens."""
+        self._wait_all_params()
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
         self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
@@ -689,6 +738,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
     def predict_action_uncached(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):
         """The same greedy decode as full re-forwards over prompt + generated tokens (no cache): prompt keys
         class 0, generated keys class 1.  Kept as the parity reference of the cached path."""
+        self._wait_all_params()
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
         self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id

@@ -114,7 +114,20 @@ def _stats(logits, grads, gold, cfg):
             n = k[len("gradsum."):]
             gr[n] = H.rel_l2(_sketch(n, grads[n]), v.float())
     st["gradnorm"], st["gradrow"] = gn, gr
+    # the 13 labelled (action-token) rows: argmax vs the reference where its top-1/top-2 margin > 0.05
+    conf_rows = rows[margin[rows] > H.MARGIN]
+    st["action_rows_conf"] = int(conf_rows.numel())
+    st["action_rows_conf_agree"] = int(agree[conf_rows].sum())
     return st
+
+
+def _dump(name, payload):
+    """Parity numbers of a run, as JSON: $SVLA_PARITY_DIR (default gpurun_out/parity, which gpurun merges back;
+    the builder copies them to profiles/)."""
+    d = os.environ.get("SVLA_PARITY_DIR", os.path.join(H.REPO, "gpurun_out", "parity"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, name), "w") as f:
+        json.dump(payload, f, indent=1, sort_keys=True)
 
 
 @pytest.mark.timeout(900)
@@ -139,6 +152,9 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
                 if n in hip_grads and not n.endswith("self_attn.k_proj.bias")}
     del P, ograds, ologits
     torch.cuda.empty_cache()
+    _dump("full4b_bf16.json", {"loss": {"hip": float(loss), "oracle_gpu": float(oloss),
+                                         "reference": float(gold["out.loss"][0])},
+                                "hip": hip, "oracle_gpu": ora, "full_tensor_grad_rel_vs_oracle_gpu": full_rel})
     summary = {k: (hip[k], ora[k]) for k in ("act", "cols", "lse", "agree_005", "agree_025", "agree_action_rows")}
     worst_n = sorted(hip["gradnorm"].items(), key=lambda kv: -kv[1])[:3]
     ratio = {n: hip["gradrow"][n] / max(ora["gradrow"][n], 5e-2 / 1.5) for n in hip["gradrow"]}
@@ -204,3 +220,35 @@ def test_full4b_train_step_b32_adamw(model4b, cuda):
     assert float(eng.gnorm) > 0 and float(eng.clip) <= 1.0
     assert H.rel_l2(eng.master[o:o + n] - master0, ref.detach() - master0) < 1e-4
     assert torch.equal(eng.flat_param[o:o + n], eng.master[o:o + n].to(torch.bfloat16))
+
+
+@pytest.mark.timeout(900)
+def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
+    """configs[4] (fp8 e4m3 q|k|v, o, gate|up, down forward and dgrad projections; attention and weight gradients
+    bf16) on the whole 4B model against the reference's bf16 golden: the fp8 quantisation error is the tolerance."""
+    batch = {k[3:]: v.to(cuda) for k, v in gold.items() if k.startswith("in.")}
+    model4b.train()
+    model4b.vision_zoe_model.eval()
+    model4b.enable_fp8_projections(True)
+    try:
+        loss, logits, grads, _ = H.run_hip(model4b, batch, depth=gold["out.depth"])
+    finally:
+        model4b.enable_fp8_projections(False)
+        model4b.zero_grad(set_to_none=True)
+    st = _stats(logits, grads, gold, model4b.config)
+    del logits
+    _dump("full4b_fp8.json", {"loss": {"hip_fp8": float(loss), "reference": float(gold["out.loss"][0])}, "hip_fp8": st})
+    worst = sorted(st["gradnorm"].items(), key=lambda kv: -kv[1])[:5]
+    print(f"4B fp8 vs reference: loss {float(loss):.5f} / {float(gold['out.loss'][0]):.5f}; act {st['act']:.4f} "
+          f"cols {st['cols']:.4f} lse {st['lse']:.4f} agree_025 {st['agree_025']:.4f} agree_005 {st['agree_005']:.4f} "
+          f"action rows {st['action_rows_conf_agree']}/{st['action_rows_conf']}; grad norm worst {worst}")
+    assert torch.isfinite(loss)
+    assert abs(float(loss) - float(gold["out.loss"][0])) < FP8_TOL["loss"]
+    assert st["act"] <= FP8_TOL["logits"] and st["cols"] <= FP8_TOL["logits"]
+    assert st["lse"] <= FP8_TOL["lse"]
+    assert st["agree_025"] >= FP8_TOL["agree_025"]
+    assert max(st["gradnorm"].values()) < FP8_TOL["gradnorm"], worst
+
+
+# configs[4] tolerances vs the reference's bf16 (provisional, set from the first measurement)
+FP8_TOL = {"loss": 0.1, "logits": 0.15, "lse": 0.2, "agree_025": 0.9, "gradnorm": 0.25}
