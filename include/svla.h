@@ -203,8 +203,9 @@ int svla_attn_decode(const svla_attn_decode_args* a, void* out, int64_t ldo, flo
 
 /* The decode step's attention in ONE launch: svla_qkv_rope_append + svla_attn_decode fused (same results, bitwise).
  * a->q / a->ldq point at the raw q|k|v projection rows (row b*Lq+t: Hq q heads, Hkv k heads, Hkv v heads, not yet
- * rotated); the new tokens sit at positions p0 = Lk-Lq .. Lk-1 and use RoPE table row t (rope_cos/rope_sin [Lq,
- * >=D/2], rope_ld).  The rotated k and the v rows are appended to cache rows p0+t; q is not written back.
+ * rotated); the new tokens sit at cache rows p0 = Lk-Lq .. Lk-1 and token row b*Lq+t uses RoPE table row b*Lq+t
+ * (rope_cos/rope_sin [B*Lq, >=D/2], rope_ld): per-sequence positions, as the reference's generate derives them
+ * from attention_mask.cumsum(-1) for padded prompts (modeling_gemma2.py:1039-1042).  The rotated k and the v rows are appended to cache rows p0+t; q is not written back.
  * workspace: >= svla_attn_decode_rope_workspace_bytes(...) bytes, 256-B aligned, ZEROED ONCE by the caller (its
  * head holds arrival counters that every launch returns to zero; one workspace per stream).
  * Replaces modeling_gemma2.py:123-154 (RoPE), :387-395 (HybridCache update) and :169-195 (eager attention). */
@@ -212,7 +213,7 @@ size_t svla_attn_decode_rope_workspace_bytes(int32_t B, int32_t Lq, int32_t Hq, 
 int svla_attn_decode_rope(const svla_attn_decode_args* a, const void* rope_cos, const void* rope_sin, int64_t rope_ld,
                           void* out, int64_t ldo, void* workspace, size_t ws_bytes, void* stream);
 
-/* Decode-step q|k|v epilogue: rotate_half RoPE on q in place (rows b*Lq+t of qkv, position table row t) and on
+/* Decode-step q|k|v epilogue: rotate_half RoPE on q in place (rows b*Lq+t of qkv, position table row b*Lq+t) and on
  * k, rotated k and plain v written to cache rows p0+t (k/v cache element (b, j, h, d) at base + b*bs + j*ld + h*D + d).
  * Replaces apply_rotary_pos_emb + the HybridCache update (model/modeling_gemma2.py:123-154, :387-395). */
 int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,

@@ -267,6 +267,75 @@ def gen_decode_tiny():
     print("decode_tiny tokens", toks.tolist())
 
 
+def padded_decode_mask(am, n_new):
+    """additive [B,1,L,L] of a padded greedy decode: the inference prefill mask (bidirectional, padded key columns
+    masked: modeling_spatialvla.py:291-305 with is_training False) for prompt rows; generated row t sees the valid
+    prompt keys and generated tokens <= t (HybridCache decode, modeling_gemma2.py:387-395)."""
+    B, P = am.shape
+    L = P + n_new
+    m = decode_mask(P, L, B).clone()
+    mn = torch.finfo(torch.bfloat16).min
+    pad_cols = torch.cat([am == 0, torch.zeros(B, n_new, dtype=torch.bool)], 1)  # [B, L]
+    return torch.where(pad_cols[:, None, None, :], torch.full((), mn, dtype=torch.bfloat16), m)
+
+
+@torch.no_grad()
+def ref_greedy_padded(model, ids, am, pv, intr, n_new):
+    """Greedy decode of a left-padded batch through the reference forward, no cache: per-sequence positions as
+    prepare_inputs_for_generation derives them (attention_mask.cumsum(-1) - 1, pads 1, modeling_gemma2.py:1039-1042;
+    + 1, modeling_spatialvla.py:473-474), the generate-time attention mask extended by ones."""
+    B, P = ids.shape
+    cur, toks, margins = ids, [], []
+    for step in range(n_new):
+        Lc = cur.shape[1]
+        am_c = torch.cat([am, torch.ones(B, Lc - P, dtype=am.dtype)], 1)
+        pos = am_c.long().cumsum(-1) - 1
+        pos.masked_fill_(am_c == 0, 1)
+        pos = pos + 1
+        mask = padded_decode_mask(am, Lc - P)
+        out = model(input_ids=cur, pixel_values=pv, intrinsic=intr, attention_mask=mask, position_ids=pos,
+                    use_cache=False, return_dict=True)
+        last = out.logits[:, -1].float()
+        top2 = last.topk(2, -1).values
+        nxt = last.argmax(-1, keepdim=True)
+        toks.append(nxt)
+        margins.append((top2[:, 0] - top2[:, 1])[:, None])
+        cur = torch.cat([cur, nxt], 1)
+        print(f"  padded decode step {step}: tokens {nxt.view(-1).tolist()} margins {margins[-1].view(-1).tolist()}",
+              flush=True)
+    return torch.cat(toks, 1), torch.cat(margins, 1)
+
+
+def gen_decode_padded():
+    """decode_padded: B=3 prompts of different lengths, left-padded (pad id 0, attention_mask 0), greedy 6 tokens."""
+    cfgd = presets.tiny()
+    model, cfg = build_reference_model(cfgd)
+    model.eval()
+    b = presets.synthetic_batch(cfgd, batch=3, seed=21)
+    t = batch_tensors(b)
+    P = int((t["token_type_ids"][0] == 0).sum())
+    ids = t["input_ids"][:, :P].clone()
+    am = torch.ones_like(ids)
+    n_img = int((ids[0] == cfg.image_token_index).sum())
+    for row, drop in ((0, 5), (2, 2)):  # shorter prompts: drop text tokens after the image block, pad on the left
+        keep = torch.cat([ids[row, :n_img + 1], ids[row, n_img + 1 + drop:]])
+        ids[row] = torch.cat([torch.zeros(drop, dtype=ids.dtype), keep])
+        am[row, :drop] = 0
+    cap = {}
+    orig_bp = model.backproject_patch
+
+    def bp(K, depth, patch_size=14, reso=2):
+        cap.setdefault("depth", depth.detach().clone())
+        return orig_bp(K, depth, patch_size=patch_size, reso=reso)
+    model.backproject_patch = bp
+    toks, margins = ref_greedy_padded(model, ids, am, t["pixel_values"], t["intrinsic"], 6)
+    save_file({"in.input_ids": ids.contiguous(), "in.attention_mask": am.contiguous(),
+               "in.pixel_values": t["pixel_values"].contiguous(), "in.intrinsic": t["intrinsic"].contiguous(),
+               "out.depth": cap["depth"].contiguous(), "out.tokens": toks.contiguous(),
+               "out.margins": margins.contiguous()}, os.path.join(OUT, "decode_padded.safetensors"))
+    print("decode_padded tokens", toks.tolist())
+
+
 def gen_full4b():
     """The whole 4B model, hash-initialised, B=1 training step + greedy decode of 4 tokens."""
     import time
@@ -331,5 +400,7 @@ if __name__ == "__main__":
         gen_layer4b()
     if "decode_tiny" in which:
         gen_decode_tiny()
+    if "decode_padded" in which:
+        gen_decode_padded()
     if "full4b" in which:
         gen_full4b()

@@ -148,7 +148,7 @@ def prefix_mask(attn_mask, tt, is_training, L, dtype):
     return cm
 
 
-def gemma_layer(P, tc, i, h, mask, cos, sin, prefix="language_model.model."):
+def gemma_layer(P, tc, i, h, mask, cos, sin, prefix="language_model.model.", attn_sink=None):
     p = lambda n: P[f"{prefix}layers.{i}.{n}"]  # noqa: E731
     eps = tc["rms_norm_eps"]
     B, L, H = h.shape
@@ -172,6 +172,8 @@ def gemma_layer(P, tc, i, h, mask, cos, sin, prefix="language_model.model."):
     a = torch.tanh(a / cap) * cap
     a = a + mask[:, :, :, :L]
     a = F.softmax(a, dim=-1, dtype=torch.float32).to(q.dtype)
+    if attn_sink is not None:  # output_attentions (:193-195 returns attn_weights)
+        attn_sink.append(a)
     o = torch.matmul(a, v).transpose(1, 2).reshape(B, L, -1)
     o = _lin(o, p("self_attn.o_proj.weight"))
     h = r + rms(o, p("post_attention_layernorm.weight"), eps)
@@ -185,7 +187,7 @@ def gemma_layer(P, tc, i, h, mask, cos, sin, prefix="language_model.model."):
 # ---------------------------------------------------------------------------------------- full model
 def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor], zoe_model=None,
             is_training: Optional[bool] = None, depth: Optional[torch.Tensor] = None, cap: Optional[dict] = None,
-            mask4d: Optional[torch.Tensor] = None):
+            mask4d: Optional[torch.Tensor] = None, attn_sink: Optional[list] = None):
     """Returns (loss or None, logits bf16 [B, L, V]).  `P` maps reference parameter names -> tensors
     (vision keys without the 4.47 `vision_model.` infix, as transformers 5 names them).  mask4d: an explicit
     additive [B, 1, L, L] mask, passed through as the reference passes a 4-D attention_mask
@@ -230,11 +232,13 @@ def forward(P: Dict[str, torch.Tensor], cfg: dict, batch: Dict[str, torch.Tensor
         am = torch.ones_like(ids)
     mask = mask4d if mask4d is not None else prefix_mask(am, tt if tt is not None else torch.zeros_like(ids),
                                                          is_training, L, dt)
-    pos = (torch.arange(L, device=ids.device) + 1)[None]
+    pos = batch.get("position_ids")  # given: used as is (:367-372); generate passes per-sequence ones
+    if pos is None:
+        pos = (torch.arange(L, device=ids.device) + 1)[None]
     cos, sin = rope_tables(pos, tc["head_dim"], dt, tc.get("rope_theta", 10000.0))
     h = emb * torch.tensor(tc["hidden_size"] ** 0.5, dtype=dt)
     for i in range(tc["num_hidden_layers"]):
-        h = gemma_layer(P, tc, i, h, mask, cos, sin)
+        h = gemma_layer(P, tc, i, h, mask, cos, sin, attn_sink=attn_sink)
     h = rms(h, P["language_model.model.norm.weight"], tc["rms_norm_eps"])
     logits = _lin(h, P["language_model.lm_head.weight"])
     fc = tc["final_logit_softcapping"]
@@ -270,13 +274,19 @@ def greedy_decode(P, cfg, batch, zoe_model=None, n_new: int = 4, depth=None):
     top-2 logit margin [B, n])."""
     ids = batch["input_ids"]
     B, Pl = ids.shape
+    am = batch.get("attention_mask")
     toks, margins = [], []
     cur = ids
     for _ in range(n_new):
         Lc = cur.shape[1]
         b = {"input_ids": cur, "pixel_values": batch["pixel_values"], "intrinsic": batch["intrinsic"]}
-        _, logits = forward(P, cfg, b, zoe_model, is_training=False, depth=depth,
-                            mask4d=decode_mask(Pl, Lc, B).to(cur.device))
+        mask = decode_mask(Pl, Lc, B).to(cur.device)
+        if am is not None:  # padded prompts (generate): per-sequence positions, padded key columns masked
+            am_c = torch.cat([am, torch.ones(B, Lc - Pl, dtype=am.dtype, device=am.device)], 1)
+            pos = am_c.long().cumsum(-1) - 1                                      # modeling_gemma2.py:1039-1042
+            b["position_ids"] = pos.masked_fill(am_c == 0, 1) + 1                 # modeling_spatialvla.py:473-474
+            mask = mask.masked_fill((am_c == 0)[:, None, None, :], torch.finfo(mask.dtype).min)
+        _, logits = forward(P, cfg, b, zoe_model, is_training=False, depth=depth, mask4d=mask)
         last = logits[:, -1].float()
         top2 = last.topk(2, -1).values
         nxt = last.argmax(-1, keepdim=True)

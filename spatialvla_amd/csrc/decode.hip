@@ -137,14 +137,15 @@ __global__ __launch_bounds__(NT) void attn_decode_split_kernel(svla_attn_decode_
       const int g = i / D, d = i % D, dl = d % HALF;
       const bool lo = d < HALF;
       const float x = bf2f(qrow[g * D + d]), xp = bf2f(qrow[g * D + (lo ? d + HALF : d - HALF)]);
-      qs[g][d] = rope_elem(x, xp, bf2f(f.cos[(int64_t)t * f.rope_ld + dl]), bf2f(f.sin[(int64_t)t * f.rope_ld + dl]), lo);
+      qs[g][d] = rope_elem(x, xp, bf2f(f.cos[(int64_t)bq * f.rope_ld + dl]), bf2f(f.sin[(int64_t)bq * f.rope_ld + dl]), lo);
     }
     for (int i = tid; i < (n1 - n0) * D; i += NT) {
       const int kk = i / D, d = i % D, dl = d % HALF, tt = n0 + kk - p0;
       const bool lo = d < HALF;
       const bf16_t* kr = new_row(tt) + (int64_t)(a.Hq + hk) * D;
       const float r = rope_elem(bf2f(kr[d]), bf2f(kr[lo ? d + HALF : d - HALF]),
-                                bf2f(f.cos[(int64_t)tt * f.rope_ld + dl]), bf2f(f.sin[(int64_t)tt * f.rope_ld + dl]), lo);
+                                bf2f(f.cos[((int64_t)b * a.Lq + tt) * f.rope_ld + dl]),
+                                bf2f(f.sin[((int64_t)b * a.Lq + tt) * f.rope_ld + dl]), lo);
       kn[kk][d] = r;
       if (t == 0) ((bf16_t*)a.k)[(int64_t)b * a.bsk + (int64_t)(n0 + kk) * a.ldk + (int64_t)hk * D + d] = f2bf(r);
     }
@@ -407,8 +408,8 @@ __global__ void qkv_rope_append_kernel(int B, int Lq, int Hq, int Hkv, int D, bf
     float xl[8], xh[8], cs[8], sn[8], ol[8], oh[8];
     unpack8(*reinterpret_cast<const u32x4*>(lo), xl);
     unpack8(*reinterpret_cast<const u32x4*>(hi), xh);
-    unpack8(*reinterpret_cast<const u32x4*>(cos_t + (int64_t)t * rope_ld + dd), cs);
-    unpack8(*reinterpret_cast<const u32x4*>(sin_t + (int64_t)t * rope_ld + dd), sn);
+    unpack8(*reinterpret_cast<const u32x4*>(cos_t + m * rope_ld + dd), cs);  // table row = token row b*Lq+t
+    unpack8(*reinterpret_cast<const u32x4*>(sin_t + m * rope_ld + dd), sn);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       ol[j] = round_bf(xl[j] * cs[j]) + round_bf(-xh[j] * sn[j]);

@@ -315,12 +315,17 @@ class GemmaAttentionFn(torch.autograd.Function):
     pre-rotation q/k (RoPE transpose), which is what the projection backward needs."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg, f8: Optional[FP8Weights] = None):
+    def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg, f8: Optional[FP8Weights] = None,
+                capture: Optional[dict] = None):
         x = _c(x)
         M, H = x.shape
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
-        rope = (cos, sin, cfg.L, cfg.D, qd + kd)
+        if cos.shape[0] != cfg.L and torch.is_grad_enabled() and x.requires_grad:
+            # the attention backward applies the RoPE transpose with table row = position in the sequence
+            raise NotImplementedError("per-sequence position_ids are an inference path (the reference's training "
+                                      "positions are shared: modeling_spatialvla.py:367-372)")
+        rope = (cos, sin, cos.shape[0], cfg.D, qd + kd)
         if f8 is not None:
             _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, kind=L.EPI_ROPE, rope=rope)
         else:
@@ -330,6 +335,8 @@ class GemmaAttentionFn(torch.autograd.Function):
         a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window)
         K.attn_fwd(a, attn, lse)
+        if capture is not None:  # output_attentions: the rotated q|k|v rows (no copy)
+            capture["qkv"] = qkv
         out = _empty(M, wo.shape[0], like=x)
         if f8 is not None:
             _fp8_linear(attn, f8, "o", (wo,), out)
@@ -381,7 +388,31 @@ class GemmaAttentionFn(torch.autograd.Function):
                     K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
                 off += n
         rets = [d[2] for d in dests]
-        return (dx, *rets, ret_wo, None, None, None, None, None)
+        return (dx, *rets, ret_wo, None, None, None, None, None, None)
+
+
+@torch.no_grad()
+def gemma_attention_weights(qkv, kv_class, cfg: GemmaAttnCfg) -> torch.Tensor:
+    """output_attentions of the reference eager attention (modeling_gemma2.py:169-195): softmax probabilities
+    [B, Hq, L, L] in bf16, from the rotated q / k rows the fused projection wrote.  The attention OUTPUT always comes
+    from the HIP kernel, which never materialises these L x L maps; this is an introspection path (torch ops, the
+    reference's op order and bf16 roundings: bf16 scores * scale, bf16 softcap, + additive mask, fp32 softmax)."""
+    B, L, Hq, Hkv, D = cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D
+    qd, kd = Hq * D, Hkv * D
+    q = qkv[:, :qd].reshape(B, L, Hq, D).transpose(1, 2)
+    k = qkv[:, qd:qd + kd].reshape(B, L, Hkv, D).transpose(1, 2)
+    k = k.repeat_interleave(Hq // Hkv, dim=1)                                   # repeat_kv (:157-166)
+    w = torch.matmul(q, k.transpose(2, 3)) * cfg.scale
+    if cfg.softcap:
+        w = torch.tanh(w / cfg.softcap) * cfg.softcap
+    mn = torch.finfo(w.dtype).min
+    i = torch.arange(L, device=qkv.device)
+    cls = (kv_class if kv_class is not None else torch.zeros(B, L, dtype=torch.uint8, device=qkv.device))[:, :L]
+    vis = (cls[:, None, :] == 0) | ((cls[:, None, :] == 1) & (i[None, :, None] >= i[None, None, :]))
+    if cfg.window:  # sliding layers (:461-473): keys at distance >= window are masked
+        vis = vis & ((i[:, None] - i[None, :]) < cfg.window)[None]
+    w = w + torch.where(vis, 0.0, mn).to(w.dtype)[:, None]
+    return torch.softmax(w, dim=-1, dtype=torch.float32).to(qkv.dtype)
 
 
 # decode steps run RoPE + cache append + attention as one launch (svla_attn_decode_rope); False = the two-launch
@@ -403,7 +434,10 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     qkv = _empty(M, qd + 2 * kd, like=x)
     attn = _empty(M, qd, like=x)
     if p0 > 0:
-        # decode step: plain projection, then one launch rotates q / k, appends k / v to the cache and attends
+        # decode step: plain projection, then one launch rotates q / k, appends k / v to the cache and attends;
+        # the kernels read table row b*Lq+t (per-sequence positions), so a shared table is repeated per sequence
+        if cos.shape[0] != B * Lq:
+            cos, sin = cos.repeat(B, 1), sin.repeat(B, 1)
         K.linear_fwd(x, [wq, wk, wv], qkv)
         if DECODE_FUSED[0]:
             K.attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
@@ -413,7 +447,7 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
             K.attn_decode(qkv[:, :qd], Lq, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
                           cfg.softcap, kv_class, cfg.window, attn)
     else:
-        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, Lq, cfg.D, qd + kd))
+        K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, cos.shape[0], cfg.D, qd + kd))
         k_cache[:, :Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
         v_cache[:, :Lq].copy_(qkv[:, qd + kd:].view(B, Lq, kd))
     if p0 == 0:

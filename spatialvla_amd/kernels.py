@@ -474,8 +474,8 @@ def attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, Lk, Hq, Hkv, D, scale,
     _req(qkv.shape[1] >= (Hq + 2 * Hkv) * D, "attn_decode_rope: qkv narrower than q|k|v")
     _req(k_cache.shape[1] >= Lk and v_cache.shape[1] >= Lk and Lk > Lq, "attn_decode_rope: cache / Lk")
     _req(k_cache.stride(2) == 1 and v_cache.stride(2) == 1, "attn_decode_rope: cache rows must be contiguous")
-    _req(cos.shape[0] >= Lq and cos.shape == sin.shape and cos.stride(1) == 1 and cos.stride(0) == sin.stride(0),
-         "attn_decode_rope: tables")
+    _req(cos.shape[0] >= B * Lq and cos.shape == sin.shape and cos.stride(1) == 1 and cos.stride(0) == sin.stride(0),
+         "attn_decode_rope: tables must hold one row per token row b*Lq+t")
     _req(kv_class is None or (kv_class.dtype == torch.uint8 and kv_class.shape[0] == B and kv_class.stride(1) == 1),
          "attn_decode_rope: kv_class must be uint8 [B, >=Lk]")
     for t, n in ((qkv, "qkv"), (k_cache, "k"), (v_cache, "v"), (out, "out"), (cos, "cos"), (sin, "sin")):
@@ -498,7 +498,8 @@ def attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, Lk, Hq, Hkv, D, scale,
 def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
     """RoPE q in place, rotated k and v into cache rows p0.. (the decode step's q|k|v epilogue)."""
     _req(qkv.shape[0] == B * Lq and qkv.stride(1) == 1, "qkv_rope_append: qkv rows")
-    _req(cos.shape[0] >= Lq and cos.shape == sin.shape and cos.stride(1) == 1, "qkv_rope_append: tables")
+    _req(cos.shape[0] >= B * Lq and cos.shape == sin.shape and cos.stride(1) == 1,
+         "qkv_rope_append: tables must hold one row per token row b*Lq+t")
     _req(k_cache.shape[1] >= p0 + Lq and v_cache.shape[1] >= p0 + Lq, "qkv_rope_append: cache too short")
     for t, n in ((qkv, "qkv"), (cos, "cos"), (sin, "sin"), (k_cache, "k_cache"), (v_cache, "v_cache")):
         _chk_bf16(t, n)

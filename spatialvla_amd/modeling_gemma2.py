@@ -131,12 +131,16 @@ class Gemma2RotaryEmbedding(nn.Module):
 
     @torch.no_grad()
     def tables(self, position_ids: torch.Tensor, dtype) -> tuple:
-        """cos/sin [L, dim/2] in the activation dtype (reference :106-120 rounds them).
-        Positions must be shared by the batch (the kernel reads one table row per token)."""
+        """cos/sin in the activation dtype (reference :106-120 rounds them): [L, dim/2] when the batch
+        shares its positions (a [L] / [1, L] tensor or a stride-0 expand of one), else [B*L, dim/2], one row per
+        token (b, t) at row b*L + t -- the per-sequence positions the reference's generate derives for padded
+        prompts (modeling_gemma2.py:1039-1042).  The kernels read table row m % rows for token row m.  No host sync
+        (usable inside a graph capture)."""
         if position_ids.dim() == 2:
-            if position_ids.shape[0] > 1 and not bool((position_ids == position_ids[:1]).all()):
-                raise ValueError("per-row position_ids are not supported by the fused RoPE path")
-            position_ids = position_ids[0]
+            if position_ids.shape[0] == 1 or position_ids.stride(0) == 0:
+                position_ids = position_ids[0]
+            else:
+                position_ids = position_ids.reshape(-1)
         freqs = position_ids.float()[:, None] * self.inv_freq.float().to(position_ids.device)[None, :]
         return freqs.cos().to(dtype).contiguous(), freqs.sin().to(dtype).contiguous()
 
@@ -181,7 +185,8 @@ class Gemma2Attention(nn.Module):
         self.o_proj = nn.Linear(self.num_heads * self.head_dim, self.hidden_size, bias=False)
         self.rotary_emb = Gemma2RotaryEmbedding(self.head_dim, self.max_position_embeddings, self.rope_theta)
 
-    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None):
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None,
+                attn_sink: Optional[list] = None):
         B, Lq, H = hidden_states.shape
         cfg = Fn.GemmaAttnCfg(B, Lq, self.num_heads, self.num_key_value_heads, self.head_dim, self.scaling,
                               float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
@@ -192,9 +197,12 @@ class Gemma2Attention(nn.Module):
                                             self.v_proj.weight, self.o_proj.weight, cos, sin, cache.key_cache[i],
                                             cache.value_cache[i], cache.kv_class, cache.seen_tokens, cfg)
             return out.view(B, Lq, H)
+        capture = {} if attn_sink is not None else None
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
-                                        cfg, getattr(self, "_svla_fp8", None))
+                                        cfg, getattr(self, "_svla_fp8", None), capture)
+        if attn_sink is not None:
+            attn_sink.append(Fn.gemma_attention_weights(capture["qkv"], attention_mask.kv_class, cfg))
         return out.view(B, Lq, H)
 
 
@@ -228,13 +236,14 @@ class Gemma2DecoderLayer(nn.Module):
         self.self_attn._svla_fp8 = f8
         self.mlp._svla_fp8 = f8
 
-    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None):
+    def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None,
+                attn_sink: Optional[list] = None):
         # reference :475-496 (sandwich norms + residuals)
         # each residual-stream tensor has two consumers (pre-norm, residual add): a ResidualSlot sums their
         # gradients inside the pre-norm's backward kernel instead of an autograd add
         s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
         x = self.input_layernorm(hidden_states, s1)
-        a = self.self_attn(x, attention_mask, rope, cache)
+        a = self.self_attn(x, attention_mask, rope, cache, attn_sink)
         h = self.post_attention_layernorm.add_forward(hidden_states, a, s1)
         x = self.pre_feedforward_layernorm(h, s2)
         m = self.mlp(x)
@@ -258,7 +267,7 @@ class Gemma2Model(nn.Module):
         self.embed_tokens = value
 
     def forward(self, hidden_states, attention_mask: KVMask, position_ids, output_hidden_states=False,
-                cache: Optional[Gemma2KVCache] = None):
+                cache: Optional[Gemma2KVCache] = None, attn_sink: Optional[list] = None):
         """hidden_states: inputs_embeds already multiplied by the bf16 normalizer (fused in the merge
         kernel, reference :741-742).  With a cache, attention_mask holds the classes of the new tokens only
         (they are appended to the cache's classes) and the cache advances by the new tokens."""
@@ -267,6 +276,8 @@ class Gemma2Model(nn.Module):
                 raise ValueError("the KV cache is an inference path: run it under torch.no_grad()")
             cache.append_classes(attention_mask.kv_class)
         rope = self.layers[0].self_attn.rotary_emb.tables(position_ids, hidden_states.dtype)
+        if attn_sink is not None and cache is not None:
+            raise NotImplementedError("output_attentions with a KV cache: run the uncached forward")
         if cache is not None and not output_hidden_states:
             return self._forward_cached(hidden_states, attention_mask, rope, cache), None
         all_h = () if output_hidden_states else None
@@ -280,7 +291,7 @@ class Gemma2Model(nn.Module):
                 hidden_states.register_hook(lambda g, i=i: hook(i))
             if pwait is not None:
                 pwait(("gemma", i))
-            hidden_states = layer(hidden_states, attention_mask, rope, cache)
+            hidden_states = layer(hidden_states, attention_mask, rope, cache, attn_sink)
         if cache is not None:
             cache.seen_tokens += hidden_states.shape[1]
         if pwait is not None:

@@ -320,6 +320,33 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         out = Fn.EmbedMergeFn.apply(ids, img_index, img2d, spatial_w, embed_w, a0, normalizer, sort_rows, offsets)
         return out.view(B, Lq, hidden)
 
+    def _merge_embeds(self, input_ids, inputs_embeds, image_features):
+        """forward(inputs_embeds=...) (reference :361-387): the caller's embeddings instead of the table lookup, the
+        spatial-token override (x * 0.0 + spatial row, quirk Q10) and the image-slot scatter keyed by input_ids, then
+        the bf16 normalizer (modeling_gemma2.py:741-742).  Rare path: stock torch ops on the device, differentiable
+        in inputs_embeds, the spatial table and the image features."""
+        self._wait_params()
+        cfg = self.config
+        emb = inputs_embeds.to(self.multi_modal_projector.linear.weight.dtype).clone()
+        if cfg.use_spatial_token and input_ids is not None:
+            a0, na = int(cfg.action_token_begin_idx), int(cfg.spatial_token_num)
+            sel = (input_ids >= a0) & (input_ids < a0 + na)
+            emb[sel] = emb[sel] * 0.0 + self.spatial_embed_tokens.weight[input_ids[sel] - a0]
+        if image_features is not None:
+            m = (input_ids == cfg.image_token_index).unsqueeze(-1).expand_as(emb)
+            if self.strict_checks:
+                n_img = image_features.shape[0] * image_features.shape[1]
+
+                def check(n_tok, n_img=n_img):
+                    if n_tok != n_img:
+                        raise ValueError(
+                            "Number of images does not match number of special image tokens in the input text. "
+                            f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
+                self._defer((input_ids == cfg.image_token_index).sum(), check)
+            emb = emb.masked_scatter(m, image_features.to(emb.dtype))
+        normalizer = torch.tensor(cfg.text_config.hidden_size ** 0.5, dtype=emb.dtype, device=emb.device)
+        return emb * normalizer
+
     def _label_rows(self, target):
         """Rows with a label, for the lm_head backward, without a host sync: the labelled rows first in order
         (stable sort of the validity flag) and their count copied to pinned memory behind an event recorded
@@ -372,26 +399,31 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         cache = past_key_values
         if cache is not None and not isinstance(cache, Gemma2KVCache):
             raise ValueError("past_key_values must be a Gemma2KVCache (see new_cache())")
-        if cache is None and use_cache and not torch.is_grad_enabled():
-            cache = self.new_cache(input_ids.shape[0], input_ids.shape[1] + 256)
-        if inputs_embeds is not None:
-            raise NotImplementedError("inputs_embeds input is not supported on the HIP path; pass input_ids")
-        if output_attentions:
-            raise NotImplementedError("output_attentions is not available from the fused attention kernel")
         return_dict = True if return_dict is None else return_dict
         is_training = token_type_ids is not None and labels is not None  # reference :359
-        B, Lq = input_ids.shape
-        dev = input_ids.device
+        if input_ids is None:
+            if inputs_embeds is None:
+                raise ValueError("forward needs input_ids (and optionally inputs_embeds)")
+            if pixel_values is not None or self.config.use_spatial_token:
+                # the reference reads input_ids for the image slots and the spatial tokens (:363-365, :376)
+                raise ValueError("inputs_embeds without input_ids: the image and spatial-token merges need the ids")
+        B, Lq = (input_ids if input_ids is not None else inputs_embeds).shape[:2]
+        dev = (input_ids if input_ids is not None else inputs_embeds).device
+        if cache is None and use_cache and not torch.is_grad_enabled():
+            cache = self.new_cache(B, Lq + 256)
 
         image_features = None
         if pixel_values is not None:
             image_features = self.get_image_features(pixel_values, intrinsic)
 
-        if labels is not None:  # reference :390-395 (BC path: only when pad_token_id occurs in labels), sync-free
+        if labels is not None and input_ids is not None:  # reference :390-395 (BC path), sync-free
             has_pad = (labels == self.pad_token_id).any()
             labels = torch.where(has_pad & (input_ids == self.pad_token_id), -100, labels)
 
-        hidden = self._merge_inputs(input_ids, image_features)
+        if inputs_embeds is not None:
+            hidden = self._merge_embeds(input_ids, inputs_embeds, image_features)
+        else:
+            hidden = self._merge_inputs(input_ids, image_features)
         past = cache.seen_tokens if cache is not None else 0
         if position_ids is None:
             start = past if cache_position is None else int(cache_position[0])
@@ -407,8 +439,9 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             if attention_mask is not None:
                 cls = torch.where(attention_mask[:, -Lq:].to(dev) != 0, 1, 2).to(torch.uint8)
             mask = KVMask(cls.contiguous())
+        attn_sink = [] if output_attentions else None
         h, all_h = self.language_model.model(hidden, mask, position_ids, output_hidden_states=bool(output_hidden_states),
-                                             cache=cache)
+                                             cache=cache, attn_sink=attn_sink)
 
         target = self._targets(labels, attention_mask, B, Lq, dev)
         stash = {}
@@ -425,7 +458,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             out = (logits,)
             return (loss,) + out if loss is not None else out
         return SpatialVLACausalLMOutputWithPast(loss=loss, logits=logits, past_key_values=cache, hidden_states=all_h,
-                                                attentions=None, image_hidden_states=image_features)
+                                                attentions=tuple(attn_sink) if attn_sink is not None else None,
+                                                image_hidden_states=image_features)
 
     def action_argmax(self):
         """argmax over V of the last forward's logits [B*L] (int64), computed in the lm_head epilogue
@@ -522,14 +556,12 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         self.__dict__["_svla_decode_states"] = {}
 
     @staticmethod
-    def _reject_padding(am):
-        """Padded prompts are not supported by the HIP decode path: the reference's generate derives per-row
-        positions from attention_mask.cumsum(-1) - 1 (+1, modeling_gemma2.py:1039-1042,
-        modeling_spatialvla.py:473-474), while the fused RoPE here uses one position table for every row.
-        Raise instead of silently rotating padded rows with the wrong phases."""
-        if am is not None and bool((am == 0).any()):
-            raise ValueError("predict_action: padded prompts (attention_mask with zeros) are not supported on the "
-                             "HIP path; run equal-length prompts (one call per prompt length)")
+    def _prompt_positions(valid: torch.Tensor) -> torch.Tensor:
+        """Per-sequence positions of a (possibly padded) prompt, as the reference's generate derives them:
+        attention_mask.cumsum(-1) - 1, pads set to 1 (modeling_gemma2.py:1039-1042), then + 1
+        (modeling_spatialvla.py:473-474).  valid: bool [B, L]."""
+        pos = valid.to(torch.int64).cumsum(-1) - 1
+        return pos.masked_fill(~valid, 1) + 1
 
     def _decode_state(self, B: int, capacity: int, dev):
         """Persistent decode state per (batch, bucketed capacity): the KV cache, the static token buffer the captured
@@ -561,6 +593,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                   "eos": torch.full((1, 1), -1, dtype=torch.int64, device=dev),
                   "pad": torch.zeros(1, 1, dtype=torch.int64, device=dev),
                   "toks": torch.zeros(B, cap + 1, dtype=torch.int64, device=dev),
+                  "npad": torch.zeros(B, 1, dtype=torch.int64, device=dev),  # pads in each prompt (static input)
                   "cls": KVMask(torch.ones(B, 1, dtype=torch.uint8, device=dev)),
                   "pool": torch.cuda.graph_pool_handle() if dev.type == "cuda" else None,
                   "side": torch.cuda.Stream(device=dev) if dev.type == "cuda" else None}
@@ -573,7 +606,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         ids, cache = x["ids"], st["cache"]
         feats = (self.get_image_features(x["pv"], x["intr"], x["kinv"], x.get("depth")) if x["pv"] is not None
                  else None)
-        pos = (torch.arange(ids.shape[1], device=ids.device) + 1)[None]
+        pos = self._prompt_positions(x["cls"] != 2)  # per-sequence positions of a padded batch (1..P unpadded)
         strict, self.strict_checks = self.strict_checks, False  # checked on the host by predict_action
         try:
             hidden = self._merge_inputs(ids, feats)
@@ -629,7 +662,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
     def _decode_body(self, st, p0):
         """One decode step at cache position p0: the token in st["tok"] -> argmax of its logits [B]."""
         tok, cache = st["tok"], st["cache"]
-        pos = torch.full((1, 1), p0 + 1, dtype=torch.int64, device=tok.device)  # 1-indexed (:372, :473-474)
+        # 1-indexed (:372, :473-474); a sequence with n pads in its prompt is n positions behind its cache row
+        pos = (p0 + 1) - st["npad"]
         h, _ = self.language_model.model(self._merge_inputs(tok, None), st["cls"], pos, cache=cache)
         stash = {}
         tgt = torch.full((tok.shape[0],), -1, dtype=torch.int64, device=tok.device)
@@ -680,7 +714,6 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         sequence has emitted eos or after max_new_tokens."""
         self._wait_all_params()
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
-        self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         graphs = self.decode_graphs and dev.type == "cuda"
@@ -688,6 +721,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         cache = st["cache"]
         cache.seen_tokens = 0
         cls = self._prompt_classes(am, B, P, dev)
+        st["npad"].copy_((cls == 2).sum(-1, keepdim=True))
         if pv is not None and self.strict_checks:  # reference :379-385, checked before any graph replay
             vc = self.config.vision_config
             n_img = B * (vc.image_size // vc.patch_size) ** 2
@@ -740,7 +774,6 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         class 0, generated keys class 1.  Kept as the parity reference of the cached path."""
         self._wait_all_params()
         ids, pv, intr, am, dev = self._predict_inputs(model_inputs)
-        self._reject_padding(am)
         eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
         B, P = ids.shape
         feats = self.get_image_features(pv, intr) if pv is not None else None
@@ -753,7 +786,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             Lc = cur.shape[1]
             cls = torch.ones(B, Lc, dtype=torch.uint8, device=dev)
             cls[:, :P] = self._prompt_classes(am, B, P, dev)
-            pos = (torch.arange(Lc, device=dev) + 1)[None]
+            pos = self._prompt_positions(cls != 2)  # generated tokens: the attention mask extended by ones
             h, _ = self.language_model.model(self._merge_inputs(cur, feats), KVMask(cls.contiguous()), pos)
             nxt, finished = self._next_token(h, finished, eos)
             out.append(nxt)

@@ -78,6 +78,18 @@ def test_oracle_greedy_decode_matches_reference(tiny_oracle):
     assert torch.equal(margins, g["out.margins"])
 
 
+def test_oracle_padded_greedy_decode_matches_reference(tiny_oracle):
+    """Left-padded prompts of different lengths: per-sequence positions (attention_mask.cumsum) and masked pad keys
+    reproduce the reference model's greedy tokens and margins bit for bit (oracle/gen_golden.py gen_decode_padded)."""
+    import spatialvla_oracle as O
+    cfgd, P, zoe = tiny_oracle
+    g = _load("decode_padded.safetensors")
+    b = {k[3:]: v for k, v in g.items() if k.startswith("in.")}
+    toks, margins = O.greedy_decode(P, cfgd, b, zoe, n_new=g["out.tokens"].shape[1], depth=g["out.depth"])
+    assert torch.equal(toks, g["out.tokens"])
+    assert torch.equal(margins, g["out.margins"])
+
+
 def test_hash_init_bitwise_reproducible():
     """spatialvla_amd.detinit.hash_tensor: the counter-hash init of the 4B fixture -- independent of chunking and
     a pure function of (name, shape, seed); the GPU test repeats the check on the device."""

@@ -225,13 +225,17 @@ def test_qkv_rope_append(cuda, B, Lq, p0):
     kd = Hkv * D
     qkv = _r(B * Lq, (Hq + 2 * Hkv) * D)
     inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
-    f = (torch.arange(p0, p0 + Lq, device=cuda).float() + 1)[:, None] * inv[None]
+    # per-sequence positions (a padded batch: sequence b is 3b tokens shorter), table row b*Lq+t
+    pos = torch.cat([torch.arange(p0, p0 + Lq, device=cuda) - 3 * b for b in range(B)]).float() + 1
+    f = pos[:, None] * inv[None]
     cos, sin = f.cos().to(BF).contiguous(), f.sin().to(BF).contiguous()
     kc = torch.zeros(B, cap, kd, dtype=BF, device=cuda)
     vc = torch.zeros_like(kc)
     ref = qkv.clone()
     nrot = (Hq + Hkv) * D
-    ref[:, :nrot] = _rope_bf16(qkv[:, :nrot].view(B, Lq, Hq + Hkv, D), cos, sin).reshape(B * Lq, nrot)
+    for b in range(B):
+        rows = slice(b * Lq, (b + 1) * Lq)
+        ref[rows, :nrot] = _rope_bf16(qkv[rows, :nrot].view(1, Lq, Hq + Hkv, D), cos[rows], sin[rows]).reshape(Lq, nrot)
     Kn.qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, kc, vc, p0)
     assert torch.equal(qkv[:, :Hq * D], ref[:, :Hq * D])
     assert torch.equal(kc[:, p0:p0 + Lq].reshape(B * Lq, kd), ref[:, Hq * D:nrot])
@@ -251,8 +255,9 @@ def test_attn_decode_rope_fused_bitwise(cuda, B, Lq, p0, Hq, Hkv, D, window, use
     kd, Lk = Hkv * D, p0 + Lq
     cap = Lk + 9
     inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
-    f = (torch.arange(p0, p0 + Lq, device=cuda).float() + 1)[:, None] * inv[None]
-    emb = torch.cat([f, f], -1)  # HF layout [Lq, D] (the kernels read the first D/2 columns)
+    pos = torch.cat([torch.arange(p0, p0 + Lq, device=cuda) - 2 * b for b in range(B)]).float() + 1
+    f = pos[:, None] * inv[None]
+    emb = torch.cat([f, f], -1)  # HF layout [B*Lq, D] (the kernels read the first D/2 columns of row b*Lq+t)
     cos, sin = emb.cos().to(BF).contiguous(), emb.sin().to(BF).contiguous()
     kc0 = _r(B, cap, kd)
     vc0 = _r(B, cap, kd)
