@@ -353,6 +353,34 @@ int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int 
                          const float* params, float p_eps, float max_t, float min_t, float clamp_eps, float* out,
                          void* stream);
 
+/* Convolution on NHWC bf16 maps as an implicit GEMM (csrc/conv.hip): the frozen ZoeDepth DPT neck and depth heads
+ * (transformers zoedepth [3p]: ZoeDepthReassembleLayer projection / resize, the neck's 3x3 convs, the
+ * PreActResidualLayer pairs, FeatureFusionLayer projections, the relative-depth head), called by the reference at
+ * model/modeling_spatialvla.py:314-323.
+ *   out[b,oy,ox,co] = post( bf16(sum_{ky,kx,ci} pre(x[b, oy*stride+ky-pad, ox*stride+kx-pad, ci]) w[co,ky,kx,ci]
+ *                                + bias[co]) ), then out = bf16(out + res1), then out = bf16(out + res2)
+ * pre = ReLU with SVLA_CONV_PRE_RELU (DPT's pre-activation), post = ReLU with SVLA_CONV_POST_RELU; zero padding.
+ * w: [Cout][KH][KW][Cin] bf16 (the torch [Cout][Cin][KH][KW] weight permuted once).  x [B,H,W,Cin],
+ * out / res1 / res2 [B,OH,OW,Cout], all NHWC and 16-B aligned; Cin and Cout multiples of 8; x under 2 GiB.
+ * SVLA_CONV_TRANSPOSED: nn.ConvTranspose2d with kernel == stride == factor, padding 0: w [factor][factor][Cout][Cin],
+ * OH = H*factor, each input pixel's output block written once (no residuals, no pre-activation). */
+enum { SVLA_CONV_PRE_RELU = 1, SVLA_CONV_POST_RELU = 2, SVLA_CONV_TRANSPOSED = 4 };
+typedef struct {
+  int32_t B, H, W, Cin;
+  int32_t OH, OW, Cout;
+  int32_t KH, KW, stride, pad;
+  int32_t flags;
+  int32_t factor;
+  int32_t _pad;
+  const void* x;
+  const void* w;
+  const void* bias;   /* [Cout] bf16 or NULL */
+  const void* res1;   /* NULL or [B,OH,OW,Cout] */
+  const void* res2;   /* NULL or [B,OH,OW,Cout] */
+  void* out;
+} svla_conv_args;
+int svla_conv2d_nhwc(const svla_conv_args* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

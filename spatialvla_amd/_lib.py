@@ -54,6 +54,15 @@ class AttnDecodeArgs(ctypes.Structure):
                 ("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("bsk", c_i64),
                 ("v", c_vp), ("ldv", c_i64), ("bsv", c_i64), ("kv_class", c_vp), ("ldc", c_i64)]
 
+class ConvArgs(ctypes.Structure):
+    _fields_ = [("B", c_i32), ("H", c_i32), ("W", c_i32), ("Cin", c_i32), ("OH", c_i32), ("OW", c_i32),
+                ("Cout", c_i32), ("KH", c_i32), ("KW", c_i32), ("stride", c_i32), ("pad", c_i32),
+                ("flags", c_i32), ("factor", c_i32), ("_pad", c_i32), ("x", c_vp), ("w", c_vp), ("bias", c_vp),
+                ("res1", c_vp), ("res2", c_vp), ("out", c_vp)]
+
+
+CONV_PRE_RELU, CONV_POST_RELU, CONV_TRANSPOSED = 1, 2, 4
+
 # name -> (restype, argtypes); every entry point of include/svla.h
 SIGNATURES = {
     "svla_last_error": (ctypes.c_char_p, []),
@@ -101,6 +110,7 @@ SIGNATURES = {
     "svla_add_bf16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "svla_ce_finalize": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "svla_ce_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp]),
+    "svla_conv2d_nhwc": (c_i32, [ctypes.POINTER(ConvArgs), c_vp]),
     "svla_action_accuracy": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.POINTER(c_i64), c_vp, c_vp,
                                      c_vp]),
     "svla_sumsq_bf16": (c_i32, [c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),

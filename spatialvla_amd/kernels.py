@@ -704,3 +704,48 @@ def geglu_bwd(dh: torch.Tensor, g: torch.Tensor, u: torch.Tensor, dg: torch.Tens
     L.check(L.lib().svla_geglu_bwd(M, I, dh.data_ptr(), dh.stride(0), g.data_ptr(), g.stride(0), u.data_ptr(),
                                    u.stride(0), dg.data_ptr(), dg.stride(0), du.data_ptr(), du.stride(0), _stream()),
             "geglu_bwd")
+
+
+# ---------------------------------------------------------------------------------------- NHWC convolution
+def conv_weight_khwc(weight: torch.Tensor, transposed: bool = False) -> torch.Tensor:
+    """torch conv weight -> the svla_conv2d_nhwc layout: Conv2d [Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin];
+    ConvTranspose2d [Cin, Cout, f, f] -> [f, f, Cout, Cin]."""
+    if transposed:
+        return weight.permute(2, 3, 1, 0).contiguous()
+    return weight.permute(0, 2, 3, 1).contiguous()
+
+
+def conv2d_cl(x: torch.Tensor, w_khwc: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+              pad: int = 0, pre_relu: bool = False, post_relu: bool = False, res1: Optional[torch.Tensor] = None,
+              res2: Optional[torch.Tensor] = None, transposed: bool = False) -> torch.Tensor:
+    """svla_conv2d_nhwc on channels-last bf16 maps: x [B, Cin, H, W] (channels_last memory) -> [B, Cout, OH, OW]
+    channels_last.  w_khwc from conv_weight_khwc.  transposed: ConvTranspose2d with kernel == stride (w [f, f, Cout,
+    Cin]).  res1 / res2: channels-last maps of the output's shape added (each rounded to bf16) after bias + relu."""
+    _req(x.is_cuda and x.dtype == BF16 and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last),
+         "conv2d_cl: x must be a channels-last bf16 CUDA map")
+    B, Cin, H, W = x.shape
+    a = L.ConvArgs()
+    if transposed:
+        f, f2, Cout, Cw = w_khwc.shape
+        _req(f == f2 and Cw == Cin, "conv2d_cl: transposed weight must be [f, f, Cout, Cin]")
+        OH, OW, KH, KW = H * f, W * f, f, f
+        a.flags |= L.CONV_TRANSPOSED
+        a.factor = f
+    else:
+        Cout, KH, KW, Cw = w_khwc.shape
+        _req(Cw == Cin, f"conv2d_cl: weight Cin {Cw} != input channels {Cin}")
+        OH, OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    _req(w_khwc.is_contiguous() and w_khwc.dtype == BF16, "conv2d_cl: weight must be contiguous bf16")
+    out = torch.empty(B, Cout, OH, OW, dtype=BF16, device=x.device, memory_format=torch.channels_last)
+    for r, nm in ((res1, "res1"), (res2, "res2")):
+        _req(r is None or (r.shape == out.shape and r.dtype == BF16
+                           and r.is_contiguous(memory_format=torch.channels_last)),
+             f"conv2d_cl: {nm} must be a channels-last bf16 map of the output's shape")
+    _req(bias is None or (bias.dtype == BF16 and bias.is_contiguous() and bias.numel() == Cout), "conv2d_cl: bias")
+    a.B, a.H, a.W, a.Cin, a.OH, a.OW, a.Cout = B, H, W, Cin, OH, OW, Cout
+    a.KH, a.KW, a.stride, a.pad = KH, KW, stride, pad
+    a.flags |= (L.CONV_PRE_RELU if pre_relu else 0) | (L.CONV_POST_RELU if post_relu else 0)
+    a.x, a.w, a.bias, a.res1, a.res2, a.out = (x.data_ptr(), w_khwc.data_ptr(), _ptr(bias), _ptr(res1), _ptr(res2),
+                                               out.data_ptr())
+    L.check(L.lib().svla_conv2d_nhwc(ctypes.byref(a), _stream()), "svla_conv2d_nhwc")
+    return out

@@ -19,6 +19,12 @@ another order (tolerances in tests/test_model_gpu.py):
 * DPT readout projections (ZoeDepthReassembleStage.readout_projects[i] = Linear(2H, H) + exact GELU): one libsvla
   GEMM with the BIAS_GELU_ERF epilogue (bf16(gelu_erf(bf16(acc + b))), the eager module's rounding points) instead
   of the stock Linear (hipBLASLt) + elementwise GELU.
+* Every convolution (nn.Conv2d / nn.ConvTranspose2d instances: the BEiT patch projection, the DPT reassemble
+  projections and resizes, the neck's 3x3 convs, the fusion and relative-head convs, the metric head's 1x1 convs) on
+  libsvla: svla_conv2d_nhwc implicit-GEMM on channels-last maps (csrc/conv.hip), the patchify conv as im2col + GEMM;
+  ZoeDepthPreActResidualLayer fuses both ReLUs into its convs (pre-activation on the A fragments, post-activation in
+  the epilogue) and its residual add into the second conv's epilogue, and ZoeDepthFeatureFusionLayer adds the
+  skip branch in the same epilogue (bf16 rounding after each add, the module order).  No MIOpen / CK kernel runs.
 * Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
   relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
   and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
@@ -89,15 +95,130 @@ def _interp(x, size=None, scale_factor=None, mode="bilinear", align_corners=None
                                            align_corners=align_corners)
 
 
+def _fast_ok(x) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and not torch.is_grad_enabled()
+
+
+def _cl(x):
+    return x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+
+
+def _conv_params(conv):
+    """(weight in svla_conv2d_nhwc layout with Cout padded to a multiple of 8, bias padded, Cout) of a frozen conv,
+    cached against the parameters' storage and version."""
+    transposed = isinstance(conv, torch.nn.ConvTranspose2d)
+    key = (conv.weight.data_ptr(), conv.weight._version, conv.bias._version if conv.bias is not None else -1)
+    hit = getattr(conv, "_svla_w", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    from . import kernels as K
+    w = conv.weight.detach().to(torch.bfloat16)
+    cout = w.shape[1] if transposed else w.shape[0]
+    cp = (cout + 7) // 8 * 8
+    b = conv.bias.detach().to(torch.bfloat16) if conv.bias is not None else None
+    if cp != cout:
+        if transposed:
+            w = torch.cat([w, w.new_zeros(w.shape[0], cp - cout, *w.shape[2:])], 1)
+        else:
+            w = torch.cat([w, w.new_zeros(cp - cout, *w.shape[1:])], 0)
+        if b is not None:
+            b = torch.cat([b, b.new_zeros(cp - cout)])
+    out = (K.conv_weight_khwc(w, transposed=transposed), b.contiguous() if b is not None else None, cout)
+    conv._svla_w = (key, out)
+    return out
+
+
+def _conv_eligible(conv, x) -> bool:
+    if not _fast_ok(x) or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    if tuple(conv.dilation) != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
+        return False
+    if conv.stride[0] != conv.stride[1] or not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1]:
+        return False
+    return True
+
+
+def _conv2d_forward(self, x):
+    """nn.Conv2d.forward of the frozen estimator on libsvla: a patchify conv (kernel == stride, 3 input channels:
+    the BEiT patch projection) as im2col + one GEMM with the bias epilogue; anything with Cin % 8 == 0 as the
+    implicit-GEMM NHWC conv.  Output channels-last (Cout padded to 8 is sliced off as a view)."""
+    from . import kernels as K
+    k, s_, p_ = self.kernel_size[0], self.stride[0], self.padding[0]
+    if _conv_eligible(self, x):
+        B, C, H, W = x.shape
+        if C == 3 and k == s_ and p_ == 0 and H == W and H % k == 0 and self.bias is not None:
+            from . import _lib as L
+            np1 = H // k
+            kc = 3 * k * k
+            kp = (kc + 7) // 8 * 8
+            cols = torch.empty(B * np1 * np1, kp, dtype=torch.bfloat16, device=x.device)
+            K.im2col_patch(x.contiguous(), k, cols)
+            key = (self.weight.data_ptr(), self.weight._version)
+            hit = getattr(self, "_svla_wpatch", None)
+            if hit is None or hit[0] != key:
+                wk = torch.zeros(self.out_channels, kp, dtype=torch.bfloat16, device=x.device)
+                wk[:, :kc] = self.weight.detach().reshape(self.out_channels, kc)
+                hit = self._svla_wpatch = (key, wk, self.bias.detach().to(torch.bfloat16).contiguous())
+            out = torch.empty(B * np1 * np1, self.out_channels, dtype=torch.bfloat16, device=x.device)
+            K.linear_fwd(cols, [hit[1]], out, kind=L.EPI_BIAS, bias=hit[2])
+            return out.view(B, np1, np1, self.out_channels).permute(0, 3, 1, 2)
+        if C % 8 == 0:
+            w, b, cout = _conv_params(self)
+            y = K.conv2d_cl(_cl(x), w, b, stride=s_, pad=p_)
+            return y if y.shape[1] == cout else y[:, :cout]
+    return type(self).forward(self, x)
+
+
+def _convt_forward(self, x, output_size=None):
+    """nn.ConvTranspose2d.forward with kernel == stride, no padding (the DPT reassemble up-sampling) on the
+    implicit-GEMM kernel's pixel-shuffle epilogue."""
+    from . import kernels as K
+    if (output_size is None and _fast_ok(x) and self.groups == 1 and tuple(self.dilation) == (1, 1)
+            and self.kernel_size[0] == self.kernel_size[1] == self.stride[0] == self.stride[1]
+            and tuple(self.padding) == (0, 0) and tuple(self.output_padding) == (0, 0) and x.shape[1] % 8 == 0
+            and self.out_channels % 8 == 0):
+        w, b, _ = _conv_params(self)
+        return K.conv2d_cl(_cl(x), w, b, transposed=True)
+    return type(self).forward(self, x, output_size) if output_size is not None else type(self).forward(self, x)
+
+
+def _preact_ok(layer, x) -> bool:
+    return (not layer.use_batch_norm and _conv_eligible(layer.convolution1, x) and x.shape[1] % 8 == 0
+            and layer.convolution1.kernel_size[0] == 3 and layer.convolution1.stride[0] == 1
+            and layer.convolution2.out_channels % 8 == 0 and layer.convolution1.out_channels % 8 == 0)
+
+
+def _preact(layer, x, skip=None):
+    """ZoeDepthPreActResidualLayer (no batch norm): conv2(relu(conv1(relu(x)))) + x [+ skip], two launches: both
+    ReLUs fused into the convs, the residual (and the fusion layer's skip) added in conv2's epilogue."""
+    from . import kernels as K
+    w1, b1, _ = _conv_params(layer.convolution1)
+    w2, b2, _ = _conv_params(layer.convolution2)
+    x = _cl(x)
+    t = K.conv2d_cl(x, w1, b1, pad=1, pre_relu=True, post_relu=True)
+    return K.conv2d_cl(t, w2, b2, pad=1, res1=x, res2=_cl(skip) if skip is not None else None)
+
+
+def _preact_forward(self, hidden_state):
+    if _preact_ok(self, hidden_state):
+        return _preact(self, hidden_state)
+    return type(self).forward(self, hidden_state)
+
+
 def _fusion_forward(self, hidden_state, residual=None):
-    """ZoeDepthFeatureFusionLayer.forward (transformers zoedepth / dpt [3p]) with the resize on the HIP kernel."""
+    """ZoeDepthFeatureFusionLayer.forward (transformers zoedepth / dpt [3p]): the resize on the HIP kernel, the
+    residual unit of the skip branch with `hidden_state + unit(residual)` fused into its last conv's epilogue."""
     if residual is not None:
         if hidden_state.shape != residual.shape:
             residual = _interp(residual, size=(hidden_state.shape[2], hidden_state.shape[3]), mode="bilinear",
                                align_corners=False)
-        hidden_state = hidden_state + self.residual_layer1(residual)
+        if _preact_ok(self.residual_layer1, residual) and _fast_ok(hidden_state):
+            hidden_state = _preact(self.residual_layer1, residual, skip=hidden_state)
+        else:
+            hidden_state = hidden_state + self.residual_layer1(residual)
     hidden_state = self.residual_layer2(hidden_state)
-    hidden_state = _interp(hidden_state, scale_factor=2, mode="bilinear", align_corners=self.align_corners)
+    hidden_state = _interp(_cl(hidden_state) if _fast_ok(hidden_state) else hidden_state, scale_factor=2,
+                           mode="bilinear", align_corners=self.align_corners)
     return self.projection(hidden_state)
 
 
@@ -168,10 +289,11 @@ def _is_exact_gelu(m) -> bool:
     return name == "GELUActivation" and getattr(m, "act", None) in (torch.nn.functional.gelu,)
 
 
-def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout: bool = True) -> torch.nn.Module:
-    """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False / readout=False keep the stock
-    metric-head tail / BEiT layers / readout projections (the other paths are bitwise identical to the stock
-    modules)."""
+def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout: bool = True,
+            convs: bool = True) -> torch.nn.Module:
+    """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False / readout=False / convs=False keep
+    the stock metric-head tail / BEiT layers / readout projections / convolutions (the other paths are bitwise
+    identical to the stock modules)."""
     for m in zoe.modules():
         name = type(m).__name__
         if name == "ZoeDepthReassembleStage" and readout and hasattr(m, "readout_projects"):
@@ -197,5 +319,14 @@ def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout:
             m._svla_fast = True
         elif name == "ZoeDepthMetricDepthEstimationHead" and tail and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_metric_head_forward, m)
+            m._svla_fast = True
+        elif name == "ZoeDepthPreActResidualLayer" and convs and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_preact_forward, m)
+            m._svla_fast = True
+        elif type(m) is torch.nn.Conv2d and convs and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_conv2d_forward, m)
+            m._svla_fast = True
+        elif type(m) is torch.nn.ConvTranspose2d and convs and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_convt_forward, m)
             m._svla_fast = True
     return zoe

@@ -82,8 +82,10 @@ def run_hip(model, batch, depth=None):
     torch.cuda.synchronize()
     grads = {}
     for n, p in model.named_parameters():
-        if p.grad is not None:
-            grads[n.replace("vision_tower.vision_model.", "vision_tower.")] = p.grad.detach().float().cpu()
+        # under a TrainEngine the kernels write dW into the flat gradient buffer (p._svla_grad), not p.grad
+        g = p.grad if p.grad is not None else (getattr(p, "_svla_grad", None) if p.requires_grad else None)
+        if g is not None:
+            grads[n.replace("vision_tower.vision_model.", "vision_tower.")] = g.detach().float().cpu()
     return out.loss.detach().float().cpu(), out.logits.detach().float().cpu(), grads, model.action_argmax()
 
 

@@ -9,18 +9,18 @@ Noise floor.  Through 27 SigLIP and 26 Gemma2 layers in bf16, any GPU implementa
 from the CPU reference on logits, because GEMM blocking changes the fp32 accumulation order and the bf16 roundings
 compound.  The test therefore also runs the oracle (the plain-torch restatement of the reference, bit-exact to it
 on the CPU: tests/test_cpu.py) on the GPU with the same weights and inputs -- the noise of a correct bf16 GPU
-implementation that follows the reference's op sequence -- and holds the HIP path to:
+implementation that follows the reference's op sequence -- and holds the HIP path to (SURVEY §8(c) tolerances):
   vs the reference golden: loss 1e-2 absolute; per-row lse 2e-2 absolute; every gradient norm within 3e-2
     relative; logits (action-token range of the labelled rows; 256 fixed columns of every row) rel-L2 <=
-    max(1e-2, 1.5 x the oracle-on-GPU error); argmax identical wherever the reference's top-2 margin > 0.25, and on
-    margin > 0.05 rows at least as often as the oracle-on-GPU minus 1 %;
-  vs the oracle on the GPU (same device, same inputs): every trainable gradient, full tensor, rel-L2 <= 8e-2
-    (k_proj.bias excluded: its true gradient is 0, both sides hold rounding noise); measured maximum ~6e-2 on the
-    SigLIP q/k weights, the end of 53 bf16 layers of backward.
-The hash-signed gradient sketches of the golden (a +-1 sum of a matrix's rows) are printed, not asserted: in the
-early SigLIP layers of a random-init 4B model they are rounding-chaotic (the oracle itself misses by up to 0.8
-there), and the fused HIP kernels round at different points than the eager op chain, so they sit further from the
-CPU reference than the oracle does while staying within the full-tensor bound above.
+    max(1e-2, 1.5 x the oracle-on-GPU error); argmax identical on every labelled (action) row whose reference
+    top-1/top-2 margin > 0.05 and on every row with margin > 0.25, and on margin > 0.05 rows at least as often as
+    the oracle-on-GPU; the gradient sketch error over the gradient norm (an estimate of the full-tensor rel-L2 error
+    against the reference, see _stats): median <= 1.25x and 90th percentile <= 1.5x the oracle-on-GPU's, every
+    tensor <= 0.15;
+  vs the oracle on the GPU (same device, same inputs): every trainable gradient, full tensor, rel-L2 <= 3e-2, except
+    the named exceptions of _full_tol (q/k projections <= 8e-2, measured max 6.0e-2; gate_proj <= 4e-2, measured
+    max 3.1e-2), each with its reason below.  k_proj.bias is excluded: its true gradient is 0 (softmax is
+    invariant to a per-row shift of the logits), both sides hold rounding noise.
 The frozen Zoe depth is compared on its own (2e-2), then the reference's depth is fed to both paths."""
 import json
 import os
@@ -101,7 +101,7 @@ def _stats(logits, grads, gold, cfg):
     act = torch.zeros_like(agree)
     act[rows] = True
     st["agree_action_rows"] = float(agree[act].float().mean())
-    gn, gr = {}, {}
+    gn, gr, gs = {}, {}, {}
     for k, v in gold.items():
         if k.startswith("gradnorm."):
             n = k[len("gradnorm."):]
@@ -112,13 +112,47 @@ def _stats(logits, grads, gold, cfg):
                 gn[n] = abs(x.norm().item() - v.item()) / max(v.item(), 1e-12)
         if k.startswith("gradsum.") and not k.endswith("self_attn.k_proj.bias"):
             n = k[len("gradsum."):]
-            gr[n] = H.rel_l2(_sketch(n, grads[n]), v.float())
-    st["gradnorm"], st["gradrow"] = gn, gr
+            sk = _sketch(n, grads[n])
+            gr[n] = H.rel_l2(sk, v.float())
+            # the sketch error over the gradient's norm: for random +-1 row signs E|sum e_i dr_i|^2 = ||dG||_F^2, so
+            # this estimates the full-tensor rel-L2 error against the REFERENCE (only its sketch is in the golden);
+            # the sketch's own norm can be small by cancellation, which makes gradrow chaotic
+            gs[n] = float((sk - v.float()).norm()) / max(float(gold["gradnorm." + n]), 1e-12)
+    st["gradnorm"], st["gradrow"], st["gradsketch"] = gn, gr, gs
     # the 13 labelled (action-token) rows: argmax vs the reference where its top-1/top-2 margin > 0.05
     conf_rows = rows[margin[rows] > H.MARGIN]
     st["action_rows_conf"] = int(conf_rows.numel())
     st["action_rows_conf_agree"] = int(agree[conf_rows].sum())
     return st
+
+
+# Named exceptions to the 3e-2 full-tensor gradient bound: the q / k projection weights (and SigLIP's q bias) of
+# every attention layer.  Their gradient is d(scores) = P o (dP - rowsum) pushed through the other operand, and P is
+# rounded to bf16 before PV (reference modeling_gemma2.py:191 / SigLIP eager attention): dP's error relative to the
+# small centred softmax gradient is ~2-3x that of any other product, and it compounds over the layers above (the
+# deepest layers, 22-26, measure 5-6e-2).  v / o / MLP / norm gradients do not pass through that centring.
+QK_EXCEPTION_SUFFIXES = ("self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.q_proj.bias")
+
+
+def _qk_exception(name: str) -> bool:
+    return name.endswith(QK_EXCEPTION_SUFFIXES)
+
+
+# A second named exception: mlp.gate_proj.weight (<= 4e-2, measured r3 max 3.11e-2 in layers 17-25).  Its gradient
+# is dG = bf16(dH * u) * gelu_tanh'(g) taken at the forward's pre-activation g, whose bf16 noise grows with depth
+# (26 layers of forward rounding), and gelu' is steepest around 0 where most g sit; up_proj (dH * gelu(g)) and
+# down_proj gradients stay under 3e-2.
+def _full_tol(name: str) -> float:
+    if _qk_exception(name):
+        return 8e-2
+    if name.endswith("mlp.gate_proj.weight"):
+        return 4e-2
+    return H.GRAD_TOL
+
+
+def _pct(vals, q):
+    v = sorted(vals)
+    return v[min(len(v) - 1, int(round(q / 100 * (len(v) - 1))))]
 
 
 def _dump(name, payload):
@@ -171,11 +205,20 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
     assert hip["act"] <= max(H.LOGITS_TOL, 1.5 * ora["act"])
     assert hip["cols"] <= max(H.LOGITS_TOL, 1.5 * ora["cols"])
     assert hip["agree_025"] == 1.0
-    # margin 0.05 is below one bf16 ulp of logits of magnitude 8-30 (0.06-0.125): those rows are ties at the
-    # logits' precision, so only a loose bound (8 of 256 rows) -- the 0.25-margin rows above must agree exactly
-    assert hip["agree_005"] >= ora["agree_005"] - 0.03
+    assert hip["action_rows_conf"] > 0 and hip["action_rows_conf_agree"] == hip["action_rows_conf"]
+    assert hip["agree_005"] >= ora["agree_005"]
     assert max(hip["gradnorm"].values()) < H.GRAD_TOL, worst_n
-    assert len(full_rel) > 700 and max(full_rel.values()) <= 8e-2, worst_f
+    # gradient sketches vs the reference golden: a one-dimensional random projection per column, so a single
+    # tensor's value is a noisy estimate (errors of weight gradients are low rank); bound the distribution against
+    # the oracle-on-GPU's (measured r3: median 0.0251 vs 0.0253, max 0.110) and every tensor absolutely
+    hs, os_ = hip["gradsketch"], ora["gradsketch"]
+    assert len(hs) > 700
+    assert _pct(hs.values(), 50) <= 1.25 * _pct(os_.values(), 50), (_pct(hs.values(), 50), _pct(os_.values(), 50))
+    assert _pct(hs.values(), 90) <= 1.5 * _pct(os_.values(), 90), (_pct(hs.values(), 90), _pct(os_.values(), 90))
+    assert max(hs.values()) <= 0.15, sorted(hs.items(), key=lambda kv: -kv[1])[:5]
+    assert len(full_rel) > 700
+    bad_f = {n: e for n, e in full_rel.items() if e > _full_tol(n)}
+    assert not bad_f, sorted(bad_f.items(), key=lambda kv: -kv[1])[:8]
 
 
 @pytest.mark.timeout(600)
@@ -191,35 +234,11 @@ def test_full4b_greedy_decode_vs_reference(model4b, gold, cuda):
     out = model4b.predict_action(inputs, max_new_tokens=ref.shape[1], eos_token_id=-1)
     n_cmp, n_ok = H.greedy_tokens_agree(out, ref, margins)
     print(f"4B decode {out.tolist()} vs reference {ref.tolist()} (margins {margins.tolist()}): {n_ok}/{n_cmp}")
-    assert n_ok >= 1
+    # every step before the first near-tie (reference margin <= 0.05) must match; greedy_tokens_agree asserts it
+    # per step, this pins the count (golden margins 0.31 / 0.16 / 0.28 / 0.03: 3 tokens)
+    conf = int((margins[0].float() > H.MARGIN).long().cumprod(0).sum())
+    assert conf >= 1 and n_ok >= conf
     del model4b.predict_depth
-
-
-@pytest.mark.timeout(900)
-def test_full4b_train_step_b32_adamw(model4b, cuda):
-    """configs[2] at its full size: one TrainEngine step at B=32 -- finite loss near ln(V), and an AdamW slice equal
-    to torch.optim.AdamW applied to the same (clipped) gradients and master weights."""
-    from spatialvla_amd import presets
-    from spatialvla_amd.engine import TrainEngine
-    model4b.train()
-    model4b.vision_zoe_model.eval()
-    eng = TrainEngine(model4b, lr=2e-5, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0)
-    b = H.batch_tensors(presets.synthetic_batch(H.cfg_dict("spatialvla_4b"), batch=32, seed=77), cuda)
-    p = model4b.language_model.model.layers[5].mlp.gate_proj.weight
-    i = next(j for j, q in enumerate(eng.params) if q is p)
-    o, n = eng.offsets[i], p.numel()
-    master0 = eng.master[o:o + n].clone()
-    loss = eng.train_step(b)
-    torch.cuda.synchronize()
-    assert torch.isfinite(loss) and 10.0 < float(loss) < 16.0, float(loss)
-    g = eng.flat_grad[o:o + n].float() * eng.clip
-    ref = torch.nn.Parameter(master0.clone())
-    opt = torch.optim.AdamW([ref], lr=eng.lr_at(0), betas=eng.betas, eps=eng.eps, weight_decay=0.0)
-    ref.grad = g
-    opt.step()
-    assert float(eng.gnorm) > 0 and float(eng.clip) <= 1.0
-    assert H.rel_l2(eng.master[o:o + n] - master0, ref.detach() - master0) < 1e-4
-    assert torch.equal(eng.flat_param[o:o + n], eng.master[o:o + n].to(torch.bfloat16))
 
 
 @pytest.mark.timeout(900)
@@ -252,3 +271,31 @@ def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
 
 # configs[4] tolerances vs the reference's bf16 (provisional, set from the first measurement)
 FP8_TOL = {"loss": 0.1, "logits": 0.15, "lse": 0.2, "agree_025": 0.9, "gradnorm": 0.25}
+
+
+@pytest.mark.timeout(900)
+def test_full4b_train_step_b32_adamw(model4b, cuda):
+    """configs[2] at its full size: one TrainEngine step at B=32 -- finite loss near ln(V), and an AdamW slice equal
+    to torch.optim.AdamW applied to the same (clipped) gradients and master weights.  Runs LAST in this module: the
+    optimizer step moves the shared model's weights away from the golden's."""
+    from spatialvla_amd import presets
+    from spatialvla_amd.engine import TrainEngine
+    model4b.train()
+    model4b.vision_zoe_model.eval()
+    eng = TrainEngine(model4b, lr=2e-5, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0)
+    b = H.batch_tensors(presets.synthetic_batch(H.cfg_dict("spatialvla_4b"), batch=32, seed=77), cuda)
+    p = model4b.language_model.model.layers[5].mlp.gate_proj.weight
+    i = next(j for j, q in enumerate(eng.params) if q is p)
+    o, n = eng.offsets[i], p.numel()
+    master0 = eng.master[o:o + n].clone()
+    loss = eng.train_step(b)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss) and 10.0 < float(loss) < 16.0, float(loss)
+    g = eng.flat_grad[o:o + n].float() * eng.clip
+    ref = torch.nn.Parameter(master0.clone())
+    opt = torch.optim.AdamW([ref], lr=eng.lr_at(0), betas=eng.betas, eps=eng.eps, weight_decay=0.0)
+    ref.grad = g
+    opt.step()
+    assert float(eng.gnorm) > 0 and float(eng.clip) <= 1.0
+    assert H.rel_l2(eng.master[o:o + n] - master0, ref.detach() - master0) < 1e-4
+    assert torch.equal(eng.flat_param[o:o + n], eng.master[o:o + n].to(torch.bfloat16))

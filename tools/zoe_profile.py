@@ -13,7 +13,7 @@ with torch.device("cuda"):
     zoe = ZoeDepthForDepthEstimation(cfg).to(torch.bfloat16).eval()
 if os.environ.get("ZFAST", "1") == "1":  # the product's fast paths (spatialvla_amd/zoe_fast.py)
     from spatialvla_amd import zoe_fast
-    zoe_fast.install(zoe)
+    zoe_fast.install(zoe, convs=os.environ.get("ZCONV", "1") == "1")
 pix = torch.rand(B, 3, 224, 224, device="cuda").to(torch.bfloat16)
 
 
@@ -31,7 +31,7 @@ t0 = time.time()
 for _ in range(3):
     run()
 torch.cuda.synchronize()
-print(f"zoe forward B={B}: {(time.time() - t0) / 3 * 1e3:.1f} ms", flush=True)
+print(f"zoe forward B={B} convs={os.environ.get('ZCONV', '1')}: {(time.time() - t0) / 3 * 1e3:.1f} ms", flush=True)
 from torch.profiler import profile, ProfilerActivity
 with profile(activities=[ProfilerActivity.CUDA, ProfilerActivity.CPU], record_shapes=True) as prof:
     run()
