@@ -637,8 +637,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
             torch.cuda.current_stream().wait_stream(side)
             graph = torch.cuda.CUDAGraph()
             try:
-                # captured on the warm-up stream: the per-stream handles of the libraries the frozen Zoe forward still
-                # calls (MIOpen and the GEMM back end it uses at B=1) exist there, none is created under capture
+                # captured on the warm-up stream, where the eager warm-up ran (lazy kernel attributes, weight caches)
                 with torch.cuda.graph(graph, pool=st["pool"], stream=side):
                     out = self._prefill_body(st, static)
             except RuntimeError as e:  # an op of the prefill cannot be captured: run this shape eagerly from now on
@@ -731,12 +730,9 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                                  f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
         # inv(K) (reference :221): the closed-form HIP inverse, captured into the prefill graph with the rest
         kinv = None
+        # the frozen Zoe forward is captured with the rest of the prefill: every convolution of it runs on libsvla
+        # (zoe_fast), no vendor library creates handles lazily under the capture
         prefill = {"ids": ids, "pv": pv, "intr": intr, "cls": cls, "kinv": kinv}
-        if graphs and pv is not None and self.config.use_vision_zoe:
-            # the frozen Zoe forward runs eagerly, ahead of the prefill graph: its DPT neck is still MIOpen
-            # convolutions, whose B=1 solvers create vendor-library handles lazily -- not capturable
-            dt = self.multi_modal_projector.linear.weight.dtype
-            prefill["depth"] = self.predict_depth(pv.to(dt))
         first = self._prefill_graph(st, prefill) if graphs else self._prefill_body(st, prefill)
         cache.seen_tokens = P
         # the per-token update runs on the device (_greedy_bookkeep); the host reads the finished flags only every

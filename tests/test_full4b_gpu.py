@@ -254,6 +254,7 @@ def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
     finally:
         model4b.enable_fp8_projections(False)
         model4b.zero_grad(set_to_none=True)
+        model4b.__dict__.pop("predict_depth", None)  # run_hip's golden-depth override
     st = _stats(logits, grads, gold, model4b.config)
     del logits
     _dump("full4b_fp8.json", {"loss": {"hip_fp8": float(loss), "reference": float(gold["out.loss"][0])}, "hip_fp8": st})
@@ -269,8 +270,12 @@ def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
     assert max(st["gradnorm"].values()) < FP8_TOL["gradnorm"], worst
 
 
-# configs[4] tolerances vs the reference's bf16 (provisional, set from the first measurement)
-FP8_TOL = {"loss": 0.1, "logits": 0.15, "lse": 0.2, "agree_025": 0.9, "gradnorm": 0.25}
+# configs[4] tolerances vs the reference's bf16: e4m3 keeps 3 mantissa bits (relative step 2^-3 at the top of a
+# binade, ~3.6e-2 rms error per row-scaled GEMM product), four quantised projections per layer over 26 layers.
+# Measured r3: loss 13.0387 vs 13.0677 (2.9e-2), action logits rel-L2 0.138, 256-column logits 0.129, lse 2.1e-3,
+# argmax agreement 0.95 on rows with a reference margin > 0.25, worst gradient norm 6.2e-2 (SigLIP layer norms:
+# the fp8 error of the Gemma2 input-gradient GEMMs reaches them through the projector).
+FP8_TOL = {"loss": 0.05, "logits": 0.15, "lse": 1e-2, "agree_025": 0.9, "gradnorm": 0.1}
 
 
 @pytest.mark.timeout(900)
