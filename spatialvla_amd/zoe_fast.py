@@ -289,11 +289,38 @@ def _is_exact_gelu(m) -> bool:
     return name == "GELUActivation" and getattr(m, "act", None) in (torch.nn.functional.gelu,)
 
 
+def _no_padding_mask(orig):
+    """transformers' create_bidirectional_mask as bound in modeling_beit: with no padding mask given the BEiT
+    encoder attends everywhere, which eager mode expresses as `None`.  Under a HIP graph capture transformers
+    cannot inspect the mask (masking_utils.is_tracing) and materialises an all-visible [B, 1, L, L] additive mask
+    instead, which would send every BeitLayer down the stock (hipBLASLt, uncapturable) path.  Returning None for a
+    None padding mask is the same attention in both modes."""
+    def create_bidirectional_mask(config, inputs_embeds, attention_mask=None, *args, **kwargs):
+        if attention_mask is None and not args and not kwargs.get("or_mask_function") \
+                and not kwargs.get("and_mask_function"):
+            return None
+        return orig(config, inputs_embeds, attention_mask, *args, **kwargs)
+    create_bidirectional_mask._svla_orig = orig
+    return create_bidirectional_mask
+
+
+def _patch_beit_mask():
+    try:
+        from transformers.models.beit import modeling_beit as mb
+    except ImportError:
+        return
+    f = getattr(mb, "create_bidirectional_mask", None)
+    if f is not None and not hasattr(f, "_svla_orig"):
+        mb.create_bidirectional_mask = _no_padding_mask(f)
+
+
 def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout: bool = True,
             convs: bool = True) -> torch.nn.Module:
     """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False / readout=False / convs=False keep
     the stock metric-head tail / BEiT layers / readout projections / convolutions (the other paths are bitwise
     identical to the stock modules)."""
+    if beit:
+        _patch_beit_mask()
     for m in zoe.modules():
         name = type(m).__name__
         if name == "ZoeDepthReassembleStage" and readout and hasattr(m, "readout_projects"):

@@ -314,3 +314,23 @@ def test_softcap_reciprocal_multiply_exact_on_bf16():
     exact at bf16 for every finite bf16 input at caps 30 and 50 (exhaustive)."""
     import runpy
     runpy.run_path(os.path.join(REPO, "tools", "check_softcap_recip.py"))
+
+
+def test_beit_mask_none_under_graph_capture(monkeypatch):
+    """zoe_fast makes the BEiT encoder's no-padding mask `None` in every mode: transformers materialises an
+    all-visible additive mask while a HIP graph is capturing (masking_utils.is_tracing), which would route every
+    BeitLayer of the captured prefill to the stock path."""
+    from transformers import BeitConfig
+    from transformers.models.beit import modeling_beit as mb
+    from spatialvla_amd import zoe_fast
+    zoe_fast._patch_beit_mask()
+    cfg = BeitConfig(hidden_size=32, num_hidden_layers=1, num_attention_heads=2, intermediate_size=64)
+    cfg._attn_implementation = "eager"  # as the estimator runs (its BeitLayer adds the mask to the scores)
+    emb = torch.zeros(2, 5, 32)
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+    assert mb.create_bidirectional_mask._svla_orig(config=cfg, inputs_embeds=emb, attention_mask=None) is not None
+    assert mb.create_bidirectional_mask(config=cfg, inputs_embeds=emb, attention_mask=None) is None
+    pad = torch.ones(2, 5, dtype=torch.long)
+    pad[1, 3:] = 0
+    m = mb.create_bidirectional_mask(config=cfg, inputs_embeds=emb, attention_mask=pad)
+    assert m is not None
