@@ -1,5 +1,6 @@
 """Per-kernel parity of libsvla against plain PyTorch fp32 references of the same op (GPU)."""
 import math
+import os
 
 import pytest
 import torch
@@ -531,6 +532,52 @@ def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
     assert rel_l2(dqkv[:, :Hq * D].view(B, L, Hq, D), qr.grad) < 2e-2
     assert rel_l2(dqkv[:, Hq * D:(Hq + Hkv) * D].view(B, L, Hkv, D), kr.grad) < 2e-2
     assert rel_l2(dqkv[:, (Hq + Hkv) * D:].view(B, L, Hkv, D), vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("L,window,attn32", [(140, 0, None), (312, 100, None), (140, 0, "1"), (140, 48, "1"),
+                                             (312, 100, "1"), (97, 0, "1")])
+def test_attention_d256_forward_window_and_classes(cuda, L, window, attn32):
+    """head_dim-256 forward (the default 16x16x32 kernel in process; the 32x32x16 one with SVLA_ATTN32=1 in a
+    subprocess, the mode is read once per process): sliding window, prefix / causal / never-visible key classes,
+    a ragged last tile, and the lse it returns (log of the softcapped exp-sum) against fp32."""
+    import subprocess
+    import sys
+    if attn32 is not None:
+        code = (f"import sys; sys.path.insert(0, 'tests'); import os; os.environ['SVLA_ATTN32']='{attn32}'; "
+                f"import test_kernels_gpu as T, torch; T._d256_fwd_check(torch.device('cuda:0'), {L}, {window})")
+        r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.dirname(__file__)),
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return
+    _d256_fwd_check(cuda, L, window)
+
+
+def _d256_fwd_check(cuda, L, window):
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(12)
+    B, Hq, Hkv, D, cap, scale = 2, 4, 2, 256, 50.0, 1 / 16
+    qkv = _r(B * L, (Hq + 2 * Hkv) * D, scale=2.0)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    cls = torch.zeros(B, L, dtype=torch.uint8, device=cuda)
+    cls[:, L // 2:] = 1
+    cls[0, 5:9] = 2
+    cls[1, L - 4:] = 2
+    a = Kn.attn_args(B, L, Hq, Hkv, D, q, qkv.stride(0), k, qkv.stride(0), v, qkv.stride(0), scale, cap, cls, window)
+    out = torch.empty(B * L, Hq * D, dtype=BF, device=cuda)
+    lse = torch.empty(B, Hq, L, device=cuda)
+    Kn.attn_fwd(a, out, lse)
+    torch.cuda.synchronize()
+    ref = _ref_attn(q.view(B, L, Hq, D), k.view(B, L, Hkv, D), v.view(B, L, Hkv, D), scale, cap, cls, window)
+    assert rel_l2(out.view(B, L, Hq, D), ref) < 1e-2
+    qf, kf = q.view(B, L, Hq, D).float().transpose(1, 2), k.view(B, L, Hkv, D).float().transpose(1, 2)
+    s_ = cap * torch.tanh(qf @ kf.repeat_interleave(Hq // Hkv, 1).transpose(-1, -2) * scale / cap)
+    i, j = torch.arange(L, device=cuda)[:, None], torch.arange(L, device=cuda)[None, :]
+    c = cls[:, None, None, :].long()
+    vis = (c == 0) | ((c == 1) & (j <= i))
+    if window:
+        vis = vis & ((i - j) < window)
+    lse_ref = torch.logsumexp(torch.where(vis, s_, torch.tensor(-1e30, device=cuda)), -1)
+    assert (lse - lse_ref).abs().max() < 2e-2
 
 
 def _rope_bf16(x, cos, sin):

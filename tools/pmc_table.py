@@ -14,11 +14,11 @@ def main():
     for d in sys.argv[1:]:
         for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
             for r in csv.DictReader(open(f)):
-                k = r["Kernel_Name"].split("(")[0][:70]
+                k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for f in glob.glob(os.path.join(d, "*kernel_stats.csv")):
             for r in csv.DictReader(open(f)):
-                durs[r["Name"].split("(")[0][:70]] = float(r["AverageNs"]) / 1e3
+                durs[r["Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]] = float(r["AverageNs"]) / 1e3
     for k in sorted(set(vals) | set(durs)):
         print(k, f"avg {durs[k]:.1f} us" if k in durs else "")
         for c, v in sorted(vals[k].items()):
