@@ -817,11 +817,38 @@ __global__ __launch_bounds__(256, 1) void attn_fwd32_kernel(svla_attn_args a, bf
 
   // p = exp(softcapped score) of score e of a half, unmasked; register e holds key
   // k0 + 32 kb + (e & 3) + 8 (e >> 2) + 4 hh
-  auto score = [&](float sv) {
-    float lg;
-    if constexpr (CAP) lg = ce.lg2p(ce.r(sv));
-    else lg = sv * (a.scale * 1.4426950408889634f);
-    return __builtin_amdgcn_exp2f(lg);
+  // The score -> p chain (CAP: exp2, add, rcp, fma, exp2) is three dependent transcendentals long: run one chain
+  // per MFMA gap and the in-order wave stalls the matrix pipe for its whole latency (phase stamps: the two softmax
+  // phases took 3-4x their MFMA time).  So the 16 chains of a half are skewed over the gaps: gap g runs stage 1 of
+  // score g, stage 2 of score g-2 and stage 3 of score g-4 (one transcendental each), four gaps of drain after.
+  struct SmState {
+    float t[16];
+  };
+  // pin(): an empty volatile asm on the value -- volatile asm keeps its order against the asm MFMAs, so a stage's
+  // inputs pinned at its start and outputs pinned at its end hold its instructions inside its own gap
+  auto pin = [](float& x) { asm volatile("" : "+v"(x)); };
+  auto sm_stage = [&](int g, float* sv, SmState& st, float* p) {
+    if constexpr (CAP) {
+      if (g < 16) pin(sv[g]);
+      if (g >= 2 && g - 2 < 16) pin(st.t[g - 2]);
+      if (g >= 4 && g - 4 < 16) pin(st.t[g - 4]);
+      if (g < 16) st.t[g] = __builtin_amdgcn_exp2f(sv[g] * ce.c2);
+      if (g >= 2 && g - 2 < 16) st.t[g - 2] = __builtin_amdgcn_rcpf(1.f + st.t[g - 2]);
+      if (g >= 4 && g - 4 < 16) p[g - 4] = __builtin_amdgcn_exp2f(ce.lg2p(st.t[g - 4]));
+      if (g < 16) pin(st.t[g]);
+      if (g >= 2 && g - 2 < 16) pin(st.t[g - 2]);
+      if (g >= 4 && g - 4 < 16) pin(p[g - 4]);
+    } else {
+      if (g < 16) {
+        pin(sv[g]);
+        p[g] = __builtin_amdgcn_exp2f(sv[g] * (a.scale * 1.4426950408889634f));
+        pin(p[g]);
+      }
+    }
+  };
+  auto sm_drain = [&](float* sv, SmState& st, float* p) {
+#pragma unroll
+    for (int g = 16; g < 20; ++g) sm_stage(g, sv, st, p);
   };
   // the mask of a tile that is not plain, applied to the 16 p of a half after the fact (p = 2^-120 for a hidden
   // key, 0 past L): the branch around it holds only these 16 values, so the O^T accumulators never become
@@ -918,8 +945,10 @@ __global__ __launch_bounds__(256, 1) void attn_fwd32_kernel(svla_attn_args a, bf
     __builtin_amdgcn_sched_barrier(0);
     A32_T(tb);
     float p[16], sv[16];
+    SmState sms;
     s_read(Z{}, sv);
-    qk(ldsK, O{}, [&](int e) { p[e] = score(sv[e]); });
+    qk(ldsK, O{}, [&](int e) { sm_stage(e, sv, sms, p); });
+    sm_drain(sv, sms, p);
     if (!plain) mask_fix(p, k0, 0);
     auto finish = [&](bf16x8* pf) {
       float l0 = 0.f, l1 = 0.f;
@@ -936,8 +965,11 @@ __global__ __launch_bounds__(256, 1) void attn_fwd32_kernel(svla_attn_args a, bf
     finish(pf0);
     __builtin_amdgcn_sched_barrier(0);
     A32_T(tc);
-    s_read(O{}, sv);
-    pv_half(ldsV, 0, pf0, [&](int e) { p[e] = score(sv[e]); });
+    pv_half(ldsV, 0, pf0, [&](int e) {
+      if (e == 0) s_read(O{}, sv);  // behind PV(0)'s first MFMA: the wait states overlap the matrix pipe
+      sm_stage(e, sv, sms, p);
+    });
+    sm_drain(sv, sms, p);
     if (!plain) mask_fix(p, k0, 1);
     finish(pf1);
     __builtin_amdgcn_sched_barrier(0);

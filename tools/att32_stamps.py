@@ -7,6 +7,8 @@ import sys
 
 import numpy as np
 
+os.environ["SVLA_ATTN32"] = "1"  # the 32x32x16 forward is opt-in
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 from spatialvla_amd import kernels as K, _lib as L  # noqa: E402
