@@ -117,7 +117,8 @@ def dominant_kernel_roofline(records, fp8=False):
     bytes_alg = ob * (M * K + N * K) + 2.0 * 3 * M * (N // 2)   # x, Wg, Wu read; h, g, u written (bf16)
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
     kern = ("svla gemm4f8_kernel (256x256 tile, 4 waves x 128x128, v_mfma_scale_f32_32x32x64_f8f6f4 e4m3, row scales)"
-            if fp8 else "svla gemm4_kernel_00 (256x256 tile, 4 waves x 128x128, AGPR accumulators)")
+            if fp8 else "svla gemm4_kernel_00g (256x256 tile, 4 waves x 128x128, AGPR C^T accumulators, gate/up B "
+                        "fragments paired per output block, GeGLU stored straight from the accumulators)")
     return {"kernel": kern + " EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
             "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "traffic": None if fp8 else pmc_traffic(), "avg_launch_ms": round(avg, 4),

@@ -246,6 +246,8 @@ int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* 
                           float eps1, float eps2, void* h, void* x, void* stream);
 int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
                        void* y, float* mean, float* rstd, void* stream);
+/* dwb_partial: two planes [2][ceil(rows/rows_per_block)][N] fp32 (dw partials, then db partials), each reduced by
+ * svla_colsum_f32. */
 int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* mean,
                        const float* rstd, const void* dy, const void* dres, void* dx, float* dwb_partial,
                        int64_t* n_partial, void* stream);

@@ -189,9 +189,19 @@ struct CDesc {
   int64_t ld;
 };
 
+#ifndef G_EPI_STORE
+#define G_EPI_STORE 0  // diagnostic builds: 1 = no output store (timing ablation, wrong results), 2 = nontemporal stores
+#endif
 __device__ __forceinline__ void store8(bf16_t* p, const float* v, int64_t n_valid) {
   if (n_valid >= 8) {
-    *reinterpret_cast<u32x4*>(p) = pack8(v);
+    if constexpr (G_EPI_STORE == 1) {
+      const u32x4 x = pack8(v);
+      asm volatile("" ::"v"(x));
+    } else if constexpr (G_EPI_STORE == 2) {
+      __builtin_nontemporal_store(pack8(v), reinterpret_cast<u32x4*>(p));
+    } else {
+      *reinterpret_cast<u32x4*>(p) = pack8(v);
+    }
   } else {
     for (int j = 0; j < n_valid; ++j) p[j] = f2bf(v[j]);
   }
@@ -1524,7 +1534,7 @@ static_assert(F8_RB1 >= 8 && F8_DA0 > F8_RB1 && F8_DB0 >= F8_DA0 + 4 && F8_RB2 >
 // The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
 // template are also instantiated for the host, where the device-only helpers they call fail to substitute and
 // the kernel stub silently disappears.
-template <int LA, int LB, bool F8 = false>
+template <int LA, int LB, bool F8 = false, bool GG = false>
 __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
                                            const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
                                            const SKArgs& sk, const F8Scales& fs) {
@@ -1680,10 +1690,17 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     } else {
     Frag<LA> f0a[8], f1a[8];
     Frag<LB> f0b[8], f1b[8];
+    // B fragment j of the wave: rows 128 wc + 16 j of the B image; GG (GeGLU): the gate block j/2 (j even) or the up
+    // block j/2 (j odd) of the wave's 64 output columns, so a lane's quads (i, 2p) and (i, 2p+1) hold the gate and the
+    // up value of the same outputs
+    auto loadB = [&](Frag<LB>& f, const char* img, int j, int ks) {
+      if constexpr (GG) f.load(img, (j & 1) * 128 + 64 * wc + 16 * (j >> 1), ks, lane);
+      else frag4_load<LB>(f, img, 128 * wc, j, ks, lane);
+    };
 #pragma unroll
     for (int i = 0; i < 8; ++i) frag4_load<LA>(f0a[i], smem, 128 * wr, i, 0, lane);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) frag4_load<LB>(f0b[j], smem + OPB, 128 * wc, j, 0, lane);
+    for (int j = 0; j < 8; ++j) loadB(f0b[j], smem + OPB, j, 0);
 
     // one k-tile; DMA: stage k-tile kt+2 into this buffer; NEXT: k-tile kt+1 exists (wait for it, read its F0).
     // RC fragments come from asm transpose reads (hipcc would drain every LDS-DMA before a builtin one), which
@@ -1707,12 +1724,13 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       static_for<0, 128>([&](auto XC) {
         constexpr int x = decltype(XC)::value;
         constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
-        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0a[ii].get(), f0b[jj].get());
-        else agpr_mfma<ii * 8 + jj>(f1a[ii].get(), f1b[jj].get());
+        // swapped operands: quad (ii, jj) accumulates C^T, so a lane holds 4 consecutive columns of one row
+        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0b[jj].get(), f0a[ii].get());
+        else agpr_mfma<ii * 8 + jj>(f1b[jj].get(), f1a[ii].get());
         if constexpr (G4_ABL & 2) {
         } else if constexpr (x % G4_RS == 0 && x / G4_RS < 8) frag4_load<LA>(f1a[x / G4_RS], cur, 128 * wr, x / G4_RS, 1, lane);
         else if constexpr (x % G4_RS == 0 && x / G4_RS < 16)
-          frag4_load<LB>(f1b[x / G4_RS - 8], cur + OPB, 128 * wc, x / G4_RS - 8, 1, lane);
+          loadB(f1b[x / G4_RS - 8], cur + OPB, x / G4_RS - 8, 1);
         if constexpr (x == G4_RB1) {
 #if G4_STAMPS
           unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -1749,7 +1767,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           constexpr int r0 = x - G4_RB2 - 1;
           constexpr int r = (r0 >= 0 && r0 % G4_RS == 0 && !(G4_ABL & 2)) ? r0 / G4_RS : -1;
           if constexpr (r >= 0 && r < 8) frag4_load<LA>(f0a[r], nxt, 128 * wr, r, 0, lane);
-          else if constexpr (r >= 8 && r < 16) frag4_load<LB>(f0b[r - 8], nxt + OPB, 128 * wc, r - 8, 0, lane);
+          else if constexpr (r >= 8 && r < 16) loadB(f0b[r - 8], nxt + OPB, r - 8, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1762,25 +1780,219 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     __syncthreads();
   };
 
+  // Direct epilogue (bf16 path, whole interior tiles).  The MFMAs accumulate C^T, so the quad (i, j) gives lane l 4
+  // consecutive columns of one row; v_permlane16_swap of quads (i, j) and (i, j + 1) (16-lane halves: lanes 16-31 of
+  // the first with lanes 0-15 of the second, 48-63 with 32-47) leaves each lane 8 consecutive columns, so every output
+  // row chunk goes out as one 16-B store straight from the accumulators: no LDS image and no barrier (the LDS path
+  // spent ~27k cycles per 256x256 tile, 22 % of a K = 2304 tile; tools/gemm_stamps.py).  After the swap lane g = l >> 4
+  // holds columns 16 (j + (g & 1)) + 8 (g >> 1) .. +7.  STORE (alpha, accumulate) and GEGLU; every other kind, edge
+  // tiles and fp8 take the LDS path.
+  auto swap4 = [](f32x4& a, f32x4& b) {  // whole-vector bit casts, constant element indices
+    // a and b come from v_accvgpr_read inside inline asm, which the hazard recognizer does not see: the 2 wait states
+    // a VALU write owes a following v_permlane read (cdna_hip_programming.md T21) are padded here
+    asm volatile("s_nop 1" ::"v"(a), "v"(b));
+    const u32x4 ua = __builtin_bit_cast(u32x4, a), ub = __builtin_bit_cast(u32x4, b);
+    const auto r0 = __builtin_amdgcn_permlane16_swap(ua[0], ub[0], false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(ua[1], ub[1], false, false);
+    const auto r2 = __builtin_amdgcn_permlane16_swap(ua[2], ub[2], false, false);
+    const auto r3 = __builtin_amdgcn_permlane16_swap(ua[3], ub[3], false, false);
+    a = __builtin_bit_cast(f32x4, u32x4{(uint32_t)r0[0], (uint32_t)r1[0], (uint32_t)r2[0], (uint32_t)r3[0]});
+    b = __builtin_bit_cast(f32x4, u32x4{(uint32_t)r0[1], (uint32_t)r1[1], (uint32_t)r2[1], (uint32_t)r3[1]});
+  };
+  auto direct_epilogue = [&](int64_t m0, int64_t n0, int lane) -> bool {
+    const int kind = E.kind;
+    if (!(kind == SVLA_EPI_STORE || (GG && kind == SVLA_EPI_GEGLU))) return false;
+    if (m0 + BM > M || n0 + BN > N) return false;
+    int cs = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (i < Cd.n && m0 >= Cd.start[i]) cs = i;
+    bf16_t* const cbase = Cd.ptr[cs];
+    const int64_t cm0 = Cd.start[cs];
+    const int g = lane >> 4, r = lane & 15;
+    const int cofs = 16 * (g & 1) + 8 * (g >> 1);
+    if (kind == SVLA_EPI_SOFTCAP_CE) {  // the bf16 tanh table to LDS (the staging buffers are free)
+      if ((int)threadIdx.x < TANH_TAB_BYTES / 16)
+        *(LDS_AS u32x4*)(smem + 16 * threadIdx.x) = reinterpret_cast<const u32x4*>(svla_tanh_bf16_tab)[threadIdx.x];
+      lds_barrier();
+    }
+    if constexpr (GG) {
+      const int64_t ncol = (n0 >> 1) + 64 * wc + cofs;
+      static_for<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const int64_t m = m0 + 128 * wr + 16 * i + r;
+        static_for<0, 2>([&](auto P) {
+          constexpr int P_ = decltype(P)::value;
+          f32x4 ga = agpr_get<i * 8 + 4 * P_>(), ua = agpr_get<i * 8 + 4 * P_ + 1>();
+          f32x4 gb = agpr_get<i * 8 + 4 * P_ + 2>(), ub = agpr_get<i * 8 + 4 * P_ + 3>();
+          swap4(ga, gb);
+          swap4(ua, ub);
+          float gv[8], uv[8], hv[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            gv[q] = round_bf(ga[q]);
+            gv[4 + q] = round_bf(gb[q]);
+            uv[q] = round_bf(ua[q]);
+            uv[4 + q] = round_bf(ub[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) hv[q] = round_bf(gelu_tanh(gv[q])) * uv[q];
+          const int64_t n = ncol + 32 * P_;
+          *reinterpret_cast<u32x4*>(cbase + (m - cm0) * Cd.ld + n) = pack8(hv);
+          *reinterpret_cast<u32x4*>((bf16_t*)E.out1 + m * E.ld_out1 + n) = pack8(gv);
+          *reinterpret_cast<u32x4*>((bf16_t*)E.out2 + m * E.ld_out2 + n) = pack8(uv);
+        });
+      });
+    } else {
+      // one row chunk: v = 8 consecutive fp32 columns n .. n+7 of row m (reference rounding points of epi_pass_fast)
+      const float alpha = E.alpha;
+      const bool acc = E.accumulate != 0;
+      const int64_t nb = n0 + 128 * wc + cofs;  // column of chunk p: nb + 32 p
+      auto run = [&](auto KC) {
+        constexpr int KIND = decltype(KC)::value;
+        constexpr bool HAS_B = KIND == SVLA_EPI_BIAS || KIND == SVLA_EPI_BIAS_GELU || KIND == SVLA_EPI_BIAS_RESID ||
+                               KIND == SVLA_EPI_BIAS_GELU_ERF || KIND == SVLA_EPI_BIAS_SCALE_RESID;
+        constexpr bool HAS_IN0 = KIND == SVLA_EPI_BIAS_RESID || KIND == SVLA_EPI_BIAS_SCALE_RESID ||
+                                 KIND == SVLA_EPI_GELU_BWD;
+        u32x4 bq[4], sq[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          bq[p] = sq[p] = u32x4{0u, 0u, 0u, 0u};
+          if (HAS_B && E.bias) bq[p] = *reinterpret_cast<const u32x4*>((const bf16_t*)E.bias + nb + 32 * p);
+          if (KIND == SVLA_EPI_BIAS_SCALE_RESID) sq[p] = *reinterpret_cast<const u32x4*>((const bf16_t*)E.colscale + nb + 32 * p);
+        }
+        const LDS_AS unsigned short* ltab = (const LDS_AS unsigned short*)smem;
+        const float cap = E.cap, icap = 1.0f / E.cap;
+        static_for<0, 8>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          const int64_t m = m0 + 128 * wr + 16 * i + r;
+          bf16_t* const rowp = cbase + (m - cm0) * Cd.ld + nb;
+          u32x4 old[4];
+          if (HAS_IN0 || (KIND == SVLA_EPI_STORE && acc)) {  // the row block's four chunks in flight at once
+            const bf16_t* src = HAS_IN0 ? (const bf16_t*)E.in0 + m * E.ld_in0 + nb : rowp;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) old[p] = *reinterpret_cast<const u32x4*>(src + 32 * p);
+          }
+          float mx = -INFINITY, se = 0.f, mold = -INFINITY;
+          int am = 0x7fffffff;
+          static_for<0, 4>([&](auto P) {
+            constexpr int p = decltype(P)::value;
+            f32x4 a = agpr_get<i * 8 + 2 * p>(), b = agpr_get<i * 8 + 2 * p + 1>();
+            swap4(a, b);
+            float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+            float bb[8], o[8];
+            if constexpr (HAS_B) unpack8(bq[p], bb);
+            if constexpr (HAS_IN0) unpack8(old[p], o);
+            if constexpr (KIND == SVLA_EPI_STORE) {
+              if (acc) {
+                unpack8(old[p], o);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = alpha * v[q] + o[q];
+              } else if (alpha != 1.f) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] *= alpha;
+              }
+            } else if constexpr (KIND == SVLA_EPI_BIAS) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] = round_bf(v[q] + bb[q]) * alpha;
+            } else if constexpr (KIND == SVLA_EPI_BIAS_GELU) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                bb[q] = round_bf(v[q] + bb[q]);  // pre-activation, saved for backward
+                v[q] = gelu_tanh(bb[q]);
+              }
+              *reinterpret_cast<u32x4*>((bf16_t*)E.out1 + m * E.ld_out1 + nb + 32 * p) = pack8(bb);
+            } else if constexpr (KIND == SVLA_EPI_BIAS_RESID) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] = round_bf(v[q] + bb[q]) + o[q];
+            } else if constexpr (KIND == SVLA_EPI_BIAS_GELU_ERF) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] = gelu_erf(round_bf(v[q] + bb[q]));
+            } else if constexpr (KIND == SVLA_EPI_BIAS_SCALE_RESID) {
+              float sc[8];
+              unpack8(sq[p], sc);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] = round_bf(sc[q] * round_bf(v[q] + bb[q])) + o[q];
+            } else if constexpr (KIND == SVLA_EPI_GELU_BWD) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) v[q] = round_bf(v[q]) * gelu_tanh_grad(o[q]);
+            } else if constexpr (KIND == SVLA_EPI_SOFTCAP_CE) {
+              // columns in increasing order across p: a strict > keeps the lowest index at the maximum
+              mold = mx;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                v[q] = softcap_bf16_tab(v[q], cap, icap, ltab);
+                if (v[q] > mx) { mx = v[q]; am = (int)(nb + 32 * p + q); }
+              }
+            }
+            *reinterpret_cast<u32x4*>(rowp + 32 * p) = pack8(v);
+            if constexpr (KIND == SVLA_EPI_SOFTCAP_CE) {
+              // online sum of exp against the lane's running max (the previous sum rescaled when the max grew)
+              float s8 = 0.f;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) s8 += __expf(v[q] - mx);
+              se = (mold == -INFINITY) ? s8 : se * __expf(mold - mx) + s8;
+            }
+          });
+          if constexpr (KIND == SVLA_EPI_SOFTCAP_CE) {
+            // the 128-column group of the row is this wave's half tile: lanes r, r+16, r+32, r+48
+            float gm = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            gm = fmaxf(gm, __shfl_xor(gm, 32, 64));
+            float sg = (mx == -INFINITY) ? 0.f : se * __expf(mx - gm);
+            int ag = (mx == gm) ? am : 0x7fffffff;
+            sg += __shfl_xor(sg, 16, 64);
+            ag = min(ag, __shfl_xor(ag, 16, 64));
+            sg += __shfl_xor(sg, 32, 64);
+            ag = min(ag, __shfl_xor(ag, 32, 64));
+            if (g == 0) {
+              const int64_t ntn = (N + 127) / 128;
+              float* rs = E.row_stats + (m * ntn + (n0 + 128 * wc) / 128) * 3;
+              rs[0] = gm;
+              rs[1] = sg;
+              rs[2] = __int_as_float(ag);
+            }
+          }
+        });
+      };
+      switch (kind) {
+        case SVLA_EPI_STORE: run(std::integral_constant<int, SVLA_EPI_STORE>{}); break;
+        case SVLA_EPI_BIAS: run(std::integral_constant<int, SVLA_EPI_BIAS>{}); break;
+        case SVLA_EPI_BIAS_GELU: run(std::integral_constant<int, SVLA_EPI_BIAS_GELU>{}); break;
+        case SVLA_EPI_BIAS_RESID: run(std::integral_constant<int, SVLA_EPI_BIAS_RESID>{}); break;
+        case SVLA_EPI_BIAS_GELU_ERF: run(std::integral_constant<int, SVLA_EPI_BIAS_GELU_ERF>{}); break;
+        case SVLA_EPI_BIAS_SCALE_RESID: run(std::integral_constant<int, SVLA_EPI_BIAS_SCALE_RESID>{}); break;
+        case SVLA_EPI_GELU_BWD: run(std::integral_constant<int, SVLA_EPI_GELU_BWD>{}); break;
+        case SVLA_EPI_SOFTCAP_CE: run(std::integral_constant<int, SVLA_EPI_SOFTCAP_CE>{}); break;
+        default: return false;
+      }
+    }
+    return true;
+  };
+
   auto epilogue = [&](int64_t m0, int64_t n0, const int t) {
     const int lane = t & 63;
+    // tile column of B fragment j of the wave (GG: gate columns [0, 128), up columns [128, 256) of the image)
+    auto colb = [&](int j) { return GG ? (j & 1) * 128 + 64 * wc + 16 * (j >> 1) : 128 * wc + 16 * j; };
     auto wp = [&](int pass, float* Ei) {
-      // pass p holds rows [64p, 64p+64): wave row wr = p >> 1, fragments 4(p&1)..4(p&1)+3
+      // pass p holds rows [64p, 64p+64): wave row wr = p >> 1, fragments 4(p&1)..4(p&1)+3.  Quad (i, j) (C^T
+      // accumulation): lane l holds row 16 i + (l & 15), columns colb(j) + 4 (l >> 4) .. +3 -> one 16-B LDS store
       if ((pass >> 1) == wr) {
         auto rows = [&](auto H) {
           static_for<0, 32>([&](auto IJ) {
             constexpr int i = decltype(IJ)::value >> 3, j = decltype(IJ)::value & 7;
             const f32x4 v = agpr_get<(4 * decltype(H)::value + i) * 8 + j>();
-            const int col = 128 * wc + 16 * j + (lane & 15);
-            const int r = 16 * i + 4 * (lane >> 4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Ei[(r + q) * (BN + 4) + col] = v[q];
+            const int col = colb(j) + 4 * (lane >> 4);
+            const int r = 16 * i + (lane & 15);
+            *reinterpret_cast<f32x4*>(Ei + r * (BN + 4) + col) = v;
           });
         };
         if (pass & 1) rows(std::integral_constant<int, 1>{});
         else rows(std::integral_constant<int, 0>{});
       }
     };
+    if constexpr (!F8) {
+      if (direct_epilogue(m0, n0, lane)) return;
+    }
     // fp8: 32x32 blocks (block q = 4i + j in a[16q:16q+15]; register r of a block: row (r&3) + 8(r>>2) + 4(l>>5),
     // column l&31), scaled by the row scales of A and B on the way into the image
     auto wp8 = [&](int pass, float* Ei) {
@@ -1942,6 +2154,11 @@ SVLA_GEMM4_KERNEL(0, 1)
 SVLA_GEMM4_KERNEL(1, 0)
 SVLA_GEMM4_KERNEL(1, 1)
 #undef SVLA_GEMM4_KERNEL
+// Gemma2 gate|up: B fragments paired gate/up per output block, GeGLU straight from the accumulators
+__global__ __launch_bounds__(256, 1) void gemm4_kernel_00g(int64_t M, int64_t N, int64_t K, svla_operand A,
+                                                           svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
+  gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, false, true>(M, N, K, A, B, Cd, E, sk, F8Scales{});
+}
 __global__ __launch_bounds__(256, 1) void gemm4f8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B,
                                                          CDesc Cd, svla_epilogue E, SKArgs sk, F8Scales fs) {
   gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, true>(M, N, K, A, B, Cd, E, sk, fs);
@@ -2484,6 +2701,15 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     return svla::check_launch("gemm4 fp8");
   }
   const int la = A.layout, lb = B.layout;
+  if (E.kind == SVLA_EPI_GEGLU) {  // B is two KC GEGLU segments (checked by the dispatcher)
+    static bool lds_set = false;
+    if (!lds_set) {
+      (void)hipFuncSetAttribute((const void*)gemm4_kernel_00g, hipFuncAttributeMaxDynamicSharedMemorySize, p4::LDS);
+      lds_set = true;
+    }
+    hipLaunchKernelGGL(gemm4_kernel_00g, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);
+    return svla::check_launch("gemm4 geglu");
+  }
   if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(0, 0)
   else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH4(0, 1)
   else if (la == SVLA_LAYOUT_RC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(1, 0)
@@ -2683,12 +2909,16 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   const int64_t t256 = tiles(256, 256);
   // ROPE's fast-path epilogue (cos/sin prefetched a row ahead) runs as well on the 4-wave kernel: q|k|v 233 -> 225 us
   // (tools/gemm_epi_bench.py, bitwise equal)
-  const bool light_epi = epi->kind == SVLA_EPI_STORE || epi->kind == SVLA_EPI_BIAS || epi->kind == SVLA_EPI_GEGLU ||
-                         epi->kind == SVLA_EPI_ROPE;
+  // The 4-wave kernel's direct epilogue (stores straight from the accumulators, gemm4_body) made it the faster kernel
+  // for the light epilogues from one k-tile loop of 512 up and from a quarter wave of tiles (tools/gemm_bench.py:
+  // o fwd 129 -> 106 us, down dgrad 422 -> 354 us, SigLIP qkv BIAS 89 -> 82 us; ROPE keeps its LDS epilogue there,
+  // bitwise the 8-phase kernel's, 0.99x).  VALU-heavy or load-carrying epilogues stay on the 8-phase kernel, whose
+  // two waves per SIMD run them faster than one wave does from registers (tools/epi_ab.py, tools/gemm_epi_bench.py:
+  // SOFTCAP_CE 13.4 vs 16.4 ms, BIAS_GELU_ERF 270 vs 312 us, GELU_BWD 178 vs 224 us, BIAS_RESID 127 vs 138 us).
+  const int ek = epi->kind;
+  const bool light_epi = ek == SVLA_EPI_STORE || ek == SVLA_EPI_BIAS || ek == SVLA_EPI_GEGLU || ek == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 2048 && t256 >= num_cus() &&
-                                        (t256 >= 512 || K >= 4096) &&
-                                        (B->layout == SVLA_LAYOUT_KC || K >= 4096)));  // short-K x RC B: +4%
+                    (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 512 && 4 * t256 >= num_cus()));
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
     if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(int64_t rows, int64_
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc += sred[(q * nv + v) * N + k];
-    partial[((int64_t)blockIdx.x * nv + v) * N + k] = acc;
+    partial[((int64_t)v * gridDim.x + blockIdx.x) * N + k] = acc;  // plane v (LN: dw, db) of [nv][blocks][N]
   }
 }
 
@@ -482,11 +482,12 @@ __global__ __launch_bounds__(NTH) void ln_bwd_kernel(int64_t rows, int64_t N, co
   for (int c = 0; c < MAXC; ++c) {
     int ch = threadIdx.x + c * NTH;
     if (ch < nch) {
-      float* p = dwb_partial + (int64_t)blockIdx.x * 2 * N + ch * 8;
-      for (int j = 0; j < 8; ++j) {
-        p[j] = dwacc[c][j];
-        p[N + j] = dbacc[c][j];
-      }
+      float* p = dwb_partial + (int64_t)blockIdx.x * N + ch * 8;  // planes [2][blocks][N]: dw, then db
+      float* pb = p + (int64_t)gridDim.x * N;
+      *reinterpret_cast<f32x4*>(p) = f32x4{dwacc[c][0], dwacc[c][1], dwacc[c][2], dwacc[c][3]};
+      *reinterpret_cast<f32x4*>(p + 4) = f32x4{dwacc[c][4], dwacc[c][5], dwacc[c][6], dwacc[c][7]};
+      *reinterpret_cast<f32x4*>(pb) = f32x4{dbacc[c][0], dbacc[c][1], dbacc[c][2], dbacc[c][3]};
+      *reinterpret_cast<f32x4*>(pb + 4) = f32x4{dbacc[c][4], dbacc[c][5], dbacc[c][6], dbacc[c][7]};
     }
   }
 }

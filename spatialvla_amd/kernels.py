@@ -371,16 +371,16 @@ def layernorm_fwd(x, w, b, eps, y, mean, rstd):
 def layernorm_bwd(x, w, mean, rstd, dy, dres, dx, dw_out, db_out, accumulate=False):
     rows, N = x.shape
     nb = (rows + RPB - 1) // RPB
-    part = torch.empty(nb, 2, N, dtype=torch.float32, device=x.device)
+    part = torch.empty(2, nb, N, dtype=torch.float32, device=x.device)
     npart = ctypes.c_int64(0)
     L.check(L.lib().svla_layernorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                        dy.data_ptr(), _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart),
                                        _stream()), "layernorm_bwd")
-    # partial layout [nb][2][N]: reduce dw (stride 2N) and db separately via contiguous copies
+    # partial planes [2][nb][N]: dw, then db, each reduced in place
     if dw_out is not None:
-        colsum_f32(part[:, 0].contiguous(), dw_out, accumulate)
+        colsum_f32(part[0], dw_out, accumulate)
     if db_out is not None:
-        colsum_f32(part[:, 1].contiguous(), db_out, accumulate)
+        colsum_f32(part[1], db_out, accumulate)
 
 
 def colsum_f32(part, out, accumulate=False):

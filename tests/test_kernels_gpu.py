@@ -257,6 +257,50 @@ def test_gemm_big_tile_epilogues(cuda):
     assert rel_l2(outs[0], dy.float().T @ x2.float()) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 1536, 2304), (1100, 1300, 640), (512, 768, 9984)])
+def test_gemm4_direct_epilogue(cuda, M, N, K):
+    """The 4-wave kernel's direct epilogue (interior tiles: stores straight from the C^T accumulators after
+    v_permlane16_swap) beside its LDS-image epilogue (edge tiles of the ragged shape): STORE with alpha and
+    accumulate, all operand layouts, and the GeGLU kernel, against fp32 references.  M x N multiples of 256 are
+    interior-only; 1100 x 1300 mixes both paths in one launch."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(11)
+    ops = {"nt": (_r(M, K), _r(N, K)), "nn": (_r(M, K), _r(K, N + (-N) % 8)[:, :N]),
+           "tn": (_r(K, M + (-M) % 8)[:, :M], _r(K, N + (-N) % 8)[:, :N])}
+    for lay, (a, b) in ops.items():
+        A = Kn._operand([a], L.LAYOUT_RC if lay == "tn" else L.LAYOUT_KC)
+        B = Kn._operand([b], L.LAYOUT_KC if lay == "nt" else L.LAYOUT_RC)
+        af = a.float().T if lay == "tn" else a.float()
+        bf = b.float().T if lay == "nt" else b.float()
+        ref = af @ bf
+        c = torch.full((M, N + (-N) % 8), 7.0, dtype=BF, device=cuda)
+        Kn.gemm(M, N, K, A, B, [c[:, :N]], [0], c.stride(0), Kn._epi(alpha=0.5), variant=3)
+        assert rel_l2(c[:, :N], 0.5 * ref) < 5e-3, lay
+        assert bool((c[:, N:] == 7.0).all())
+        c0 = c.clone()
+        Kn.gemm(M, N, K, A, B, [c[:, :N]], [0], c.stride(0), Kn._epi(accumulate=True), variant=3)
+        assert rel_l2(c[:, :N], c0[:, :N].float() + ref) < 5e-3, lay
+        c2 = torch.empty(M, N + (-N) % 8, dtype=BF, device=cuda)[:, :N]
+        Kn.gemm(M, N, K, A, B, [c2], [0], c2.stride(0), Kn._epi(), variant=3)
+        c3 = torch.empty(M, N + (-N) % 8, dtype=BF, device=cuda)[:, :N]
+        Kn.gemm(M, N, K, A, B, [c3], [0], c3.stride(0), Kn._epi(), variant=3)
+        assert torch.equal(c2, c3) and rel_l2(c2, ref) < 5e-3, lay
+    I = (N // 2 + 127) // 128 * 128
+    x, wg, wu = _r(M, K), _r(I, K, scale=0.05), _r(I, K, scale=0.05)
+    h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    try:
+        Kn.gemm_variant = 3  # the GeGLU 4-wave kernel at any K
+        Kn.linear_geglu_fwd(x, wg, wu, h, g, u)
+    finally:
+        Kn.gemm_variant = 0
+    gr, ur = x.float() @ wg.float().T, x.float() @ wu.float().T
+    assert rel_l2(g, gr) < 5e-3 and rel_l2(u, ur) < 5e-3
+    # h from the kernel's own bf16 g, u: the epilogue's arithmetic exactly (bf16(gelu_tanh(g)) * u, rounded)
+    hr = (F.gelu(g.float(), approximate="tanh").to(BF).float() * u.float()).to(BF)
+    assert (h.float() - hr.float()).abs().max().item() <= 2 * hr.float().abs().max().item() * 2 ** -8
+    assert rel_l2(h, F.gelu(gr, approximate="tanh") * ur) < 1e-2
+
+
 def test_gemm_epilogues(cuda):
     from spatialvla_amd import kernels as Kn, _lib as L
     torch.manual_seed(1)

@@ -50,5 +50,15 @@ t2 = timeit(lambda: K.gemm(M, V, 2304, K._operand([x], L.LAYOUT_KC), K._operand(
                            K._epi()))
 t3 = timeit(lambda: K.gemm(M, V, 2304, K._operand([x], L.LAYOUT_KC), K._operand([wl], L.LAYOUT_KC), [logits], [0], Vp,
                            K._epi(L.EPI_SOFTCAP_CE, cap=30.0, row_stats=stats)))
+sc = lambda: K.gemm(M, V, 2304, K._operand([x], L.LAYOUT_KC), K._operand([wl], L.LAYOUT_KC), [logits], [0], Vp,  # noqa
+                    K._epi(L.EPI_SOFTCAP_CE, cap=30.0, row_stats=stats))
+ref_l, ref_s = logits.clone(), stats.clone()
+K.gemm_variant = 4  # never the 4-wave kernel: the 8-phase kernel's LDS epilogue
+t4 = timeit(sc)
+l8, s8 = logits.clone(), stats.clone()
+K.gemm_variant = 0
 fl = 2.0 * M * V * 2304
-print(f"lm_head store {t2:.3f} ms ({fl / t2 / 1e9:.0f} TF)   softcap_ce {t3:.3f} ms ({fl / t3 / 1e9:.0f} TF)", flush=True)
+print(f"lm_head store {t2:.3f} ms ({fl / t2 / 1e9:.0f} TF)   softcap_ce {t3:.3f} ms ({fl / t3 / 1e9:.0f} TF)   "
+      f"softcap_ce 8-phase {t4:.3f} ms; logits equal {torch.equal(ref_l[:, :V], l8[:, :V])}, max |dstats| "
+      f"{(ref_s[..., :2] - s8[..., :2]).abs().max().item():.3e}, argmax equal "
+      f"{torch.equal(ref_s[..., 2].view(torch.int32), s8[..., 2].view(torch.int32))}", flush=True)
