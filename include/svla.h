@@ -302,6 +302,11 @@ int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stre
  * action argmax train/monkey_patch.py:267-309).  Logits come from svla_gemm_bf16 with
  * SVLA_EPI_SOFTCAP_CE, which leaves per (row, 128-col tile) {max, sumexp, argmax} in row_stats.
  * ---------------------------------------------------------------------------------------- */
+/* The same softcap and row_stats as SVLA_EPI_SOFTCAP_CE, as a streaming pass over raw bf16 logits [M][ld] (N valid
+ * columns) written by a plain-store GEMM, in place: logits = bf16(cap*tanh(bf16(bf16(y)/cap))) (the reference's bf16
+ * op order, modeling_gemma2.py:993-997), row_stats [M][ceil(N/128)][3] bitwise the epilogue's.  One read and one
+ * write of the logits at HBM rate instead of the VALU-heavy epilogue inside the MFMA loop's tiles. */
+int svla_softcap_ce_rows(int64_t M, int64_t N, void* logits, int64_t ld, float cap, float* row_stats, void* stream);
 /* Reduce row_stats -> lse[m], argmax[m]; loss_rows[m] = lse - logit[m, target[m]] for target >= 0
  * (else 0); loss_out[0] = sum(loss_rows)/max(n_valid,1) where n_valid = #(target >= 0). */
 int svla_ce_finalize(int64_t M, int64_t N, int64_t ntiles, const float* row_stats, const void* logits, int64_t ldl,

@@ -108,6 +108,7 @@ SIGNATURES = {
     "svla_relu_fwd": (c_i32, [c_i64, c_vp, c_vp, c_vp]),
     "svla_relu_bwd": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "svla_add_bf16": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "svla_softcap_ce_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_f32, c_vp, c_vp]),
     "svla_ce_finalize": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "svla_ce_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp]),
     "svla_conv2d_nhwc": (c_i32, [ctypes.POINTER(ConvArgs), c_vp]),

@@ -2938,6 +2938,78 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------------------
+// Softcap + softmax statistics of raw lm_head logits, in place (svla_softcap_ce_rows).  A wave covers 512 columns of
+// a row (8 per lane, 16-B loads/stores), 16 lanes = one 128-column group: per lane {max, first argmax, sum exp} of
+// its 8 values, then the group combine of SOFTCAP_CE's LDS epilogue (same chunk partition, same butterfly), so the
+// statistics are bitwise the fused epilogue's.  Persistent blocks, the bf16 tanh table staged in LDS once per block.
+// ------------------------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void softcap_rows_kernel(int64_t M, int64_t N, bf16_t* __restrict__ lg, int64_t ld,
+                                                           float cap, float* __restrict__ row_stats) {
+  __shared__ __attribute__((aligned(16))) unsigned short tab[TANH_TAB_BYTES / 2];
+  if ((int)threadIdx.x < TANH_TAB_BYTES / 16)
+    reinterpret_cast<u32x4*>(tab)[threadIdx.x] = reinterpret_cast<const u32x4*>(svla_tanh_bf16_tab)[threadIdx.x];
+  __syncthreads();
+  const float icap = 1.0f / cap;
+  const int lane = threadIdx.x & 63;
+  const int64_t cpr = (N + 511) / 512;          // 512-column chunks per row
+  const int64_t ntn = (N + 127) / 128;
+  const int64_t total = M * cpr;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  for (int64_t u = wid; u < total; u += nw) {
+    const int64_t m = u / cpr;
+    const int64_t n = (u - m * cpr) * 512 + 8 * lane;
+    const int64_t nv = N - n;
+    bf16_t* p = lg + m * ld + n;
+    float v[8];
+    float mx = -INFINITY, se = 0.f;
+    int am = 0x7fffffff;
+    if (nv > 0) {
+      load8f(p, v, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = softcap_bf16_tab(v[j], cap, icap, tab);
+        if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < nv) se += __expf(v[j] - mx);
+      if (mx == -INFINITY) se = 0.f;
+      store8(p, v, nv);
+    }
+    float gm = mx;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) gm = fmaxf(gm, __shfl_xor(gm, o, 64));
+    se = (mx == -INFINITY) ? 0.f : se * __expf(mx - gm);
+    am = (mx == gm) ? am : 0x7fffffff;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      se += __shfl_xor(se, o, 64);
+      am = min(am, __shfl_xor(am, o, 64));
+    }
+    if ((lane & 15) == 0 && nv > 0) {
+      float* rs = row_stats + (m * ntn + n / 128) * 3;
+      rs[0] = gm;
+      rs[1] = se;
+      rs[2] = __int_as_float(am);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int svla_softcap_ce_rows(int64_t M, int64_t N, void* logits, int64_t ld, float cap, float* row_stats,
+                                    void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && ld >= N && ld % 8 == 0 && cap > 0.f, "softcap_ce_rows: M, N, ld (multiple of 8 "
+                 ">= N), cap > 0");
+  SVLA_CHECK_ARG(logits && row_stats && ((uintptr_t)logits & 15) == 0, "softcap_ce_rows: logits 16-B aligned");
+  const int64_t units = M * ((N + 511) / 512);
+  const int64_t blocks = std::min<int64_t>((units + 3) / 4, (int64_t)num_cus() * 8);
+  hipLaunchKernelGGL(softcap_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, N,
+                     (bf16_t*)logits, ld, cap, row_stats);
+  return svla::check_launch("softcap_ce_rows");
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // fp8 e4m3 GEMM (BASELINE configs[4]): both operands KC fp8 with per-row fp32 scales, the 4-wave kernel in fp8 mode.
 // ------------------------------------------------------------------------------------------------------------
 extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const float* a_scale,

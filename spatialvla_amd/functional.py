@@ -731,7 +731,10 @@ class LMHeadCEFn(torch.autograd.Function):
         logits_buf = _empty(M, ldv, like=h)
         ntn = K.ceil_div(V, 128)
         stats = _empty(M, ntn, 3, dtype=F32, like=h)
-        K.linear_fwd(h, [w], logits_buf[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=stats, cap=cap)
+        # plain-store GEMM (the 4-wave kernel's direct epilogue), then softcap + statistics as one HBM pass: the
+        # VALU-heavy SOFTCAP_CE epilogue inside the GEMM cost 13.4-13.9 ms per step against 9.2 + ~2 ms
+        K.linear_fwd(h, [w], logits_buf[:, :V])
+        K.softcap_ce_rows(logits_buf, V, stats, cap)
         lse = _empty(M, dtype=F32, like=h)
         argmax = _empty(M, dtype=torch.int64, like=h)
         loss_rows = _empty(M, dtype=F32, like=h)

@@ -573,6 +573,16 @@ def add(a, b, out):
     L.check(L.lib().svla_add_bf16(a.numel(), a.data_ptr(), b.data_ptr(), out.data_ptr(), _stream()), "add")
 
 
+def softcap_ce_rows(logits: torch.Tensor, N: int, row_stats: torch.Tensor, cap: float):
+    """In place: logits[:, :N] = softcap(logits) and row_stats [M, ceil(N/128), 3] (svla_softcap_ce_rows)."""
+    _chk_bf16(logits, "softcap_ce_rows")
+    M, ld = logits.shape[0], _ld(logits)
+    _req(row_stats.dtype == torch.float32 and row_stats.is_contiguous() and row_stats.numel() >= M * ceil_div(N, 128) * 3,
+         "softcap_ce_rows: row_stats must be a contiguous fp32 [M, ceil(N/128), 3]")
+    L.check(L.lib().svla_softcap_ce_rows(M, N, logits.data_ptr(), ld, float(cap), row_stats.data_ptr(), _stream()),
+            "svla_softcap_ce_rows")
+
+
 def ce_finalize(N, ntiles, row_stats, logits, target, lse, argmax, loss_rows, loss_out):
     M = logits.shape[0]
     L.check(L.lib().svla_ce_finalize(M, N, ntiles, row_stats.data_ptr(), logits.data_ptr(), _ld(logits),

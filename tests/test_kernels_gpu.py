@@ -399,6 +399,27 @@ def test_gemm_softcap_ce(cuda, M):
     assert d[:, V:].abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("M,V", [(300, 1000), (512, 30011), (9, 264)])
+def test_softcap_ce_rows_matches_epilogue(cuda, M, V):
+    """svla_softcap_ce_rows over plain-store logits == the SOFTCAP_CE GEMM epilogue bitwise: the softcapped logits
+    and every row_stats entry {max, sumexp, argmax} (same 8-column chunks, same 16-lane group combine)."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(31)
+    K = 256
+    h, w = _r(M, K), _r(V, K, scale=0.3)
+    ldv = Kn.round_up(V, 64)
+    ntn = Kn.ceil_div(V, 128)
+    fused = torch.empty(M, ldv, dtype=BF, device=cuda)
+    st_f = torch.full((M, ntn, 3), float("nan"), device=cuda)
+    Kn.linear_fwd(h, [w], fused[:, :V], kind=L.EPI_SOFTCAP_CE, row_stats=st_f, cap=30.0)
+    raw = torch.empty(M, ldv, dtype=BF, device=cuda)
+    Kn.linear_fwd(h, [w], raw[:, :V])
+    st_r = torch.full((M, ntn, 3), float("nan"), device=cuda)
+    Kn.softcap_ce_rows(raw, V, st_r, 30.0)
+    assert torch.equal(raw[:, :V], fused[:, :V])
+    assert torch.equal(st_r.view(torch.int32), st_f.view(torch.int32))
+
+
 @pytest.mark.parametrize("M", [256, 4])  # 256: MFMA tile epilogue; 4: the decode GEMV path
 def test_softcap_every_bf16_logit(cuda, M):
     """Every finite bf16 logit value through the SOFTCAP_CE epilogue (reciprocal-multiply divide, table tanh) against
