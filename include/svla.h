@@ -297,6 +297,15 @@ int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh, const void
                    int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* stream);
 int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream);
 
+/* Decode step (M <= 8 token rows, K <= 2560): the two Gemma2 norms between sublayers fused into the next projection,
+ * modeling_gemma2.py:487-496 -- h = bf16(res + bf16(rms(y; w1))) (stored to h_out, the new residual stream) and
+ * x = bf16(rms(h; w2)), bitwise svla_add_rmsnorm2_fwd -- then C = epi(x @ B^T) as svla_gemm_bf16's small-M path:
+ * epi STORE (q|k|v, B KC, segments allowed) or GEGLU (gate|up, two SVLA_SEG_GEGLU segments, out1 = g, out2 = u).
+ * res / y / h_out share the row stride ldx. */
+int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* res, const void* y, int64_t ldx, const void* w1,
+                       const void* w2, float eps1, float eps2, void* h_out, const svla_operand* B, void* c,
+                       int64_t ldc, const svla_epilogue* epi, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Softcapped lm_head cross-entropy (modeling_gemma2.py:993-997 + modeling_spatialvla.py:415-430,
  * action argmax train/monkey_patch.py:267-309).  Logits come from svla_gemm_bf16 with

@@ -2594,6 +2594,165 @@ bool try_gemv_pf(int variant, int M, int64_t rows, int64_t K, const svla_operand
   return false;
 }
 
+// Decode GEMV with the two preceding Gemma2 norms in its prologue (svla_gemv_rmsnorm2): x = bf16(rms(h; w2)),
+// h = bf16(res + bf16(rms(y; w1))) -- rms_add_norm2_kernel's chunk map and reduction order, so h and x are bitwise
+// its outputs -- computed per block into LDS, h also stored by block 0; then the prefetching GEMV of gemv_pf_kernel
+// on x.  Every thread issues its norm-input loads before its weight loads (vmcnt retires in order: the norm waits
+// for its own inputs only), and the norm's block reductions use raw barriers (no vmcnt drain), so the weight stream
+// is in flight while the norms run -- one launch and one HBM round trip fewer per fused norm.
+constexpr int GN_MAXC = 2;  // norm chunks per thread: K <= 256 * 8 * 2
+template <int KCH, bool GEGLU>
+__global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ res,
+                                                         const bf16_t* __restrict__ y, int64_t ldx,
+                                                         const bf16_t* __restrict__ w1, const bf16_t* __restrict__ w2,
+                                                         float eps1, float eps2, bf16_t* __restrict__ h_out,
+                                                         svla_operand B, bf16_t* __restrict__ c, int64_t ldc,
+                                                         svla_epilogue E) {
+  constexpr int NW = GEGLU ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) bf16_t xs[GEMV_MAXM * 2560];
+  __shared__ float red[2][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int nch = (int)(K >> 3);
+  // norm inputs first (older in vmcnt order than the weight stream)
+  u32x4 yv[GEMV_MAXM][GN_MAXC], rv[GEMV_MAXM][GN_MAXC], w1v[GN_MAXC], w2v[GN_MAXC];
+#pragma unroll
+  for (int cI = 0; cI < GN_MAXC; ++cI) {
+    const int ch = t + cI * 256;
+    w1v[cI] = w2v[cI] = u32x4{0u, 0u, 0u, 0u};
+    if (ch < nch) {
+      w1v[cI] = *reinterpret_cast<const u32x4*>(w1 + ch * 8);
+      w2v[cI] = *reinterpret_cast<const u32x4*>(w2 + ch * 8);
+    }
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) {
+      yv[m][cI] = rv[m][cI] = u32x4{0u, 0u, 0u, 0u};
+      if (m < M && ch < nch) {
+        yv[m][cI] = *reinterpret_cast<const u32x4*>(y + m * ldx + ch * 8);
+        rv[m][cI] = *reinterpret_cast<const u32x4*>(res + m * ldx + ch * 8);
+      }
+    }
+  }
+  // weight stream (as gemv_pf_kernel, one row -- or gate|up row pair -- per wave)
+  const int64_t r0 = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t n = r0 < rows ? r0 : rows - 1;
+  u32x4 wt[NW][KCH];
+  {
+    const bf16_t* wr[NW];
+    if constexpr (GEGLU) {
+      wr[0] = (const bf16_t*)B.ptr[0] + n * B.ld;
+      wr[NW - 1] = (const bf16_t*)B.ptr[1] + n * B.ld;
+    } else {
+      wr[0] = gemv_row(B, n);
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+#pragma unroll
+      for (int i = 0; i < KCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        wt[q][i] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + k)) : u32x4{0, 0, 0, 0};
+      }
+  }
+  // the norms, one row at a time (block_sum's order: wave butterfly, then the four waves in order)
+  auto bsum = [&](float v, int slot) {
+    v = wave_sum(v);
+    if (lane == 0) red[slot][wv] = v;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    return ((red[slot][0] + red[slot][1]) + red[slot][2]) + red[slot][3];
+  };
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) {
+    if (m < M) {
+      float v[GN_MAXC][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int cI = 0; cI < GN_MAXC; ++cI)
+        if (t + cI * 256 < nch) {
+          unpack8(yv[m][cI], v[cI]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += v[cI][j] * v[cI][j];
+        }
+      const float rstd1 = rsqrtf(bsum(ss, 0) / (float)K + eps1);
+      float ss2 = 0.f;
+#pragma unroll
+      for (int cI = 0; cI < GN_MAXC; ++cI) {
+        const int ch = t + cI * 256;
+        if (ch < nch) {
+          float wf[8], r[8];
+          unpack8(w1v[cI], wf);
+          unpack8(rv[m][cI], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[cI][j] = round_bf(r[j] + round_bf((v[cI][j] * rstd1) * (1.0f + wf[j])));
+            ss2 += v[cI][j] * v[cI][j];
+          }
+          if (blockIdx.x == 0) *reinterpret_cast<u32x4*>(h_out + m * ldx + ch * 8) = pack8(v[cI]);
+        }
+      }
+      const float rstd2 = rsqrtf(bsum(ss2, 1) / (float)K + eps2);
+#pragma unroll
+      for (int cI = 0; cI < GN_MAXC; ++cI) {
+        const int ch = t + cI * 256;
+        if (ch < nch) {
+          float wf[8], o[8];
+          unpack8(w2v[cI], wf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (v[cI][j] * rstd2) * (1.0f + wf[j]);
+          *reinterpret_cast<u32x4*>(xs + m * 2560 + ch * 8) = pack8(o);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (r0 >= rows) return;
+  float acc[NW][GEMV_MAXM];
+#pragma unroll
+  for (int q = 0; q < NW; ++q)
+#pragma unroll
+    for (int m = 0; m < GEMV_MAXM; ++m) acc[q][m] = 0.f;
+#pragma unroll
+  for (int i = 0; i < KCH; ++i) {
+    const int64_t k = (int64_t)lane * 8 + i * 512;
+    if (k < K) {
+      float wf[NW][8];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) unpack8(wt[q][i], wf[q]);
+#pragma unroll
+      for (int m = 0; m < GEMV_MAXM; ++m) {
+        if (m < M) {
+          float xf[8];
+          unpack8(*reinterpret_cast<const u32x4*>(xs + m * 2560 + k), xf);
+#pragma unroll
+          for (int q = 0; q < NW; ++q)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[q][m] = fmaf(wf[q][j], xf[j], acc[q][m]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < GEMV_MAXM; ++m) {
+    if (m < M) {
+      float v[NW];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) v[q] = wave_sum(acc[q][m]);
+      if (lane == 0) {
+        if constexpr (GEGLU) {
+          const float g = round_bf(v[0]), u = round_bf(v[1]);
+          c[m * ldc + r0] = f2bf(round_bf(gelu_tanh(g)) * u);
+          ((bf16_t*)E.out1)[m * E.ld_out1 + r0] = f2bf(g);
+          ((bf16_t*)E.out2)[m * E.ld_out2 + r0] = f2bf(u);
+        } else {
+          c[m * ldc + r0] = f2bf(v[0]);
+        }
+      }
+    }
+  }
+}
+
 template <int RW, bool GEGLU>
 int launch_gemv(int M, int64_t rows, int64_t K, const svla_operand& A, const svla_operand& B, bf16_t* c,
                 int64_t ldc, const svla_epilogue& E, hipStream_t s) {
@@ -2786,6 +2945,37 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
   ctx.ws_bytes = workspace ? ws_bytes : 0;
   ctx.variant = variant;
   return gemm_dispatch(M, N, K, A, B, c_ptr, c_seg_start, c_nseg, ldc, epi, ctx, stream);
+}
+
+extern "C" int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* res, const void* y, int64_t ldx,
+                                  const void* w1, const void* w2, float eps1, float eps2, void* h_out,
+                                  const svla_operand* B, void* c, int64_t ldc, const svla_epilogue* epi, void* stream) {
+  SVLA_CHECK_ARG(M >= 1 && M <= GEMV_MAXM && N > 0 && K > 0 && K % 8 == 0 && K <= 2560 && K <= 256 * 8 * GN_MAXC,
+                 "gemv_rmsnorm2: M in [1, %d], K a multiple of 8 <= 2560", GEMV_MAXM);
+  SVLA_CHECK_ARG(res && y && w1 && w2 && h_out && B && c && epi, "gemv_rmsnorm2: NULL argument");
+  SVLA_CHECK_ARG(ldx % 8 == 0 && ldx >= K && ldc % 8 == 0, "gemv_rmsnorm2: ldx >= K and ldc multiples of 8");
+  SVLA_CHECK_ARG(B->layout == SVLA_LAYOUT_KC && B->ld % 8 == 0, "gemv_rmsnorm2: B must be KC with ld % 8 == 0");
+  const bool geglu = epi->kind == SVLA_EPI_GEGLU;
+  SVLA_CHECK_ARG(geglu || (epi->kind == SVLA_EPI_STORE && !epi->accumulate && epi->alpha == 1.0f),
+                 "gemv_rmsnorm2: epilogue STORE (plain) or GEGLU");
+  if (geglu)
+    SVLA_CHECK_ARG(B->nseg == 2 && B->seg_dim == SVLA_SEG_GEGLU && B->seg_start[1] * 2 == N && epi->out1 && epi->out2,
+                   "gemv_rmsnorm2: GEGLU needs two B segments of N/2 rows and out1/out2");
+  const int64_t rows = geglu ? N / 2 : N;
+  const int kch = (int)((K + 511) / 512);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+#define SVLA_GN(KC, GG)                                                                                            \
+  hipLaunchKernelGGL((gemv_norm2_kernel<KC, GG>), grid, block, 0, s, (int)M, rows, K, (const bf16_t*)res,           \
+                     (const bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2, (bf16_t*)h_out, *B,     \
+                     (bf16_t*)c, ldc, *epi)
+  if (geglu) {
+    if (kch <= 4) SVLA_GN(4, true); else SVLA_GN(5, true);
+  } else {
+    if (kch <= 4) SVLA_GN(4, false); else SVLA_GN(5, false);
+  }
+#undef SVLA_GN
+  return svla::check_launch("gemv_rmsnorm2");
 }
 
 namespace {

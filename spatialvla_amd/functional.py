@@ -420,15 +420,26 @@ def gemma_attention_weights(qkv, kv_class, cfg: GemmaAttnCfg) -> torch.Tensor:
 DECODE_FUSED = [os.environ.get("SVLA_DECODE_FUSED", "1") != "0"]
 
 
+# decode steps fold the two norms between sublayers into the next projection's prologue (svla_gemv_rmsnorm2)
+DECODE_NORM_FUSED = [os.environ.get("SVLA_DECODE_NORM_FUSED", "1") != "0"]
+
+
 @torch.no_grad()
-def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_class, p0, cfg: GemmaAttnCfg):
+def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_class, p0, cfg: GemmaAttnCfg,
+                           pre=None):
     """Gemma2Attention.forward with a KV cache (modeling_gemma2.py:364-413, cache update :387-395), inference
     only.  x holds the cfg.L new tokens of each of the cfg.B sequences, at absolute positions p0 .. p0+L-1;
     their rotated k and v are written into rows p0.. of k_cache/v_cache ([B, capacity, Hkv*D]).  The prefill
     (p0 == 0) runs the flash kernel of the uncached forward over the prompt, so it is bit-identical to it;
-    later steps run the decode kernel over the first p0+L cache rows."""
-    x = _c(x)
-    M, H = x.shape
+    later steps run the decode kernel over the first p0+L cache rows.  pre = (res, y, w1, w2, eps1, eps2, h_out): a
+    decode step whose input x = rms(res + rms(y; w1); w2) is formed inside the q|k|v GEMV (h_out the new residual)."""
+    if pre is not None:
+        if p0 == 0:
+            raise ValueError("gemma_attention_cached: the fused norm prologue is a decode-step path (p0 > 0)")
+        M, H = pre[1].shape
+    else:
+        x = _c(x)
+        M, H = x.shape
     B, Lq = cfg.B, cfg.L
     qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
     qkv = _empty(M, qd + 2 * kd, like=x)
@@ -438,7 +449,10 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         # the kernels read table row b*Lq+t (per-sequence positions), so a shared table is repeated per sequence
         if cos.shape[0] != B * Lq:
             cos, sin = cos.repeat(B, 1), sin.repeat(B, 1)
-        K.linear_fwd(x, [wq, wk, wv], qkv)
+        if pre is not None:
+            K.gemv_rmsnorm2(*pre, [wq, wk, wv], qkv)
+        else:
+            K.linear_fwd(x, [wq, wk, wv], qkv)
         if DECODE_FUSED[0]:
             K.attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
                                cfg.softcap, kv_class, cfg.window, attn)
@@ -458,6 +472,20 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         K.attn_fwd(a, attn, lse)
     out = _empty(M, wo.shape[0], like=x)
     K.linear_fwd(attn, [wo], out)
+    return out
+
+
+@torch.no_grad()
+def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd):
+    """Decode-step Gemma2 MLP (modeling_gemma2.py:91-92) whose input is the post-attention + pre-feedforward norm pair
+    (:487-490), formed inside the gate|up GEMV: h_out = res + rms(y; w1) (the residual stream), returns
+    down(gelu_tanh(gate x) * up x) with x = rms(h_out; w2)."""
+    M = y.shape[0]
+    I = wg.shape[0]
+    hact, g, u = (_empty(M, I, like=y) for _ in range(3))
+    K.gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, [wg, wu], hact, geglu_out=(g, u))
+    out = _empty(M, wd.shape[0], like=y)
+    K.linear_fwd(hact, [wd], out)
     return out
 
 

@@ -175,6 +175,29 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
               colscale=colscale))
 
 
+def gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, weights: List[torch.Tensor], out: torch.Tensor, geglu_out=None):
+    """Decode step: h_out = bf16(res + rms(y; w1)), x = rms(h_out; w2) (svla_add_rmsnorm2_fwd, bitwise), then
+    out = x @ cat(weights)^T (STORE), or with geglu_out = (g, u) and weights = [w_gate, w_up]: out = GeGLU of the
+    gate|up projection (svla_gemv_rmsnorm2, M <= 8 rows)."""
+    M, Kd = y.shape
+    for t, nm in ((res, "res"), (y, "y"), (h_out, "h_out"), (w1, "w1"), (w2, "w2"), (out, "out")):
+        _chk_bf16(t, "gemv_rmsnorm2 " + nm)
+    _req(res.shape == y.shape == h_out.shape and _ld(res) == _ld(y) == _ld(h_out), "gemv_rmsnorm2: res/y/h_out rows")
+    if geglu_out is not None:
+        I = weights[0].shape[0]
+        B = _operand(weights, L.LAYOUT_KC, L.SEG_GEGLU, [0, I])
+        N = 2 * I
+        e = _epi(L.EPI_GEGLU, out1=geglu_out[0], out2=geglu_out[1])
+    else:
+        weights = _merge_rows(weights)
+        starts, N = _starts([w.shape[0] for w in weights])
+        B = _operand(weights, L.LAYOUT_KC, L.SEG_OUTER, starts)
+        e = _epi(L.EPI_STORE)
+    L.check(L.lib().svla_gemv_rmsnorm2(M, N, Kd, res.data_ptr(), y.data_ptr(), _ld(y), w1.data_ptr(), w2.data_ptr(),
+                                       float(eps1), float(eps2), h_out.data_ptr(), ctypes.byref(B), out.data_ptr(),
+                                       _ld(out), ctypes.byref(e), _stream()), "svla_gemv_rmsnorm2")
+
+
 # Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch
 # record a pair of HIP events on the stream it is launched on (the current torch stream).
 launch_timer: dict = {}

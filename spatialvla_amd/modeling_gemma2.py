@@ -185,11 +185,14 @@ class Gemma2Attention(nn.Module):
         self.o_proj = nn.Linear(self.num_heads * self.head_dim, self.hidden_size, bias=False)
         self.rotary_emb = Gemma2RotaryEmbedding(self.head_dim, self.max_position_embeddings, self.rope_theta)
 
+    def attn_cfg(self, B: int, Lq: int) -> "Fn.GemmaAttnCfg":
+        return Fn.GemmaAttnCfg(B, Lq, self.num_heads, self.num_key_value_heads, self.head_dim, self.scaling,
+                               float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
+
     def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None,
                 attn_sink: Optional[list] = None):
         B, Lq, H = hidden_states.shape
-        cfg = Fn.GemmaAttnCfg(B, Lq, self.num_heads, self.num_key_value_heads, self.head_dim, self.scaling,
-                              float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
+        cfg = self.attn_cfg(B, Lq)
         cos, sin = rope
         if cache is not None:
             i = self.layer_idx
@@ -316,6 +319,9 @@ class Gemma2Model(nn.Module):
         shp = hidden.shape
         H = shp[-1]
         res = hidden.reshape(-1, H).contiguous()
+        if (Fn.DECODE_NORM_FUSED[0] and cache.seen_tokens > 0 and res.shape[0] <= 8
+                and all(getattr(l.mlp, "_svla_fp8", None) is None for l in layers)):
+            return self._decode_fused(res, shp, rope, cache)
         x = layers[0].input_layernorm(res)
         for i, layer in enumerate(layers):
             a = layer.self_attn(x.view(shp), attention_mask, rope, cache).reshape(-1, H)
@@ -327,6 +333,37 @@ class Gemma2Model(nn.Module):
             po = layer.post_feedforward_layernorm
             res, x = torch.empty_like(res), torch.empty_like(res)
             Kn.add_rmsnorm2_fwd(h, m, po.weight, nxt.weight, po.eps, nxt.eps, res, x)
+        cache.seen_tokens += shp[1]
+        return x.view(shp)
+
+
+    def _decode_fused(self, res, shp, rope, cache):
+        """A decode step (<= 8 new tokens) with every norm pair between sublayers inside the next projection's GEMV
+        (svla_gemv_rmsnorm2): post_feedforward + the next input_layernorm in the q|k|v GEMV, post_attention +
+        pre_feedforward in the gate|up GEMV -- the outputs of _forward_cached's unfused loop, two launches fewer per
+        layer (modeling_gemma2.py:475-496, :777)."""
+        layers = self.layers[: self.config.num_hidden_layers]
+        B, Lq = shp[0], shp[1]
+        cos, sin = rope
+        x = layers[0].input_layernorm(res)
+        h = m = None
+        for i, layer in enumerate(layers):
+            at, mlp = layer.self_attn, layer.mlp
+            pre = None
+            if i > 0:
+                po = layers[i - 1].post_feedforward_layernorm
+                res = torch.empty_like(h)
+                pre = (h, m, po.weight, layer.input_layernorm.weight, po.eps, layer.input_layernorm.eps, res)
+            a = Fn.gemma_attention_cached(x if i == 0 else None, at.q_proj.weight, at.k_proj.weight, at.v_proj.weight,
+                                          at.o_proj.weight, cos, sin, cache.key_cache[i], cache.value_cache[i],
+                                          cache.kv_class, cache.seen_tokens, at.attn_cfg(B, Lq), pre=pre)
+            pa, pf = layer.post_attention_layernorm, layer.pre_feedforward_layernorm
+            h = torch.empty_like(res)
+            m = Fn.gemma_mlp_decode(res, a, pa.weight, pf.weight, pa.eps, pf.eps, h, mlp.gate_proj.weight,
+                                    mlp.up_proj.weight, mlp.down_proj.weight)
+        po = layers[-1].post_feedforward_layernorm
+        res, x = torch.empty_like(h), torch.empty_like(h)
+        Kn.add_rmsnorm2_fwd(h, m, po.weight, self.norm.weight, po.eps, self.norm.eps, res, x)
         cache.seen_tokens += shp[1]
         return x.view(shp)
 

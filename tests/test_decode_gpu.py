@@ -309,3 +309,59 @@ def test_add_rmsnorm2_bitwise(cuda, rows):
     h, x = torch.empty_like(res), torch.empty_like(res)
     Kn.add_rmsnorm2_fwd(res, y, w1, w2, 1e-6, 1e-6, h, x)
     assert torch.equal(h, h_ref) and torch.equal(x, x_ref)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("geglu", [False, True])
+def test_gemv_rmsnorm2_bitwise(cuda, M, geglu):
+    """svla_gemv_rmsnorm2 == svla_add_rmsnorm2_fwd followed by the decode GEMV, bit for bit: h, and the q|k|v
+    (three weight segments) or gate|up GeGLU outputs."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(17)
+    N = 2304
+    res, y = _r(M, N), _r(M, N, scale=3.0)
+    w1, w2 = _r(N, scale=0.3), _r(N, scale=0.3)
+    h_ref, x_ref = torch.empty_like(res), torch.empty_like(res)
+    Kn.add_rmsnorm2_fwd(res, y, w1, w2, 1e-6, 1e-6, h_ref, x_ref)
+    h = torch.full_like(res, 7.0)
+    if geglu:
+        I = 9216
+        wg, wu = _r(I, N, scale=0.02), _r(I, N, scale=0.02)
+        ref = [torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3)]
+        Kn.linear_geglu_fwd(x_ref, wg, wu, *ref)
+        out = [torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3)]
+        Kn.gemv_rmsnorm2(res, y, w1, w2, 1e-6, 1e-6, h, [wg, wu], out[0], geglu_out=(out[1], out[2]))
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+    else:
+        ws = [_r(2048, N, scale=0.02), _r(1024, N, scale=0.02), _r(1024, N, scale=0.02)]
+        ref = torch.empty(M, 4096, dtype=BF, device=cuda)
+        Kn.linear_fwd(x_ref, ws, ref)
+        out = torch.empty_like(ref)
+        Kn.gemv_rmsnorm2(res, y, w1, w2, 1e-6, 1e-6, h, ws, out)
+        assert torch.equal(out, ref)
+    assert torch.equal(h, h_ref)
+
+
+def test_decode_norm_fusion_bitwise(cuda):
+    """A decode step with the norm pairs inside the projections' GEMVs gives the logits of the unfused loop, bit for
+    bit (predict_action tokens as well)."""
+    from spatialvla_amd import functional as Fn
+    model, g = _tiny_model(cuda)
+    ids = g["in.input_ids"][:, :-13]
+    inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    model.decode_graphs = False
+    outs = {}
+    try:
+        for fused in (False, True):
+            Fn.DECODE_NORM_FUSED[0] = fused
+            with torch.no_grad():
+                o1 = model(input_ids=ids.to(cuda), pixel_values=inputs["pixel_values"].to(cuda),
+                           intrinsic=inputs["intrinsic"].to(cuda), use_cache=True)
+                o2 = model(input_ids=ids[:, -1:].to(cuda), past_key_values=o1.past_key_values)
+            outs[fused] = (o2.logits.clone(), model.predict_action(inputs, max_new_tokens=6, eos_token_id=-1))
+    finally:
+        Fn.DECODE_NORM_FUSED[0] = True
+        model.decode_graphs = True
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
