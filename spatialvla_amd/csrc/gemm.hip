@@ -2609,8 +2609,9 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
                                                          svla_operand B, bf16_t* __restrict__ c, int64_t ldc,
                                                          svla_epilogue E) {
   constexpr int NW = GEGLU ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) bf16_t xs[GEMV_MAXM * 2560];
-  __shared__ float red[2][4];
+  extern __shared__ __attribute__((aligned(16))) char gn_smem[];  // [M][K] bf16 x, then the reduction slots
+  bf16_t* const xs = reinterpret_cast<bf16_t*>(gn_smem);
+  float (*red)[4] = reinterpret_cast<float (*)[4]>(gn_smem + (size_t)M * K * 2);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int nch = (int)(K >> 3);
   // norm inputs first (older in vmcnt order than the weight stream)
@@ -2699,7 +2700,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
           unpack8(w2v[cI], wf);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = (v[cI][j] * rstd2) * (1.0f + wf[j]);
-          *reinterpret_cast<u32x4*>(xs + m * 2560 + ch * 8) = pack8(o);
+          *reinterpret_cast<u32x4*>(xs + m * K + ch * 8) = pack8(o);
         }
       }
     }
@@ -2724,7 +2725,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
       for (int m = 0; m < GEMV_MAXM; ++m) {
         if (m < M) {
           float xf[8];
-          unpack8(*reinterpret_cast<const u32x4*>(xs + m * 2560 + k), xf);
+          unpack8(*reinterpret_cast<const u32x4*>(xs + m * K + k), xf);
 #pragma unroll
           for (int q = 0; q < NW; ++q)
 #pragma unroll
@@ -2964,9 +2965,10 @@ extern "C" int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* r
   const int64_t rows = geglu ? N / 2 : N;
   const int kch = (int)((K + 511) / 512);
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const size_t lds = (size_t)M * K * 2 + 2 * 4 * sizeof(float);  // x rows + reduction slots: occupancy as the GEMV's
   hipStream_t s = (hipStream_t)stream;
 #define SVLA_GN(KC, GG)                                                                                            \
-  hipLaunchKernelGGL((gemv_norm2_kernel<KC, GG>), grid, block, 0, s, (int)M, rows, K, (const bf16_t*)res,           \
+  hipLaunchKernelGGL((gemv_norm2_kernel<KC, GG>), grid, block, lds, s, (int)M, rows, K, (const bf16_t*)res,         \
                      (const bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2, (bf16_t*)h_out, *B,     \
                      (bf16_t*)c, ldc, *epi)
   if (geglu) {

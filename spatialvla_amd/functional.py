@@ -437,13 +437,15 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         if p0 == 0:
             raise ValueError("gemma_attention_cached: the fused norm prologue is a decode-step path (p0 > 0)")
         M, H = pre[1].shape
+        like = pre[1]
     else:
         x = _c(x)
         M, H = x.shape
+        like = x
     B, Lq = cfg.B, cfg.L
     qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
-    qkv = _empty(M, qd + 2 * kd, like=x)
-    attn = _empty(M, qd, like=x)
+    qkv = _empty(M, qd + 2 * kd, like=like)
+    attn = _empty(M, qd, like=like)
     if p0 > 0:
         # decode step: plain projection, then one launch rotates q / k, appends k / v to the cache and attends;
         # the kernels read table row b*Lq+t (per-sequence positions), so a shared table is repeated per sequence
@@ -465,12 +467,12 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         k_cache[:, :Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
         v_cache[:, :Lq].copy_(qkv[:, qd + kd:].view(B, Lq, kd))
     if p0 == 0:
-        lse = _empty(B, cfg.Hq, Lq, dtype=F32, like=x)
+        lse = _empty(B, cfg.Hq, Lq, dtype=F32, like=like)
         cls = kv_class[:, :Lq].contiguous()  # held until the launch: attn_args keeps only its pointer
         a = K.attn_args(B, Lq, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, cls, cfg.window)
         K.attn_fwd(a, attn, lse)
-    out = _empty(M, wo.shape[0], like=x)
+    out = _empty(M, wo.shape[0], like=like)
     K.linear_fwd(attn, [wo], out)
     return out
 
