@@ -296,6 +296,11 @@ int svla_relu_bwd(int64_t n, const void* x, const void* dy, void* dx, void* stre
 int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg, const void* u,
                    int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* stream);
 int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream);
+/* GELU pass over a [M][N] bf16 matrix (N % 8 == 0), the rounding points of the fused GEMM epilogues: mode 0
+ * y = bf16(gelu_tanh(x)) (SigLIP MLP fc1 activation, transformers SiglipMLP gelu_pytorch_tanh), 1 y = bf16(gelu_erf(x))
+ * (BEiT MLP, exact GELU; in place allowed), 2 y = bf16(x * gelu_tanh'(pre)) (the fc1 input gradient, x = dL/dact). */
+int svla_gelu_rows(int64_t M, int64_t N, int32_t mode, const void* x, int64_t ldx, const void* pre, int64_t ldp,
+                   void* y, int64_t ldy, void* stream);
 
 /* Decode step (M <= 8 token rows, K <= 2560): the two Gemma2 norms between sublayers fused into the next projection,
  * modeling_gemma2.py:487-496 -- h = bf16(res + bf16(rms(y; w1))) (stored to h_out, the new residual stream) and

@@ -2601,7 +2601,7 @@ bool try_gemv_pf(int variant, int M, int64_t rows, int64_t K, const svla_operand
 // for its own inputs only), and the norm's block reductions use raw barriers (no vmcnt drain), so the weight stream
 // is in flight while the norms run -- one launch and one HBM round trip fewer per fused norm.
 constexpr int GN_MAXC = 2;  // norm chunks per thread: K <= 256 * 8 * 2
-template <int KCH, bool GEGLU>
+template <int KCH, bool GEGLU, int MR>
 __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, int64_t K, const bf16_t* __restrict__ res,
                                                          const bf16_t* __restrict__ y, int64_t ldx,
                                                          const bf16_t* __restrict__ w1, const bf16_t* __restrict__ w2,
@@ -2615,7 +2615,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int nch = (int)(K >> 3);
   // norm inputs first (older in vmcnt order than the weight stream)
-  u32x4 yv[GEMV_MAXM][GN_MAXC], rv[GEMV_MAXM][GN_MAXC], w1v[GN_MAXC], w2v[GN_MAXC];
+  u32x4 yv[MR][GN_MAXC], rv[MR][GN_MAXC], w1v[GN_MAXC], w2v[GN_MAXC];
 #pragma unroll
   for (int cI = 0; cI < GN_MAXC; ++cI) {
     const int ch = t + cI * 256;
@@ -2625,7 +2625,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
       w2v[cI] = *reinterpret_cast<const u32x4*>(w2 + ch * 8);
     }
 #pragma unroll
-    for (int m = 0; m < GEMV_MAXM; ++m) {
+    for (int m = 0; m < MR; ++m) {
       yv[m][cI] = rv[m][cI] = u32x4{0u, 0u, 0u, 0u};
       if (m < M && ch < nch) {
         yv[m][cI] = *reinterpret_cast<const u32x4*>(y + m * ldx + ch * 8);
@@ -2663,7 +2663,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
     return ((red[slot][0] + red[slot][1]) + red[slot][2]) + red[slot][3];
   };
 #pragma unroll
-  for (int m = 0; m < GEMV_MAXM; ++m) {
+  for (int m = 0; m < MR; ++m) {
     if (m < M) {
       float v[GN_MAXC][8];
       float ss = 0.f;
@@ -2709,11 +2709,11 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (r0 >= rows) return;
-  float acc[NW][GEMV_MAXM];
+  float acc[NW][MR];
 #pragma unroll
   for (int q = 0; q < NW; ++q)
 #pragma unroll
-    for (int m = 0; m < GEMV_MAXM; ++m) acc[q][m] = 0.f;
+    for (int m = 0; m < MR; ++m) acc[q][m] = 0.f;
 #pragma unroll
   for (int i = 0; i < KCH; ++i) {
     const int64_t k = (int64_t)lane * 8 + i * 512;
@@ -2722,7 +2722,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
 #pragma unroll
       for (int q = 0; q < NW; ++q) unpack8(wt[q][i], wf[q]);
 #pragma unroll
-      for (int m = 0; m < GEMV_MAXM; ++m) {
+      for (int m = 0; m < MR; ++m) {
         if (m < M) {
           float xf[8];
           unpack8(*reinterpret_cast<const u32x4*>(xs + m * K + k), xf);
@@ -2735,7 +2735,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
     }
   }
 #pragma unroll
-  for (int m = 0; m < GEMV_MAXM; ++m) {
+  for (int m = 0; m < MR; ++m) {
     if (m < M) {
       float v[NW];
 #pragma unroll
@@ -2967,16 +2967,20 @@ extern "C" int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* r
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const size_t lds = (size_t)M * K * 2 + 2 * 4 * sizeof(float);  // x rows + reduction slots: occupancy as the GEMV's
   hipStream_t s = (hipStream_t)stream;
-#define SVLA_GN(KC, GG)                                                                                            \
-  hipLaunchKernelGGL((gemv_norm2_kernel<KC, GG>), grid, block, lds, s, (int)M, rows, K, (const bf16_t*)res,         \
+#define SVLA_GN1(KC, GG, MR)                                                                                       \
+  hipLaunchKernelGGL((gemv_norm2_kernel<KC, GG, MR>), grid, block, lds, s, (int)M, rows, K, (const bf16_t*)res,     \
                      (const bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2, (bf16_t*)h_out, *B,     \
                      (bf16_t*)c, ldc, *epi)
+  // MR: rows held in registers (the norm inputs of every row are loaded up front; M = 1 is the batch-1 decode step)
+#define SVLA_GN(KC, GG) \
+  if (M == 1) SVLA_GN1(KC, GG, 1); else SVLA_GN1(KC, GG, GEMV_MAXM);
   if (geglu) {
-    if (kch <= 4) SVLA_GN(4, true); else SVLA_GN(5, true);
+    if (kch <= 4) { SVLA_GN(4, true) } else { SVLA_GN(5, true) }
   } else {
-    if (kch <= 4) SVLA_GN(4, false); else SVLA_GN(5, false);
+    if (kch <= 4) { SVLA_GN(4, false) } else { SVLA_GN(5, false) }
   }
 #undef SVLA_GN
+#undef SVLA_GN1
   return svla::check_launch("gemv_rmsnorm2");
 }
 

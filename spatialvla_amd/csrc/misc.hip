@@ -207,6 +207,31 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, co
   *reinterpret_cast<u32x4*>(du + m * lddu + c) = pack8(ou);
 }
 
+// GELU as an HBM pass after a plain-store / bias GEMM (svla_gelu_rows): the VALU-heavy GELU epilogues ran slower
+// inside the GEMM than as a separate read-once / write-once pass.  The rounding points of the fused epilogues:
+// mode 0 y = bf16(gelu_tanh(x)), 1 y = bf16(gelu_erf(x)), 2 y = bf16(x * gelu_tanh'(pre)) (x = bf16 dL/dy).
+template <int MODE>
+__global__ __launch_bounds__(256) void gelu_rows_kernel(int64_t M, int64_t N, const bf16_t* x, int64_t ldx,
+                                                        const bf16_t* __restrict__ pre, int64_t ldp, bf16_t* y,
+                                                        int64_t ldy) {
+  const int64_t cpr = N / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * cpr) return;
+  const int64_t m = idx / cpr, c = (idx % cpr) * 8;
+  float v[8], o[8];
+  unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + c), v);
+  if constexpr (MODE == 2) {
+    float p[8];
+    unpack8(*reinterpret_cast<const u32x4*>(pre + m * ldp + c), p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j] * gelu_tanh_grad(p[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = MODE == 0 ? gelu_tanh(v[j]) : gelu_erf(v[j]);
+  }
+  *reinterpret_cast<u32x4*>(y + m * ldy + c) = pack8(o);
+}
+
 __global__ void add_kernel(int64_t n, const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
                            bf16_t* __restrict__ y) {
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
@@ -568,6 +593,26 @@ extern "C" int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh,
                      (const bf16_t*)dh, ldh, (const bf16_t*)g, ldg, (const bf16_t*)u, ldu, (bf16_t*)dg, lddg,
                      (bf16_t*)du, lddu);
   return svla::check_launch("geglu_bwd");
+}
+
+extern "C" int svla_gelu_rows(int64_t M, int64_t N, int32_t mode, const void* x, int64_t ldx, const void* pre,
+                              int64_t ldp, void* y, int64_t ldy, void* stream) {
+  SVLA_CHECK_ARG(M > 0 && N > 0 && N % 8 == 0 && mode >= 0 && mode <= 2 && x && y && (mode != 2 || pre),
+                 "gelu_rows: M, N (multiple of 8), mode 0..2, pointers");
+  SVLA_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && (mode != 2 || ldp % 8 == 0) && al16(x) && al16(y) &&
+                     (mode != 2 || al16(pre)), "gelu_rows: rows must be 16-B aligned");
+  const dim3 g(nblk(M * (N / 8), 256)), b(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0)
+    hipLaunchKernelGGL(gelu_rows_kernel<0>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
+                       (bf16_t*)y, ldy);
+  else if (mode == 1)
+    hipLaunchKernelGGL(gelu_rows_kernel<1>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
+                       (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(gelu_rows_kernel<2>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
+                       (bf16_t*)y, ldy);
+  return svla::check_launch("gelu_rows");
 }
 
 // ---------------------------------------------------------------- action-token accuracy (integer, bit-exact)

@@ -625,6 +625,11 @@ class SiglipAttentionFn(torch.autograd.Function):
         return (dx, dres, *rets, ret_wo, ret_bo, None, None)
 
 
+# SigLIP fc1 / BEiT fc1: bias GEMM + GELU pass (svla_gelu_rows) instead of the VALU-heavy GELU GEMM epilogues, which
+# ran slower inside the tile loop (profiles/r3l_epi_ab.txt); bitwise the same values (test_gelu_rows_matches_epilogues)
+GELU_PASS = [os.environ.get("SVLA_GELU_PASS", "1") != "0"]
+
+
 class SiglipMLPFn(torch.autograd.Function):
     """SiglipMLP + residual: res + fc2(gelu_tanh(fc1 x)) (transformers siglip [3p]); fc1 bias+GELU and
     fc2 bias+residual fused in GEMM epilogues, GELU derivative fused into the fc2 dgrad epilogue."""
@@ -637,7 +642,11 @@ class SiglipMLPFn(torch.autograd.Function):
         I = w1.shape[0]
         pre = _empty(M, I, like=x)
         act = _empty(M, I, like=x)
-        K.linear_fwd(x, [w1], act, kind=L.EPI_BIAS_GELU, bias=b1, out1=pre)
+        if GELU_PASS[0]:  # bias GEMM (the 4-wave kernel's direct epilogue), then the GELU as an HBM pass
+            K.linear_fwd(x, [w1], pre, kind=L.EPI_BIAS, bias=b1)
+            K.gelu_rows(K.GELU_TANH, pre, act)
+        else:
+            K.linear_fwd(x, [w1], act, kind=L.EPI_BIAS_GELU, bias=b1, out1=pre)
         out = _empty(M, w2.shape[0], like=x)
         K.linear_fwd(act, [w2], out, kind=L.EPI_BIAS_RESID, bias=b2, in0=res)
         ctx.save_for_backward(x, w1, b1, w2, b2, pre, act)
@@ -653,7 +662,11 @@ class SiglipMLPFn(torch.autograd.Function):
             K.linear_wgrad(dout, act, [dw2], accumulate=acc2)
         ret_b2 = _bias_grad(dout, b2, nig[5])
         dpre = torch.empty_like(pre)
-        K.linear_dgrad(dout, [w2], dpre, kind=L.EPI_GELU_BWD, in0=pre)
+        if GELU_PASS[0]:
+            K.linear_dgrad(dout, [w2], dpre)
+            K.gelu_rows(K.GELU_TANH_BWD, dpre, dpre, pre=pre)
+        else:
+            K.linear_dgrad(dout, [w2], dpre, kind=L.EPI_GELU_BWD, in0=pre)
         dx = torch.empty_like(x) if nig[0] else None
         if dx is not None:
             K.linear_dgrad(dpre, [w1], dx)
@@ -946,7 +959,11 @@ def beit_layer(layer, hidden_states, bias):
                  colscale=_layer_scale(layer.lambda_1, H, x), in0=x)
     K.layernorm_fwd(h, ln_after.weight, ln_after.bias, float(ln_after.eps), xn, mean, rstd)
     f1 = _empty(M, layer.mlp.fc1.weight.shape[0], like=x)
-    K.linear_fwd(xn, [layer.mlp.fc1.weight], f1, kind=L.EPI_BIAS_GELU_ERF, bias=layer.mlp.fc1.bias)
+    if GELU_PASS[0]:
+        K.linear_fwd(xn, [layer.mlp.fc1.weight], f1, kind=L.EPI_BIAS, bias=layer.mlp.fc1.bias)
+        K.gelu_rows(K.GELU_ERF, f1, f1)
+    else:
+        K.linear_fwd(xn, [layer.mlp.fc1.weight], f1, kind=L.EPI_BIAS_GELU_ERF, bias=layer.mlp.fc1.bias)
     y = _empty(M, H, like=x)
     K.linear_fwd(f1, [layer.mlp.fc2.weight], y, kind=L.EPI_BIAS_SCALE_RESID, bias=layer.mlp.fc2.bias,
                  colscale=_layer_scale(layer.lambda_2, H, x), in0=h)

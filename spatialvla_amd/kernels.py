@@ -596,6 +596,19 @@ def add(a, b, out):
     L.check(L.lib().svla_add_bf16(a.numel(), a.data_ptr(), b.data_ptr(), out.data_ptr(), _stream()), "add")
 
 
+GELU_TANH, GELU_ERF, GELU_TANH_BWD = 0, 1, 2
+
+
+def gelu_rows(mode: int, x: torch.Tensor, y: torch.Tensor, pre: Optional[torch.Tensor] = None):
+    """y = gelu_tanh(x) / gelu_erf(x) / x * gelu_tanh'(pre) over [M, N] bf16 rows (svla_gelu_rows)."""
+    _chk_bf16(x, "gelu_rows x")
+    _chk_bf16(y, "gelu_rows y")
+    M, N = x.shape
+    _req(y.shape == x.shape and (pre is None or pre.shape == x.shape), "gelu_rows: shapes")
+    L.check(L.lib().svla_gelu_rows(M, N, int(mode), x.data_ptr(), _ld(x), _ptr(pre), _ld(pre) if pre is not None else 0,
+                                   y.data_ptr(), _ld(y), _stream()), "svla_gelu_rows")
+
+
 def softcap_ce_rows(logits: torch.Tensor, N: int, row_stats: torch.Tensor, cap: float):
     """In place: logits[:, :N] = softcap(logits) and row_stats [M, ceil(N/128), 3] (svla_softcap_ce_rows)."""
     _chk_bf16(logits, "softcap_ce_rows")

@@ -826,3 +826,29 @@ def test_inv3x3_closed_form(cuda):
     assert (got - ref).abs().max() <= 1e-5 * ref.abs().max()
     got_bf = Kn.inv3x3(K0.to(torch.bfloat16).to(cuda)[None])  # the model's bf16 intrinsic, upcast like K.float()
     assert torch.allclose(got_bf[0], torch.linalg.inv(K0.to(torch.bfloat16).float()).to(cuda), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 4304, 1152), (1024, 4096, 1024)])
+def test_gelu_rows_matches_epilogues(cuda, M, N, K):
+    """Bias GEMM + svla_gelu_rows == the fused BIAS_GELU / BIAS_GELU_ERF epilogues, and plain dgrad + the backward
+    pass == the GELU_BWD epilogue, bit for bit."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(41)
+    x, w, b = _r(M, K), _r(N, K, scale=0.05), _r(N, scale=0.5)
+    act_f, pre_f = torch.empty(M, N, dtype=BF, device=cuda), torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, [w], act_f, kind=L.EPI_BIAS_GELU, bias=b, out1=pre_f)
+    pre, act = torch.empty_like(pre_f), torch.empty_like(act_f)
+    Kn.linear_fwd(x, [w], pre, kind=L.EPI_BIAS, bias=b)
+    Kn.gelu_rows(Kn.GELU_TANH, pre, act)
+    assert torch.equal(pre, pre_f) and torch.equal(act, act_f)
+    erf_f = torch.empty_like(act_f)
+    Kn.linear_fwd(x, [w], erf_f, kind=L.EPI_BIAS_GELU_ERF, bias=b)
+    Kn.gelu_rows(Kn.GELU_ERF, pre, pre)
+    assert torch.equal(pre, erf_f)
+    dout, w2 = _r(M, K), _r(K, N, scale=0.05)
+    d_f = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.linear_dgrad(dout, [w2], d_f, kind=L.EPI_GELU_BWD, in0=pre_f)
+    d = torch.empty_like(d_f)
+    Kn.linear_dgrad(dout, [w2], d)
+    Kn.gelu_rows(Kn.GELU_TANH_BWD, d, d, pre=pre_f)
+    assert torch.equal(d, d_f)
