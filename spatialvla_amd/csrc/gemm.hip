@@ -34,9 +34,9 @@ namespace {
 // a bf16 value, and bf16(tanh(a)) is a for |a| < 2^-8, 1 for |a| >= 4, and a 1280-entry table in between
 // (tools/gen_tanh_table.py; a correctly rounded fp32 tanh cast to bf16, as the reference's bf16 tanh).  Replaces
 // the branch-free polynomial/exp tanh (~17 VALU ops and two transcendentals) of the lm_head epilogue.
-template <typename Tab>
+template <typename Tab, bool V_IS_BF16 = false>
 __device__ __forceinline__ float softcap_bf16_tab(float v, float cap, float icap, Tab tab) {
-  const float a = round_bf(round_bf(v) * icap);
+  const float a = round_bf((V_IS_BF16 ? v : round_bf(v)) * icap);  // V_IS_BF16: v already a bf16 value
   const uint32_t u = __float_as_uint(a);
   const uint32_t ab = (u >> 16) & 0x7fffu;
   const uint32_t lo = (uint32_t)SVLA_TANH_TAB_E0 << 7, hi = (uint32_t)SVLA_TANH_TAB_E1 << 7;
@@ -75,6 +75,7 @@ struct Cfg {
 using CfgBig = Cfg<256, 256, 2, 4>;
 using CfgMid = Cfg<256, 128, 4, 2>;
 using CfgSmall = Cfg<128, 128, 2, 2>;
+using CfgTiny = Cfg<64, 64, 2, 2>;  // sub-wave grids of the B = 1 prefill (4x the blocks of 128x128)
 
 // RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
@@ -2939,7 +2940,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
                                  void* stream) {
-  SVLA_CHECK_ARG(variant >= 0 && variant <= 8, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 9, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   GemmCtx ctx;
   ctx.ws = workspace;
@@ -3122,6 +3123,16 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
     return launch<CfgBig>(M, N, K, *A, *B, C, *epi, s);
   }
   if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);
+  // Sub-wave grids (the B = 1 prefill: SigLIP / BEiT at 256 / 577 tokens): 128x128 tiles leave most CUs idle and a
+  // launch costs one tile's k-loop latency; 64x64 tiles put 4x the blocks on the chip.  Epilogues whose partials or
+  // halves assume a 128-column group (softcap-CE, GeGLU) and the head-wide ROPE keep the larger tiles.
+  // (both operands KC: the projections x @ W^T of the prefill; the RC staging of this kernel needs 128-wide tiles).
+  // 19.7 -> 14.9 us (BEiT q|k|v), 18.4 -> 11.4 (BEiT o), 52 -> 34 (BEiT fc2), 19.7 -> 12.5 (SigLIP q|k|v), bitwise
+  // the 128x128 result (tools/prefill_gemm_bench.py, profiles/r3n_prefill_gemm_ab.txt).
+  if ((variant == 0 || variant == 9) && tiles(128, 128) < num_cus() && seg_ok(64, 64) &&
+      A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && ek != SVLA_EPI_SOFTCAP_CE &&
+      ek != SVLA_EPI_GEGLU && ek != SVLA_EPI_ROPE)
+    return launch<CfgTiny>(M, N, K, *A, *B, C, *epi, s);
   if (variant != 1 && !kseg && seg_ok(256, 256) &&
       (tiles(256, 256) >= 512 || (sk_ok && tiles(256, 256) * nk >= 8 * num_cus()) || (variant == 8 && sk_ok)))
     return launch8(M, N, K, *A, *B, C, *epi, ctx, s);
@@ -3164,7 +3175,7 @@ __global__ __launch_bounds__(256) void softcap_rows_kernel(int64_t M, int64_t N,
       load8f(p, v, nv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        v[j] = softcap_bf16_tab(v[j], cap, icap, tab);
+        v[j] = softcap_bf16_tab<decltype(tab), true>(v[j], cap, icap, tab);  // v unpacked from bf16 logits
         if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
       }
 #pragma unroll

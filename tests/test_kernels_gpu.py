@@ -852,3 +852,38 @@ def test_gelu_rows_matches_epilogues(cuda, M, N, K):
     Kn.linear_dgrad(dout, [w2], d)
     Kn.gelu_rows(Kn.GELU_TANH_BWD, d, d, pre=pre_f)
     assert torch.equal(d, d_f)
+
+
+@pytest.mark.parametrize("M,N,K", [(577, 3072, 1024), (256, 1152, 4304), (300, 200, 136)])
+@pytest.mark.parametrize("layouts", ["nt", "nn", "tn"])
+def test_gemm_tiny_tiles(cuda, M, N, K, layouts):
+    """64x64 tiles of the sub-wave prefill grids (variant 9 = their dispatch; KC x KC only, the other layouts keep
+    the 128x128 tiles) against fp32, plain store and the bias / bias+residual epilogues; the same values as the
+    128x128 tiles (variant 1) within fp32 reordering."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(51)
+    if layouts == "nt":
+        a, b = _r(M, K), _r(N, K, scale=0.05)
+        ref = a.float() @ b.float().T
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_KC)
+    elif layouts == "nn":
+        a, b = _r(M, K), _r(K, N + (-N) % 8, scale=0.05)[:, :N]
+        ref = a.float() @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_RC)
+    else:
+        a, b = _r(K, M + (-M) % 8)[:, :M], _r(K, N + (-N) % 8, scale=0.05)[:, :N]
+        ref = a.float().T @ b.float()
+        A, B = Kn._operand([a], L.LAYOUT_RC), Kn._operand([b], L.LAYOUT_RC)
+    bias, res = _r(N + (-N) % 8, scale=0.5)[:N], _r(M, N + (-N) % 8)[:, :N]
+    outs = {}
+    for v in (9, 1):
+        c = torch.full((M, N + (-N) % 8), 7.0, dtype=BF, device=cuda)
+        Kn.gemm(M, N, K, A, B, [c[:, :N]], [0], c.stride(0), Kn._epi(), variant=v)
+        cb = torch.empty_like(c)
+        Kn.gemm(M, N, K, A, B, [cb[:, :N]], [0], cb.stride(0), Kn._epi(L.EPI_BIAS_RESID, bias=bias, in0=res),
+                variant=v)
+        outs[v] = (c, cb)
+    c, cb = outs[9]
+    assert rel_l2(c[:, :N], ref) < 5e-3 and bool((c[:, N:] == 7.0).all())
+    assert rel_l2(cb[:, :N], ref + bias.float() + res.float()) < 5e-3
+    assert rel_l2(c[:, :N], outs[1][0][:, :N]) < 2e-3

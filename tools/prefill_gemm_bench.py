@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from spatialvla_amd import kernels as K  # noqa: E402
 
 BF = torch.bfloat16
+VARIANTS = [int(v) for v in os.environ.get("SVLA_VARIANTS", "0,8").split(",")]
 SHAPES = [("beit_qkv", 577, 3072, 1024), ("beit_o", 577, 1024, 1024), ("beit_fc1", 577, 4096, 1024),
           ("beit_fc2", 577, 1024, 4096), ("siglip_qkv", 256, 3456, 1152), ("siglip_o", 256, 1152, 1152),
           ("siglip_fc1", 256, 4304, 1152), ("siglip_fc2", 256, 1152, 4304)]
@@ -44,14 +45,14 @@ def main():
         w = (torch.randn(N, Kd, device="cuda") * 0.03).to(BF)
         res = {}
         outs = {}
-        for v in (0, 8):
+        for v in VARIANTS:
             K.gemm_variant = v
             y = torch.empty(M, N, dtype=BF, device="cuda")
             res[v] = round(timed(lambda: K.linear_fwd(x, [w], y)), 2)
             outs[v] = y.float()
         K.gemm_variant = 0
-        rel = float((outs[0] - outs[8]).norm() / outs[0].norm())
-        print(json.dumps({"shape": name, "M": M, "N": N, "K": Kd, "us_auto": res[0], "us_streamk": res[8],
+        rel = {v: float((outs[0] - outs[v]).norm() / outs[0].norm()) for v in VARIANTS}
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": Kd, "us": {f"v{v}": res[v] for v in VARIANTS},
                           "rel_diff": rel}), flush=True)
 
 
