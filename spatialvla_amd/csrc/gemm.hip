@@ -1802,7 +1802,8 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   };
   auto direct_epilogue = [&](int64_t m0, int64_t n0, int lane) -> bool {
     const int kind = E.kind;
-    if (!(kind == SVLA_EPI_STORE || (GG && kind == SVLA_EPI_GEGLU))) return false;
+    if (!(kind == SVLA_EPI_STORE || (GG && (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE)))) return false;
+    if (GG && kind == SVLA_EPI_STORE) return false;  // the paired kernel runs GEGLU and head-256 ROPE only
     if (m0 + BM > M || n0 + BN > N) return false;
     int cs = 0;
 #pragma unroll
@@ -1818,6 +1819,51 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       lds_barrier();
     }
     if constexpr (GG) {
+     if (kind == SVLA_EPI_ROPE) {
+      // head_dim 256, one head per tile: quads (i, 2p) hold the low half (d < 128) and (i, 2p + 1) the high half of
+      // the same d, so rotate_half pairs meet in one lane.  epi_pass_fast<ROPE>'s rounding: x = bf16(acc),
+      // out = bf16(bf16(x cos) + bf16(rotate_half(x) sin)); columns beyond rope_cols (v) are stored as they are.
+      const bool rot = n0 < E.rope_cols;
+      const int dl0 = 64 * wc + cofs;  // d of the lane's low-half chunk (pair P adds 32)
+      const bf16_t* const ctab = (const bf16_t*)E.rope_cos + dl0;
+      const bf16_t* const stab = (const bf16_t*)E.rope_sin + dl0;
+      static_for<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        const int64_t m = m0 + 128 * wr + 16 * i + r;
+        const int64_t pos = m % E.rope_L;
+        u32x4 c4[2], s4[2];
+        if (rot) {
+#pragma unroll
+          for (int P_ = 0; P_ < 2; ++P_) {
+            c4[P_] = *reinterpret_cast<const u32x4*>(ctab + pos * E.rope_ld + 32 * P_);
+            s4[P_] = *reinterpret_cast<const u32x4*>(stab + pos * E.rope_ld + 32 * P_);
+          }
+        }
+        static_for<0, 2>([&](auto P) {
+          constexpr int P_ = decltype(P)::value;
+          f32x4 la = agpr_get<i * 8 + 4 * P_>(), ha = agpr_get<i * 8 + 4 * P_ + 1>();
+          f32x4 lb = agpr_get<i * 8 + 4 * P_ + 2>(), hb = agpr_get<i * 8 + 4 * P_ + 3>();
+          swap4(la, lb);
+          swap4(ha, hb);
+          float lo[8] = {la[0], la[1], la[2], la[3], lb[0], lb[1], lb[2], lb[3]};
+          float hi[8] = {ha[0], ha[1], ha[2], ha[3], hb[0], hb[1], hb[2], hb[3]};
+          if (rot) {
+            float cf[8], sf[8];
+            unpack8(c4[P_], cf);
+            unpack8(s4[P_], sf);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const float xl = round_bf(lo[q]), xh = round_bf(hi[q]);
+              lo[q] = round_bf(xl * cf[q]) + round_bf(-xh * sf[q]);
+              hi[q] = round_bf(xh * cf[q]) + round_bf(xl * sf[q]);
+            }
+          }
+          bf16_t* const p = cbase + (m - cm0) * Cd.ld + n0 + dl0 + 32 * P_;
+          *reinterpret_cast<u32x4*>(p) = pack8(lo);
+          *reinterpret_cast<u32x4*>(p + 128) = pack8(hi);
+        });
+      });
+     } else {
       const int64_t ncol = (n0 >> 1) + 64 * wc + cofs;
       static_for<0, 8>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -1844,6 +1890,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           *reinterpret_cast<u32x4*>((bf16_t*)E.out2 + m * E.ld_out2 + n) = pack8(uv);
         });
       });
+     }
     } else {
       // one row chunk: v = 8 consecutive fp32 columns n .. n+7 of row m (reference rounding points of epi_pass_fast)
       const float alpha = E.alpha;
@@ -2862,7 +2909,9 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     return svla::check_launch("gemm4 fp8");
   }
   const int la = A.layout, lb = B.layout;
-  if (E.kind == SVLA_EPI_GEGLU) {  // B is two KC GEGLU segments (checked by the dispatcher)
+  // GeGLU (B: two KC GEGLU segments, checked by the dispatcher) and head_dim-256 RoPE (q|k|v): the paired kernel
+  if (E.kind == SVLA_EPI_GEGLU ||
+      (E.kind == SVLA_EPI_ROPE && E.rope_D == 256 && la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC)) {
     static bool lds_set = false;
     if (!lds_set) {
       (void)hipFuncSetAttribute((const void*)gemm4_kernel_00g, hipFuncAttributeMaxDynamicSharedMemorySize, p4::LDS);
@@ -3104,18 +3153,18 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
     }
   }
   const int64_t t256 = tiles(256, 256);
-  // ROPE's fast-path epilogue (cos/sin prefetched a row ahead) runs as well on the 4-wave kernel: q|k|v 233 -> 225 us
-  // (tools/gemm_epi_bench.py, bitwise equal)
   // The 4-wave kernel's direct epilogue (stores straight from the accumulators, gemm4_body) made it the faster kernel
   // for the light epilogues from one k-tile loop of 512 up and from a quarter wave of tiles (tools/gemm_bench.py:
-  // o fwd 129 -> 106 us, down dgrad 422 -> 354 us, SigLIP qkv BIAS 89 -> 82 us; ROPE keeps its LDS epilogue there,
-  // bitwise the 8-phase kernel's, 0.99x).  VALU-heavy or load-carrying epilogues stay on the 8-phase kernel, whose
+  // o fwd 129 -> 106 us, down dgrad 422 -> 354 us, SigLIP qkv BIAS 89 -> 82 us; head_dim-256 ROPE
+  // rotates in registers on the paired-fragment kernel, bitwise the 8-phase kernel's).  VALU-heavy or load-carrying epilogues stay on the 8-phase kernel, whose
   // two waves per SIMD run them faster than one wave does from registers (tools/epi_ab.py, tools/gemm_epi_bench.py:
   // SOFTCAP_CE 13.4 vs 16.4 ms, BIAS_GELU_ERF 270 vs 312 us, GELU_BWD 178 vs 224 us, BIAS_RESID 127 vs 138 us).
+  // The k-loop floor is 384: the lm_head weight gradient (265344 x 2304 x 416) runs 0.70 ms here vs 0.85 ms on the
+  // 8-phase kernel (tools/gemm_probe.py); head_dim-256 RoPE stores from the paired accumulators (qkv 0.23 -> 0.19 ms).
   const int ek = epi->kind;
   const bool light_epi = ek == SVLA_EPI_STORE || ek == SVLA_EPI_BIAS || ek == SVLA_EPI_GEGLU || ek == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
-                    (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 512 && 4 * t256 >= num_cus()));
+                    (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 384 && 4 * t256 >= num_cus()));
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
     if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);

@@ -887,3 +887,39 @@ def test_gemm_tiny_tiles(cuda, M, N, K, layouts):
     assert rel_l2(c[:, :N], ref) < 5e-3 and bool((c[:, N:] == 7.0).all())
     assert rel_l2(cb[:, :N], ref + bias.float() + res.float()) < 5e-3
     assert rel_l2(c[:, :N], outs[1][0][:, :N]) < 2e-3
+
+
+@pytest.mark.parametrize("M", [600, 1024])
+def test_gemm4_rope_paired_bitwise(cuda, M):
+    """head_dim-256 RoPE on the paired-fragment 4-wave kernel (direct epilogue on interior tiles, LDS image on the
+    ragged rows of M=600) == the 8-phase kernel's RoPE epilogue, bit for bit (q 8 heads | k 4 heads rotated, v not)."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(61)
+    Kd, L_ = 512, 300
+    x = _r(M, Kd)
+    ws = [_r(2048, Kd, scale=0.05), _r(1024, Kd, scale=0.05), _r(1024, Kd, scale=0.05)]
+    pos = torch.arange(1, L_ + 1, device=cuda).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, 256, 2, device=cuda).float() / 256))
+    fr = pos[:, None] * inv[None]
+    cos = torch.cat([fr.cos(), fr.cos()], -1).to(BF).contiguous()
+    sin = torch.cat([fr.sin(), fr.sin()], -1).to(BF).contiguous()
+    outs = {}
+    for v in (3, 4):
+        o = torch.empty(M, 4096, dtype=BF, device=cuda)
+        try:
+            Kn.gemm_variant = v
+            Kn.linear_fwd(x, ws, o, kind=L.EPI_ROPE, rope=(cos, sin, L_, 256, 3072))
+        finally:
+            Kn.gemm_variant = 0
+        outs[v] = o
+    assert torch.equal(outs[3], outs[4])
+    # against eager bf16 RoPE (rotate_half) on the bf16 projection
+    y = (x.float() @ torch.cat(ws).float().T).to(BF).float()
+    p = torch.arange(M, device=cuda) % L_
+    c, s = cos.float()[p], sin.float()[p]
+    ref = y.clone()
+    for h in range(12):
+        seg = y[:, 256 * h:256 * (h + 1)]
+        rot = torch.cat([-seg[:, 128:], seg[:, :128]], -1)
+        ref[:, 256 * h:256 * (h + 1)] = (seg * c).to(BF).float() + (rot * s).to(BF).float()
+    assert rel_l2(outs[3], ref) < 5e-3
