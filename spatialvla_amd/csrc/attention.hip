@@ -26,6 +26,15 @@
 #ifndef SVLA_ATT_QW
 #define SVLA_ATT_QW 2  // query sub-tiles per wave of the forward at head_dim 64 / 72 (variant builds: 1)
 #endif
+#ifndef SVLA_ATT_RS64
+#define SVLA_ATT_RS64 0  // head_dim 64 (BEiT) tiles with 128-B rows (16 KB K+V stages, 32 KB per block) instead of 256-B
+#endif
+#ifndef SVLA_ATT_WPE64
+#define SVLA_ATT_WPE64 3  // head_dim 64 forward with SVLA_ATT_RS64: waves per SIMD the registers are sized for
+#endif
+#ifndef SVLA_ATT_BPF
+#define SVLA_ATT_BPF 1  // key tiles of score bias (BEiT) in flight ahead of the tile being scored: 1 or 2
+#endif
 #ifndef SVLA_ATT_QW256
 #define SVLA_ATT_QW256 1  // head_dim 256 forward: 1 = head pairs (NH 2), 16 queries per wave; 2 = one head, 32 per wave
 #endif
@@ -37,12 +46,19 @@ constexpr float MASKVAL = -3.3895313892515355e38f;  // torch.finfo(bfloat16).min
 template <int D> struct Cfg;
 template <> struct Cfg<256> { static constexpr int DP = 256, DV = 256, RS = 256; };
 template <> struct Cfg<72>  { static constexpr int DP = 96,  DV = 80,  RS = 128; };
-template <> struct Cfg<64>  { static constexpr int DP = 64,  DV = 64,  RS = 128; };  // BEiT (ZoeDepth backbone)
+template <> struct Cfg<64>  { static constexpr int DP = 64,  DV = 64,  RS = SVLA_ATT_RS64 ? 64 : 128; };  // BEiT (ZoeDepth)
 
+// chunk swizzle of row r: 2(r & 7) for 256-B and wider rows, r & 7 for the 128-B rows of head_dim 64 (8 chunks);
+// both conflict-free for the ds_read_b128 row reads and the ds_read_b64_tr_b16 transposed reads, and periodic in 8
+// rows (TrFrag reads rows r and r + 16 with one swizzle)
+template <int RS>
+__device__ __forceinline__ int swz(int r) {
+  return RS == 64 ? (r & 7) : ((r & 7) << 1);
+}
 // byte offset of 16-B chunk `ch` of row `r` in a [64][RS] bf16 LDS tile
 template <int RS>
 __device__ __forceinline__ int toff(int r, int ch) {
-  return r * RS * 2 + ((ch ^ ((r & 7) << 1)) << 4);
+  return r * RS * 2 + ((ch ^ swz<RS>(r)) << 4);
 }
 
 // fragment of 16 rows (r0..r0+15) x 8 consecutive columns (32ks + 8g ..) : ds_read_b128
@@ -92,7 +108,7 @@ __device__ __forceinline__ void glds_tile(char* lds, const bf16_t* base, int64_t
   for (int i = 0; i < NI / NW; ++i) {
     const int j = w + NW * i;
     const int r = j * RPI + lane / CPR;
-    const int ch = (lane % CPR) ^ ((r & 7) << 1);
+    const int ch = (lane % CPR) ^ swz<RS>(r);
     const uint32_t voff = (r < nrows && ch * 8 < D) ? (uint32_t)(r * ld * 2 + ch * 16) : SVLA_OOB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(lds + j * 1024), 16, voff, 0, 0, 0);
   }
@@ -269,7 +285,7 @@ __device__ __forceinline__ void mfma_tr_sweep_q(f32x4 (&acc)[QW][NDT], const cha
 }
 
 template <int D, int NH, bool CAP, bool BIAS = false, int QW = 1>
-__global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
+__global__ __launch_bounds__(256 * NH, (D == 64 && SVLA_ATT_RS64) ? SVLA_ATT_WPE64 : 1) void attn_fwd_kernel(svla_attn_args a, bf16_t* __restrict__ out,
                                                                int64_t ldo, float* __restrict__ lse) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
   constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH, QT = 64 * QW;
@@ -306,22 +322,25 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   glds_tile<RS, 64, NW>(smem + TB, vbase, a.ldv, L, D, w, lane);
   // BIAS: this lane's bias rows (its queries) are read one key tile ahead into registers (keys 16nt + 4g .. +3 of
   // the tile; 8 B per nt, zero beyond the padded row): the loads of tile kt+1 are in flight during tile kt
+  // (SVLA_ATT_BPF = 2: two tiles ahead, in a ring of two register sets)
   const bf16_t* brow[QW];
-  u32x2 bnext[QW][4];
-  auto bias_fetch = [&](int kt_) {
+  u32x2 bnext[SVLA_ATT_BPF][QW][4];
+  auto bias_fetch = [&](int kt_, auto bslot) {
+    constexpr int BS = decltype(bslot)::value;
 #pragma unroll
     for (int u = 0; u < QW; ++u)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int k = kt_ * 64 + 16 * nt + 4 * g;
-        bnext[u][nt] = k < a.bias_ld ? *reinterpret_cast<const u32x2*>(brow[u] + k) : u32x2{0u, 0u};
+        bnext[BS][u][nt] = k < a.bias_ld ? *reinterpret_cast<const u32x2*>(brow[u] + k) : u32x2{0u, 0u};
       }
   };
   if constexpr (BIAS) {
 #pragma unroll
     for (int u = 0; u < QW; ++u)
       brow[u] = (const bf16_t*)a.bias + ((int64_t)h * L + (qvalid[u] ? qi[u] : 0)) * a.bias_ld;
-    bias_fetch(0);
+    bias_fetch(0, std::integral_constant<int, 0>{});
+    if constexpr (SVLA_ATT_BPF == 2) bias_fetch(1, std::integral_constant<int, 1>{});
   }
 
   f32x4 acc[QW][NDT];
@@ -336,8 +355,12 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
   const float LOG2E = 1.4426950408889634f;
   const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
 
-  for (int kt = 0; kt < nkt; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // one key tile; SL = kt % SVLA_ATT_BPF as a constant (the bias register ring is indexed statically)
+  auto tile = [&](const int kt, auto slot) {
+    constexpr int SL = decltype(slot)::value;
+    // tile kt landed (and, BIAS with BPF 2, the bias of tile kt: only the QW*4 loads of tile kt+1 may stay in flight)
+    if (BIAS && SVLA_ATT_BPF == 2 && kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QW * 4) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile kt landed for every wave; every wave is done with the stage refilled below
     const char* ldsK = smem + (kt & 1) * STAGE;
     const char* ldsV = ldsK + TB;
@@ -378,11 +401,11 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
       for (int u = 0; u < QW; ++u)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const u32x2 w2 = bnext[u][nt];
+          const u32x2 w2 = bnext[SL][u][nt];
           bb[u][nt][0] = __uint_as_float(w2[0] << 16); bb[u][nt][1] = __uint_as_float(w2[0] & 0xffff0000u);
           bb[u][nt][2] = __uint_as_float(w2[1] << 16); bb[u][nt][3] = __uint_as_float(w2[1] & 0xffff0000u);
         }
-      if (kt + 1 < nkt) bias_fetch(kt + 1);
+      if (kt + SVLA_ATT_BPF < nkt) bias_fetch(kt + SVLA_ATT_BPF, slot);
     }
     bf16x8 pb[2][QW];  // P of key halves 0 / 1 (the B operands of the PV products)
 #pragma unroll
@@ -447,6 +470,11 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_fwd_kernel(svla_attn_args a,
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) mfma_tr_sweep_q<RS, NDT, QW>(acc, ldsV, 32 * ks, pb[ks], lane);
+  };
+  for (int kt = 0; kt < nkt; kt += SVLA_ATT_BPF) {
+    tile(kt, std::integral_constant<int, 0>{});
+    if constexpr (SVLA_ATT_BPF == 2)
+      if (kt + 1 < nkt) tile(kt + 1, std::integral_constant<int, SVLA_ATT_BPF - 1>{});
   }
   // O^T accumulators (d = 16dt + 4g + j, q = lane col) -> per-wave LDS image [QW*16 q][DV + 16] -> 16-B stores.
   // The 16-element row pad puts the 16 query rows of one 8-B store 32 B apart (an unpadded DV = 256 row stride
