@@ -27,13 +27,16 @@
 #define SVLA_ATT_QW 2  // query sub-tiles per wave of the forward at head_dim 64 / 72 (variant builds: 1)
 #endif
 #ifndef SVLA_ATT_RS64
-#define SVLA_ATT_RS64 0  // head_dim 64 (BEiT) tiles with 128-B rows (16 KB K+V stages, 32 KB per block) instead of 256-B
+#define SVLA_ATT_RS64 1  // head_dim 64 (BEiT) tiles with 128-B rows (16 KB K+V stages, 32 KB per block) instead of 256-B:
+                         // BEiT B=32 forward 157.5 -> 137.6 us with bias, 123 -> 86 us without (bitwise equal outputs;
+                         // tools/beit_attn_probe.py, profiles/r3o_beit_attn_ab.txt)
 #endif
 #ifndef SVLA_ATT_WPE64
-#define SVLA_ATT_WPE64 3  // head_dim 64 forward with SVLA_ATT_RS64: waves per SIMD the registers are sized for
+#define SVLA_ATT_WPE64 2  // head_dim 64 forward with SVLA_ATT_RS64: waves per SIMD the registers are sized for (3: spills
+                          // 12 VGPRs, 165 us)
 #endif
 #ifndef SVLA_ATT_BPF
-#define SVLA_ATT_BPF 1  // key tiles of score bias (BEiT) in flight ahead of the tile being scored: 1 or 2
+#define SVLA_ATT_BPF 1  // key tiles of score bias (BEiT) in flight ahead of the tile being scored: 1 or 2 (2: 245-261 us)
 #endif
 #ifndef SVLA_ATT_QW256
 #define SVLA_ATT_QW256 1  // head_dim 256 forward: 1 = head pairs (NH 2), 16 queries per wave; 2 = one head, 32 per wave
