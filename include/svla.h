@@ -246,15 +246,21 @@ int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* 
                           float eps1, float eps2, void* h, void* x, void* stream);
 int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
                        void* y, float* mean, float* rstd, void* stream);
-/* dwb_partial: two planes [2][ceil(rows/rows_per_block)][N] fp32 (dw partials, then db partials), each reduced by
- * svla_colsum_f32. */
+/* dwb_partial: two planes [2][ceil(rows/rows_per_block)][N] fp32 (dw partials, then db partials), reduced by
+ * svla_colsum2_f32. */
 int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, const float* mean,
                        const float* rstd, const void* dy, const void* dres, void* dx, float* dwb_partial,
                        int64_t* n_partial, void* stream);
-/* out[n] = bf16(sum_p in[p, n]) (+ existing out if accumulate): reduces partial sums. */
+/* out[n] = bf16(sum_p in[p, n]) (+ existing out if accumulate): reduces partial sums in one launch, fixed order
+ * (the weight-gradient reduction autograd does for Gemma2RMSNorm.weight / nn.LayerNorm, modeling_gemma2.py:60-77).
+ * N % 8 == 0; workspace unused (may be NULL). */
 int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate, float* workspace,
                     void* stream);
-/* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients). workspace >= 64*N fp32 */
+/* The two planes [2][P][N] of svla_layernorm_bwd in one launch: out0 = bf16(sum_p in[0][p]), out1 = plane 1. */
+int svla_colsum2_f32(int64_t P, int64_t N, const float* in, void* out0_bf16, void* out1_bf16, int32_t accumulate,
+                     void* stream);
+/* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients of nn.Linear), one launch, fixed order.
+ * N % 8 == 0, ldx % 8 == 0; workspace unused (may be NULL). */
 int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16, int32_t accumulate,
                      float* workspace, void* stream);
 

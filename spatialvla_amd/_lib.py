@@ -97,6 +97,7 @@ SIGNATURES = {
     "svla_layernorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    ctypes.POINTER(c_i64), c_vp]),
     "svla_colsum_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "svla_colsum2_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "svla_colsum_bf16": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "svla_embed_merge": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     "svla_embed_merge_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp]),

@@ -99,7 +99,7 @@ __device__ __forceinline__ void rope_pair_t(float& lo, float& hi, float c, float
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA staging of a [ROWS][RS] tile (rows row0.. of a (b, ·, head) slice, D valid columns) into the
 // swizzled image toff<RS>: wave-instruction j writes 1 KiB lane-linearly (RPI = 512/RS rows); lane l lands at
-// row j*RPI + l/CPR, image chunk p = l%CPR, which holds global chunk p ^ 2*(row&7).  Rows >= nrows and
+// row j*RPI + l/CPR, image chunk p = l%CPR, which holds global chunk p ^ swz<RS>(row).  Rows >= nrows and
 // columns >= D read as zero (descriptor range check).
 template <int RS, int ROWS, int NW>
 __device__ __forceinline__ void glds_tile(char* lds, const bf16_t* base, int64_t ld, int nrows, int D, int w,

@@ -3,8 +3,8 @@
 //
 // One 256-thread block per row; each thread owns up to MAXC 16-B chunks (8 bf16) of the row in
 // registers, so x is read from HBM exactly once per pass.  Weight-gradient partial sums are
-// written per block (RPB rows) in fp32 and reduced in a fixed order by svla_colsum_f32 —
-// no atomics, bitwise reproducible.
+// written per block (RPB rows) in fp32 and reduced in a fixed order by svla_colsum_f32 / svla_colsum2_f32
+// (one launch) — no atomics, bitwise reproducible.
 #include "svla_common.h"
 
 namespace {
@@ -493,38 +493,73 @@ __global__ __launch_bounds__(NTH) void ln_bwd_kernel(int64_t rows, int64_t N, co
 }
 
 // ------------------------------------------------------------------ column reductions
-// Deterministic column sums: a block owns 64 columns; its 256 threads are 4 row-groups of 64 lanes
-// (coalesced 256-B row segments), each summing a strided subset of its row range; the 4 partials are
-// combined in a fixed order through LDS.  grid.y splits the rows into independent partial rows.
-template <typename T>
-__device__ __forceinline__ float ldf(const T* p);
-template <>
-__device__ __forceinline__ float ldf<float>(const float* p) { return *p; }
-template <>
-__device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p) { return bf2f(*p); }
-
-template <typename T, bool FINAL>
-__global__ __launch_bounds__(256) void colsum_kernel(int64_t P, int64_t N, const T* __restrict__ in, int64_t ld,
-                                                     float* __restrict__ part, bf16_t* __restrict__ out, int acc) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, sg = threadIdx.x >> 6;
-  const int64_t n = (int64_t)blockIdx.x * 64 + cl;
-  const int64_t per = (P + gridDim.y - 1) / gridDim.y;
-  const int64_t p0 = (int64_t)blockIdx.y * per, p1 = min(P, p0 + per);
-  float s = 0.f;
-  if (n < N)
-    for (int64_t p = p0 + sg; p < p1; p += 4) s += ldf<T>(in + p * ld + n);
-  red[sg][cl] = s;
-  __syncthreads();
-  if (sg == 0 && n < N) {
-    float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
-    if (FINAL) {
-      if (acc) t += bf2f(out[n]);
-      out[n] = f2bf(t);
+// Single-pass deterministic column sums (round 4: replaces the two colsum_kernel passes, 768 launches a step).  A
+// block owns CB columns of every one of the P rows: its 256 threads are CB/8 column lanes (8 consecutive columns,
+// one 16-B bf16 or two 16-B fp32 loads per row) x RG = 2048/CB row groups; group g sums rows g, g+RG, .. in
+// increasing order in fp32 registers, four rows in flight, then one thread per column adds the RG group sums in
+// group order from LDS.  grid.y = planes (plane y reads in + y * plane_stride, writes out_y), so the dw and db
+// planes of the LayerNorm backward reduce in one launch.  Fixed assignment and order: bitwise reproducible.
+template <typename T, int CB>
+__global__ __launch_bounds__(256) void colsum1_kernel(int64_t P, int64_t N, const T* __restrict__ in, int64_t ld,
+                                                      int64_t plane_stride, bf16_t* __restrict__ out0,
+                                                      bf16_t* __restrict__ out1, int acc) {
+  constexpr int CL = CB / 8, RG = 256 / CL;
+  __shared__ float red[RG][CB + 1];
+  const int cl = threadIdx.x % CL, rg = threadIdx.x / CL;
+  const int64_t n0 = (int64_t)blockIdx.x * CB + cl * 8;
+  const T* src = in + (int64_t)blockIdx.y * plane_stride + n0;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  auto add_row = [&](int64_t p) {
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      unpack8(*reinterpret_cast<const u32x4*>(src + p * ld), v);
     } else {
-      part[(int64_t)blockIdx.y * N + n] = t;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(src + p * ld);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(src + p * ld + 4);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+      v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += v[j];
+  };
+  if (n0 < N) {
+    int64_t p = rg;
+    for (; p + 3 * RG < P; p += 4 * RG) {  // four independent row loads in flight, summed in row order
+      add_row(p);
+      add_row(p + RG);
+      add_row(p + 2 * RG);
+      add_row(p + 3 * RG);
+    }
+    for (; p < P; p += RG) add_row(p);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][cl * 8 + j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < CB) {
+    const int64_t n = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (n < N) {
+      float t = 0.f;
+      for (int q = 0; q < RG; ++q) t += red[q][threadIdx.x];
+      bf16_t* o = blockIdx.y ? out1 : out0;
+      if (acc) t += bf2f(o[n]);
+      o[n] = f2bf(t);
     }
   }
+}
+
+template <typename T>
+int launch_colsum1(int64_t P, int64_t N, const T* in, int64_t ld, int64_t plane_stride, int planes, bf16_t* out0,
+                   bf16_t* out1, int acc, hipStream_t s) {
+  // 32 columns a block when that still gives >= 64 blocks, else 16 (more blocks, shorter row segments)
+  if ((N + 31) / 32 * planes >= 64)
+    hipLaunchKernelGGL((colsum1_kernel<T, 32>), dim3((unsigned)((N + 31) / 32), (unsigned)planes), dim3(256), 0, s, P,
+                       N, in, ld, plane_stride, out0, out1, acc);
+  else
+    hipLaunchKernelGGL((colsum1_kernel<T, 16>), dim3((unsigned)((N + 15) / 16), (unsigned)planes), dim3(256), 0, s, P,
+                       N, in, ld, plane_stride, out0, out1, acc);
+  return svla::check_launch("colsum");
 }
 
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -608,29 +643,25 @@ extern "C" int svla_layernorm_bwd(int64_t rows, int64_t N, const void* x, const 
 
 extern "C" int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32_t accumulate,
                                float* workspace, void* stream) {
-  SVLA_CHECK_ARG(P > 0 && N > 0 && in && out_bf16, "colsum_f32: bad args");
-  hipStream_t s = (hipStream_t)stream;
-  if (workspace && P > 64) {  // two fixed-order passes: P rows -> 64 partial rows -> out
-    const unsigned parts = 64;
-    hipLaunchKernelGGL((colsum_kernel<float, false>), dim3((unsigned)((N + 63) / 64), parts), dim3(256), 0, s, P, N,
-                       in, N, workspace, (bf16_t*)nullptr, 0);
-    if (int rc = svla::check_launch("colsum_f32")) return rc;
-    in = workspace;
-    P = parts;
-  }
-  hipLaunchKernelGGL((colsum_kernel<float, true>), dim3((unsigned)((N + 63) / 64), 1), dim3(256), 0, s, P, N, in, N,
-                     (float*)nullptr, (bf16_t*)out_bf16, accumulate);
-  return svla::check_launch("colsum_f32");
+  (void)workspace;  // single pass since round 4; kept in the ABI
+  SVLA_CHECK_ARG(P > 0 && N > 0 && N % 8 == 0 && in && out_bf16 && al16(in), "colsum_f32: bad args");
+  return launch_colsum1<float>(P, N, in, N, 0, 1, (bf16_t*)out_bf16, nullptr, accumulate, (hipStream_t)stream);
+}
+
+extern "C" int svla_colsum2_f32(int64_t P, int64_t N, const float* in, void* out0_bf16, void* out1_bf16,
+                                int32_t accumulate, void* stream) {
+  SVLA_CHECK_ARG(P > 0 && N > 0 && N % 8 == 0 && in && out0_bf16 && out1_bf16 && al16(in), "colsum2_f32: bad args");
+  return launch_colsum1<float>(P, N, in, N, P * N, 2, (bf16_t*)out0_bf16, (bf16_t*)out1_bf16, accumulate,
+                               (hipStream_t)stream);
 }
 
 extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16,
                                 int32_t accumulate, float* workspace, void* stream) {
-  SVLA_CHECK_ARG(M > 0 && N > 0 && x && out_bf16 && workspace && ldx >= N, "colsum_bf16: bad args");
-  const unsigned parts = (unsigned)((M + 63) / 64 < 64 ? (M + 63) / 64 : 64);
-  hipLaunchKernelGGL((colsum_kernel<bf16_t, false>), dim3((unsigned)((N + 63) / 64), parts), dim3(256), 0,
-                     (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, workspace, (bf16_t*)nullptr, 0);
-  if (int rc = svla::check_launch("colsum_bf16")) return rc;
-  return svla_colsum_f32(parts, N, workspace, out_bf16, accumulate, nullptr, stream);
+  (void)workspace;  // single pass since round 4; kept in the ABI
+  SVLA_CHECK_ARG(M > 0 && N > 0 && N % 8 == 0 && x && out_bf16 && ldx >= N && ldx % 8 == 0 && al16(x),
+                 "colsum_bf16: bad args");
+  return launch_colsum1<bf16_t>(M, N, (const bf16_t*)x, ldx, 0, 1, (bf16_t*)out_bf16, nullptr, accumulate,
+                                (hipStream_t)stream);
 }
 
 extern "C" int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,

@@ -321,10 +321,6 @@ class GemmaAttentionFn(torch.autograd.Function):
         M, H = x.shape
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
-        if cos.shape[0] != cfg.L and torch.is_grad_enabled() and x.requires_grad:
-            # the attention backward applies the RoPE transpose with table row = position in the sequence
-            raise NotImplementedError("per-sequence position_ids are an inference path (the reference's training "
-                                      "positions are shared: modeling_spatialvla.py:367-372)")
         rope = (cos, sin, cos.shape[0], cfg.D, qd + kd)
         if f8 is not None:
             _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, kind=L.EPI_ROPE, rope=rope)
@@ -351,6 +347,9 @@ class GemmaAttentionFn(torch.autograd.Function):
     def backward(ctx, dout):
         x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class = ctx.saved_tensors
         cfg = ctx.cfg
+        if cos.shape[0] != cfg.L:  # Gemma2Attention.forward refuses this case up front (check_rope_for_grad)
+            raise NotImplementedError("GemmaAttentionFn.backward: per-sequence RoPE tables (the backward's RoPE "
+                                      "transpose reads table row = position in the sequence)")
         dout = _c(dout)
         M = x.shape[0]
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
@@ -615,9 +614,20 @@ class SiglipAttentionFn(torch.autograd.Function):
             for i, (dw, accw, _r) in enumerate(dws):
                 if dw is not None:
                     K.linear_wgrad(_c(dqkv[:, i * Hd:(i + 1) * Hd]), x, [dw], accumulate=accw)
-        for i, b in enumerate((bq, bk, bv)):
-            retb = _bias_grad(dqkv[:, i * Hd:(i + 1) * Hd], b, nig[3 + 2 * i])  # strided view, no copy
-            rets += [dws[i][2], retb]
+        bds = [_grad_dest(b, nig[3 + 2 * i]) for i, b in enumerate((bq, bk, bv))]
+        cat = None
+        if all(d[0] is not None for d in bds) and len({d[1] for d in bds}) == 1:
+            cat = _cat_views([d[0] for d in bds])
+            if cat.data_ptr() != bds[0][0].data_ptr():  # not back to back (no engine flat buffer): a copy, unusable
+                cat = None
+        if cat is not None:  # the q|k|v bias gradients in one column sum over dqkv (engine: adjacent in the flat grad)
+            K.colsum_bf16(dqkv, cat, accumulate=bds[0][1])
+        else:
+            for i, (db, accb, _r) in enumerate(bds):
+                if db is not None:
+                    K.colsum_bf16(dqkv[:, i * Hd:(i + 1) * Hd], db, accumulate=accb)  # strided view, no copy
+        for i in range(3):
+            rets += [dws[i][2], bds[i][2]]
         dres = dout
         if ctx.slot is not None:  # handed to layer_norm1's backward (ResidualSlot)
             ctx.slot.put(dout)

@@ -175,11 +175,15 @@ def linear_fwd(x: torch.Tensor, weights: List[torch.Tensor], out: torch.Tensor, 
               colscale=colscale))
 
 
+GEMV_NORM_MAX_K = 2560  # svla_gemv_rmsnorm2 holds a row of up to this many features in registers (gemm.hip)
+
+
 def gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, weights: List[torch.Tensor], out: torch.Tensor, geglu_out=None):
     """Decode step: h_out = bf16(res + rms(y; w1)), x = rms(h_out; w2) (svla_add_rmsnorm2_fwd, bitwise), then
     out = x @ cat(weights)^T (STORE), or with geglu_out = (g, u) and weights = [w_gate, w_up]: out = GeGLU of the
     gate|up projection (svla_gemv_rmsnorm2, M <= 8 rows)."""
     M, Kd = y.shape
+    _req(Kd <= GEMV_NORM_MAX_K and Kd % 8 == 0, f"gemv_rmsnorm2: K {Kd} must be a multiple of 8 <= {GEMV_NORM_MAX_K}")
     for t, nm in ((res, "res"), (y, "y"), (h_out, "h_out"), (w1, "w1"), (w2, "w2"), (out, "out")):
         _chk_bf16(t, "gemv_rmsnorm2 " + nm)
     _req(res.shape == y.shape == h_out.shape and _ld(res) == _ld(y) == _ld(h_out), "gemv_rmsnorm2: res/y/h_out rows")
@@ -399,26 +403,30 @@ def layernorm_bwd(x, w, mean, rstd, dy, dres, dx, dw_out, db_out, accumulate=Fal
     L.check(L.lib().svla_layernorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                        dy.data_ptr(), _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart),
                                        _stream()), "layernorm_bwd")
-    # partial planes [2][nb][N]: dw, then db, each reduced in place
-    if dw_out is not None:
+    # partial planes [2][nb][N]: dw, then db -- both reduced by one launch when both are wanted
+    if dw_out is not None and db_out is not None:
+        L.check(L.lib().svla_colsum2_f32(npart.value, N, part.data_ptr(), dw_out.data_ptr(), db_out.data_ptr(),
+                                         int(accumulate), _stream()), "colsum2_f32")
+    elif dw_out is not None:
         colsum_f32(part[0], dw_out, accumulate)
-    if db_out is not None:
+    elif db_out is not None:
         colsum_f32(part[1], db_out, accumulate)
 
 
 def colsum_f32(part, out, accumulate=False):
-    """out[n] = bf16(sum_p part[p, n]) (+ out), two fixed-order passes when P > 64."""
+    """out[n] = bf16(sum_p part[p, n]) (+ out), one launch, fixed order."""
     P, N = part.shape
-    ws = torch.empty(64, N, dtype=torch.float32, device=part.device) if P > 64 else None
-    L.check(L.lib().svla_colsum_f32(P, N, part.data_ptr(), out.data_ptr(), int(accumulate), _ptr(ws), _stream()),
+    _req(part.is_contiguous() and out.numel() == N, "colsum_f32: contiguous [P, N] partials, [N] output")
+    L.check(L.lib().svla_colsum_f32(P, N, part.data_ptr(), out.data_ptr(), int(accumulate), None, _stream()),
             "colsum_f32")
 
 
 def colsum_bf16(x, out, accumulate=False):
+    """out[n] = bf16(sum_m x[m, n]) (+ out) over a row-strided bf16 matrix (bias gradients), one launch."""
     M, N = x.shape
-    ws = torch.empty(64, N, dtype=torch.float32, device=x.device)
-    L.check(L.lib().svla_colsum_bf16(M, N, x.data_ptr(), _ld(x), out.data_ptr(), int(accumulate), ws.data_ptr(),
-                                     _stream()), "colsum_bf16")
+    _req(out.numel() == N and out.is_contiguous(), "colsum_bf16: [N] contiguous output")
+    L.check(L.lib().svla_colsum_bf16(M, N, x.data_ptr(), _ld(x), out.data_ptr(), int(accumulate), None, _stream()),
+            "colsum_bf16")
 
 
 # ---------------------------------------------------------------------------------------- attention

@@ -200,6 +200,13 @@ class Gemma2Attention(nn.Module):
                                             self.v_proj.weight, self.o_proj.weight, cos, sin, cache.key_cache[i],
                                             cache.value_cache[i], cache.kv_class, cache.seen_tokens, cfg)
             return out.view(B, Lq, H)
+        if cos.shape[0] != Lq and torch.is_grad_enabled() and (
+                hidden_states.requires_grad or any(w.requires_grad for w in (self.q_proj.weight, self.k_proj.weight))):
+            # autograd.Function.forward runs with grad mode off, so this is checked here, where the caller's grad
+            # mode is visible: the attention backward applies the RoPE transpose with table row = position in the
+            # sequence, which per-sequence tables ([B*L] rows, padded prompts) would not match
+            raise NotImplementedError("per-sequence position_ids are an inference path (the reference's training "
+                                      "positions are shared: modeling_spatialvla.py:367-372); run under no_grad")
         capture = {} if attn_sink is not None else None
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
@@ -262,6 +269,8 @@ class Gemma2Model(nn.Module):
         self.embed_tokens = nn.Embedding(config.vocab_size, config.hidden_size, self.padding_idx)
         self.layers = nn.ModuleList([Gemma2DecoderLayer(config, i) for i in range(config.num_hidden_layers)])
         self.norm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
+        # reference :669 / :752-762; accepted and recorded, never recomputes (Gemma2ForCausalLM._set_gradient_checkpointing)
+        self.gradient_checkpointing = False
 
     def get_input_embeddings(self):
         return self.embed_tokens
@@ -320,6 +329,7 @@ class Gemma2Model(nn.Module):
         H = shp[-1]
         res = hidden.reshape(-1, H).contiguous()
         if (Fn.DECODE_NORM_FUSED[0] and cache.seen_tokens > 0 and res.shape[0] <= 8
+                and H <= Kn.GEMV_NORM_MAX_K and H % 8 == 0
                 and all(getattr(l.mlp, "_svla_fp8", None) is None for l in layers)):
             return self._decode_fused(res, shp, rope, cache)
         x = layers[0].input_layernorm(res)
@@ -395,6 +405,45 @@ class Gemma2ForCausalLM(nn.Module):
 
     def set_decoder(self, decoder):
         self.model = decoder
+
+    def _set_gradient_checkpointing(self, enable: bool = True, gradient_checkpointing_func=None):
+        """The reference training script's call (train/spatialvla_pretrain.py:331-332 -> transformers'
+        _set_gradient_checkpointing, which flips `gradient_checkpointing` on the modules that have it; the reference
+        decoder then re-runs each layer in backward, modeling_gemma2.py:752-762).  Accepted as a recorded no-op: the
+        whole B=32 working set (~120 GB) stays resident in the 288 GB of HBM, so recompute would only
+        add a forward pass.  Numerically the two are the same computation."""
+        for m in self.modules():
+            if hasattr(m, "gradient_checkpointing"):
+                m.gradient_checkpointing = bool(enable)
+                m._gradient_checkpointing_func = gradient_checkpointing_func
+
+    def prepare_inputs_for_generation(self, input_ids, past_key_values=None, attention_mask=None, inputs_embeds=None,
+                                      cache_position=None, position_ids=None, use_cache=True, num_logits_to_keep=None,
+                                      **kwargs):
+        """Reference :1015-1091 for the KV cache here (Gemma2KVCache): input_ids sliced to the tokens not yet in the
+        cache, per-sequence positions attention_mask.cumsum - 1 (pads 1) for those tokens, inputs_embeds only at
+        the first step.  The 2-D attention_mask is passed through: SpatialVLAForConditionalGeneration.forward builds
+        the per-key classes from it (the reference builds the 4-D HybridCache mask here instead, :1057-1077)."""
+        if past_key_values is not None:
+            if inputs_embeds is not None:
+                input_ids = input_ids[:, -cache_position.shape[0]:]
+            elif input_ids.shape[1] != cache_position.shape[0]:
+                input_ids = input_ids[:, cache_position]
+        if attention_mask is not None and position_ids is None:
+            position_ids = attention_mask.long().cumsum(-1) - 1
+            position_ids.masked_fill_(attention_mask == 0, 1)
+            if past_key_values is not None:
+                position_ids = position_ids[:, -input_ids.shape[1]:].clone(memory_format=torch.contiguous_format)
+        if inputs_embeds is not None and int(cache_position[0]) == 0:
+            model_inputs = {"inputs_embeds": inputs_embeds, "input_ids": None}
+        else:
+            model_inputs = {"input_ids": input_ids.clone(memory_format=torch.contiguous_format), "inputs_embeds": None}
+        if num_logits_to_keep is not None:
+            model_inputs["num_logits_to_keep"] = num_logits_to_keep
+        model_inputs.update({"position_ids": position_ids, "cache_position": cache_position,
+                             "past_key_values": past_key_values, "use_cache": use_cache,
+                             "attention_mask": attention_mask})
+        return model_inputs
 
     def head(self, hidden_states, target, stash):
         """lm_head + softcap (reference :993-997) fused with the shifted CE; returns (logits2d, loss)."""

@@ -7,8 +7,9 @@ arguments and the `SpatialVLACausalLMOutputWithPast` return, `get_image_features
 
 Hot-path compute runs on libsvla (HIP, gfx950) through `spatialvla_amd.functional`:
 SigLIP, Ego3D, projector, embedding merge, 26 Gemma2 layers, softcapped lm_head + CE.
-The frozen ZoeDepth estimator (and its bicubic resampling) stays on stock PyTorch-ROCm ops under
-no_grad — it is not a north-star kernel target.
+The frozen ZoeDepth estimator runs under no_grad with its BEiT layers, every convolution, the DPT resizes and the
+metric-head tail on libsvla (zoe_fast); its preprocessing (reflect pad + bicubic, process_zoe) and the attractor /
+seed-regressor modules are the remaining stock PyTorch-ROCm ops.
 """
 import os
 import warnings
@@ -80,7 +81,7 @@ def _zoe_norm_consts(dtype, device):
 
 
 def process_zoe(pixel_values, pad_mode="reflect", output_size=(384, 512)):
-    """Reference :99-110 (ZoeDepth preprocessing), stock torch ops."""
+    """Reference :99-110 (ZoeDepth preprocessing)."""
     ph, pw = 31, 31
     images = F.pad(pixel_values, (pw, pw, ph, ph), mode=pad_mode)
     images = F.interpolate(images, size=(384, 384), mode="bicubic", align_corners=True)
@@ -108,7 +109,9 @@ class SpatialVLAMultiModalProjector(nn.Module):
 class SpatialVLAPreTrainedModel(PreTrainedModel):
     config_class = SpatialVLAConfig
     base_model_prefix = "model"
-    supports_gradient_checkpointing = False
+    # accepted (gradient_checkpointing_enable, the training script's language_model._set_gradient_checkpointing()),
+    # never recomputes: the working set stays resident in HBM (Gemma2ForCausalLM._set_gradient_checkpointing)
+    supports_gradient_checkpointing = True
     _no_split_modules = ["SpatialVLAMultiModalProjector", "ZoeDepthForDepthEstimation", "Ego3DPositionEmbeddingMLP"]
 
     def _init_weights(self, module):
@@ -205,10 +208,16 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
     def tie_weights(self, *args, **kwargs):
         return None  # SpatialVLA unties lm_head (spatialvla_pretrain.py:321-325)
 
+    def _set_gradient_checkpointing(self, enable: bool = True, gradient_checkpointing_func=None):
+        """gradient_checkpointing_enable() lands here: recorded on every module that carries the flag, no recompute
+        (see Gemma2ForCausalLM._set_gradient_checkpointing)."""
+        self.language_model._set_gradient_checkpointing(enable, gradient_checkpointing_func)
+        self.vision_tower.gradient_checkpointing = bool(enable)
+
     # ------------------------------------------------------------------ image path
     @torch.no_grad()
     def predict_depth(self, pixel_values):
-        """Zoe depth at image resolution (reference :314-323), frozen, stock torch ops."""
+        """Zoe depth at image resolution (reference :314-323), frozen; the estimator's layers on libsvla (zoe_fast)."""
         zoe_pv, ph, pw = process_zoe(pixel_values, pad_mode="reflect")
         pvh, pvw = pixel_values.shape[-2:]
         depth = self.vision_zoe_model(pixel_values=zoe_pv).predicted_depth
@@ -763,6 +772,77 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
                 first_eos = torch.where(hit, torch.arange(n, device=dev), n).min(1).values
                 toks = toks[:, :int(first_eos.max()) + 1]
         return toks
+
+    # ------------------------------------------------------------------ HF generate() surface
+    def prepare_inputs_for_generation(self, input_ids, past_key_values=None, inputs_embeds=None, cache_position=None,
+                                      position_ids=None, pixel_values=None, intrinsic=None, attention_mask=None,
+                                      token_type_ids=None, use_cache=True, num_logits_to_keep=None, labels=None,
+                                      **kwargs):
+        """Reference :445-482: the language model's hook (slicing to the uncached tokens, per-sequence positions),
+        positions + 1 (PaliGemma positions are 1-indexed), pixel values only at the first step, intrinsic passed
+        through.  The prefill's bidirectional prefix mask (:478-480) is built by forward() from the 2-D mask."""
+        model_inputs = self.language_model.prepare_inputs_for_generation(
+            input_ids, past_key_values=past_key_values, inputs_embeds=inputs_embeds, attention_mask=attention_mask,
+            position_ids=position_ids, cache_position=cache_position, use_cache=use_cache,
+            num_logits_to_keep=num_logits_to_keep, **kwargs)
+        if model_inputs.get("position_ids") is not None:
+            model_inputs["position_ids"] += 1
+        if int(cache_position[0]) == 0:
+            model_inputs["pixel_values"] = pixel_values
+        model_inputs["token_type_ids"] = token_type_ids if int(cache_position[0]) == 0 and labels is not None else None
+        model_inputs["intrinsic"] = intrinsic
+        return model_inputs
+
+    @torch.no_grad()
+    def generate(self, input_ids=None, pixel_values=None, intrinsic=None, attention_mask=None,
+                 max_new_tokens: int = 256, do_sample: bool = False, eos_token_id=None, pad_token_id=None,
+                 generation_config=None, **kwargs):
+        """Greedy `generate` as the reference's predict_action calls it (:491, HF generate with do_sample=False over a
+        HybridCache): the loop runs prepare_inputs_for_generation -> forward(past_key_values=Gemma2KVCache) per step
+        and returns prompt + new tokens; finished sequences get pad_token_id, the loop stops once every sequence
+        emitted eos.  Every step is eager here; predict_action is the graph-replayed fast path with the same tokens."""
+        if generation_config is not None:
+            max_new_tokens = getattr(generation_config, "max_new_tokens", None) or max_new_tokens
+            do_sample = bool(getattr(generation_config, "do_sample", do_sample))
+            eos_token_id = getattr(generation_config, "eos_token_id", None) if eos_token_id is None else eos_token_id
+            pad_token_id = getattr(generation_config, "pad_token_id", None) if pad_token_id is None else pad_token_id
+        if do_sample or int(kwargs.pop("num_beams", 1)) != 1:
+            raise NotImplementedError("generate: greedy decoding only (the reference calls do_sample=False)")
+        kwargs.pop("token_type_ids", None)
+        for k in ("output_attentions", "output_hidden_states", "return_dict_in_generate", "use_cache"):
+            kwargs.pop(k, None)
+        if kwargs:
+            raise TypeError(f"generate: unsupported arguments {sorted(kwargs)}")
+        self._wait_all_params()
+        eos = eos_token_id if eos_token_id is not None else self.config.text_config.eos_token_id
+        if isinstance(eos, (list, tuple)):
+            eos = eos[0] if eos else None
+        pad = pad_token_id if pad_token_id is not None else max(self.pad_token_id, 0)
+        dev = self.language_model.lm_head.weight.device
+        ids = input_ids.to(dev)
+        B, P = ids.shape
+        am = (attention_mask.to(dev) if attention_mask is not None
+              else torch.ones(B, P, dtype=torch.int64, device=dev))
+        pv = pixel_values.to(dev, torch.bfloat16) if pixel_values is not None else None
+        intr = intrinsic.to(dev, torch.bfloat16) if intrinsic is not None else None
+        cache = self.new_cache(B, P + max_new_tokens)
+        cache_position = torch.arange(P, device=dev)
+        finished = torch.zeros(B, dtype=torch.bool, device=dev)
+        for _ in range(max_new_tokens):
+            mi = self.prepare_inputs_for_generation(ids, past_key_values=cache, cache_position=cache_position,
+                                                    pixel_values=pv, intrinsic=intr, attention_mask=am)
+            mi.pop("cache_position")
+            self(**mi, return_dict=True)
+            nxt = self.action_argmax().view(B, -1)[:, -1]
+            if eos is not None:
+                nxt = torch.where(finished, torch.full_like(nxt, pad), nxt)
+                finished = finished | (nxt == eos)
+            ids = torch.cat([ids, nxt[:, None]], 1)
+            am = torch.cat([am, torch.ones(B, 1, dtype=am.dtype, device=dev)], 1)
+            cache_position = cache_position[-1:] + 1
+            if eos is not None and bool(finished.all()):
+                break
+        return ids
 
     @torch.no_grad()
     def predict_action_uncached(self, model_inputs, max_new_tokens: int = 256, eos_token_id: Optional[int] = None):

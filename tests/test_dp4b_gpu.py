@@ -1,0 +1,215 @@
+"""BASELINE configs[3]'s code path at the 4B workload: the ZeRO-1 exchange of TrainEngine (scripts/zero1.json:2-10)
+with the real SpatialVLA-4B bucket layout (~25 buckets of 256 MB, lm_head larger than one bucket) and the per-layer
+gradient hooks at full depth (26 Gemma2 + 27 SigLIP layers), 2 ranks over gloo, both on cuda:0 (the GPU box has one
+card; the 8-GPU RCCL run is the driver's), against one process training on the concatenated batch.
+
+Each rank trains on one episode of a 2-episode synthetic OXE batch for 2 steps; the single process on both episodes.
+Compared on sampled tensors (whole parameters, lm_head a row block), gathered from the ranks' owned ZeRO chunks:
+  * loss: the label-count-weighted mean of the rank losses equals the single-process loss (5e-3 relative), step 2
+    included -- so the all-gathered parameters of step 1 are the single process's;
+  * grad norm (after the reduce-scatter, clip input): 2e-2 relative;
+  * the averaged gradient of step 2 (each rank's owned chunks after the bf16 AVG reduce-scatter) vs the single
+    process's gradient: rel-L2 <= GRAD_TOL per tensor.  The per-rank GEMMs see M = 312 instead of 624 rows (other
+    tile / stream-K schedules, so other fp32 partial-sum orders) and each weight gradient is summed in two bf16 halves
+    and averaged in bf16;
+  * the fp32 masters after 2 AdamW steps: every element within 2 * steps * lr of the single process's (AdamW moves an
+    element by at most lr per step), and the ranks' bf16 parameters bitwise identical.
+The measured numbers go to gpurun_out/parity/dp4b.json."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import harness as H
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 2
+WORLD = 2
+LR = 1e-4
+# (parameter name, first row, rows) -- rows None = the whole tensor
+SAMPLES = [
+    ("language_model.model.layers.0.self_attn.q_proj.weight", 0, None),
+    ("language_model.model.layers.0.self_attn.v_proj.weight", 0, None),
+    ("language_model.model.layers.12.mlp.down_proj.weight", 0, None),
+    ("language_model.model.layers.25.mlp.gate_proj.weight", 0, None),
+    ("language_model.model.layers.25.self_attn.o_proj.weight", 0, None),
+    ("language_model.model.layers.3.post_feedforward_layernorm.weight", 0, None),
+    ("language_model.model.norm.weight", 0, None),
+    ("language_model.lm_head.weight", 257153, 4096),   # the first 4096 action-token rows
+    ("language_model.lm_head.weight", 1000, 2048),
+    ("spatial_embed_tokens.weight", 0, None),
+    ("multi_modal_projector.linear.weight", 0, None),
+    ("vision_tower.vision_model.encoder.layers.5.mlp.fc1.weight", 0, None),
+    ("vision_tower.vision_model.encoder.layers.26.self_attn.q_proj.bias", 0, None),
+    ("vision_tower.vision_model.embeddings.patch_embedding.weight", 0, None),
+    ("position_embedding_3d.position_embedding_head.0.weight", 0, None),
+]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(device):
+    from spatialvla_amd import SpatialVLAConfig, presets
+    from spatialvla_amd.detinit import hash_init_
+    from spatialvla_amd.modeling_spatialvla import SpatialVLAForConditionalGeneration
+    cfg = SpatialVLAConfig(**json.loads(json.dumps(presets.spatialvla_4b())))
+    cfg.vision_zoe_config._attn_implementation = "eager"
+    cfg.vision_zoe_config.backbone_config._attn_implementation = "eager"
+    with torch.device(device):
+        m = SpatialVLAForConditionalGeneration(cfg)
+    m = m.to(torch.bfloat16)
+    hash_init_(m, seed=H.SEED)
+    m.language_model.model.embed_tokens.weight.requires_grad_(False)
+    m.vision_zoe_model.eval()
+    for p in m.vision_zoe_model.parameters():
+        p.requires_grad_(False)
+    m.train()
+    m.vision_zoe_model.eval()
+    return m
+
+
+def _batches(device):
+    from spatialvla_amd import presets
+    cfgd = H.cfg_dict("spatialvla_4b")
+    return [H.batch_tensors(presets.synthetic_batch(cfgd, batch=WORLD, seed=300 + s), device) for s in range(STEPS)]
+
+
+def _owned_samples(eng, names):
+    """{(name, row0): (flat element indices relative to the slice, averaged grad, fp32 master, digest of the whole
+    bf16 slice, slice length)} for the parts of each sampled slice inside this rank's owned ZeRO chunks."""
+    import hashlib
+    ex = eng.exchange
+    pidx = {id(p): i for i, p in enumerate(eng.params)}
+    out = {}
+    for name, r0, nr in SAMPLES:
+        p = names[name]
+        i = pidx[id(p)]
+        row = p.numel() // p.shape[0] if p.dim() > 1 else 1
+        lo = eng.offsets[i] + r0 * row
+        hi = lo + (nr * row if nr is not None else p.numel() - r0 * row)
+        idx, g, m = [], [], []
+        digest = hashlib.sha1(eng.flat_param[lo:hi].view(torch.int16).cpu().numpy().tobytes()).hexdigest()
+        for b in range(len(eng.buckets)):
+            o, c = ex.owned(b)
+            a, e = max(lo, o), min(hi, o + c)
+            if a >= e:
+                continue
+            so = eng.shard_offsets[b] + (a - o)
+            idx.append(np.arange(a - lo, e - lo))
+            g.append(eng.flat_grad[a:e].float().cpu().numpy())
+            m.append(eng.master[so:so + (e - a)].cpu().numpy())
+        cat = (lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.float32))  # noqa: E731
+        out[(name, r0)] = (np.concatenate(idx) if idx else np.zeros(0, np.int64), cat(g), cat(m), digest, hi - lo)
+    return out
+
+
+def _train(rank, world, device):
+    from spatialvla_amd.engine import TrainEngine
+    model = _model(device)
+    names = dict(model.named_parameters())
+    per = WORLD // world
+    depth = torch.rand(WORLD, 1, 224, 224, generator=torch.Generator().manual_seed(11)).mul(3).add(0.5).to(device)
+    model.predict_depth = lambda pv, _d=depth[rank * per:(rank + 1) * per]: _d
+    init = {}
+    for name, r0, nr in SAMPLES:
+        t = names[name].detach()
+        t = t.reshape(t.shape[0], -1)[r0:(r0 + nr if nr is not None else None)] if t.dim() > 1 else t
+        init[(name, r0)] = t.float().cpu().numpy().ravel().copy()
+    eng = TrainEngine(model, lr=LR, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0)
+    losses, gnorms = [], []
+    for b in _batches(device):
+        part = {k: v[rank * per:(rank + 1) * per] for k, v in b.items()}
+        losses.append(float(eng.train_step(part).item()))
+        gnorms.append(float(eng.gnorm.item()))
+    eng.sync_params()
+    torch.cuda.synchronize()
+    res = _owned_samples(eng, names)
+    return {"losses": losses, "gnorms": gnorms, "samples": res, "init": init, "nbuckets": len(eng.buckets),
+            "hooked": len(eng.exchange.ready_end)}
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _train(rank, world, "cuda:0")))
+    except Exception as e:  # surface the failure instead of a queue timeout
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _assemble(parts, key):
+    n = parts[0][key][4]
+    g, m = (np.full(n, np.nan, np.float32) for _ in range(2))
+    cover = np.zeros(n, np.int64)
+    for r in parts:
+        idx, gg, mm, _, _ = r[key]
+        g[idx], m[idx] = gg, mm
+        cover[idx] += 1
+    return g, m, cover
+
+
+@pytest.mark.timeout(1100)
+def test_dp2_zero1_4b_equals_single_process(cuda):
+    torch.cuda.empty_cache()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=900) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+    for r, v in res:
+        assert isinstance(v, dict), (r, v)
+    assert all(p.exitcode == 0 for p in procs)
+    ranks = [v for _, v in res]
+    single = _train(0, 1, "cuda:0")
+    assert ranks[0]["nbuckets"] > 16 and ranks[0]["hooked"] >= 26 + 27  # the real 4B layout, every layer hooked
+    report = {"losses_dp": [r["losses"] for r in ranks], "losses_single": single["losses"],
+              "gnorm_dp": ranks[0]["gnorms"], "gnorm_single": single["gnorms"], "tensors": {}}
+    for s in range(STEPS):
+        mean = float(np.mean([r["losses"][s] for r in ranks]))  # 13 labelled tokens per episode: equal weights
+        assert abs(mean - single["losses"][s]) <= 5e-3 * abs(single["losses"][s]), (s, mean, single["losses"][s])
+        for r in ranks:
+            assert r["gnorms"][s] == ranks[0]["gnorms"][s]
+        assert ranks[0]["gnorms"][s] == pytest.approx(single["gnorms"][s], rel=2e-2)
+    bound = 2 * STEPS * LR * 1.05
+    for name, r0, _ in SAMPLES:
+        key = (name, r0)
+        g, m, cover = _assemble([r["samples"] for r in ranks], key)
+        assert (cover == 1).all(), (key, "owned chunks must tile every parameter exactly once")
+        idx1, g1, m1, w1, _ = single["samples"][key]
+        assert np.array_equal(idx1, np.arange(len(g1)))
+        p0 = single["init"][key]
+        grel = float(np.linalg.norm(g - g1) / max(np.linalg.norm(g1), 1e-30))
+        d1 = m1 - p0
+        urel = float(np.linalg.norm((m - p0) - d1) / max(np.linalg.norm(d1), 1e-30))
+        umax = float(np.abs(m - m1).max())
+        report["tensors"][f"{name}[{r0}:]"] = {"grad_rel": grel, "update_rel": urel, "master_maxdiff": umax}
+        assert grel <= H.GRAD_TOL, (key, grel)
+        assert umax <= bound, (key, umax, bound)
+        # the ranks' bf16 parameters after the all-gather: bitwise identical
+        assert len({r["samples"][key][3] for r in ranks}) == 1, key
+    d = os.environ.get("SVLA_PARITY_DIR", os.path.join(H.REPO, "gpurun_out", "parity"))
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "dp4b.json"), "w") as f:
+        json.dump(report, f, indent=1)
+    print("dp4b:", json.dumps({k: v for k, v in report.items() if k != "tensors"}),
+          {k: round(v["grad_rel"], 5) for k, v in report["tensors"].items()})

@@ -152,6 +152,9 @@ _NORM_SUFFIXES = ("layernorm.weight", "layer_norm1.weight", "layer_norm2.weight"
                   "model.norm.weight")
 
 
+N_OVER_GRAD_TOL_R3 = 12
+
+
 def _full_tol(name: str) -> float:
     if _qk_exception(name):
         return 8e-2
@@ -198,7 +201,10 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
     torch.cuda.empty_cache()
     _dump("full4b_bf16.json", {"loss": {"hip": float(loss), "oracle_gpu": float(oloss),
                                          "reference": float(gold["out.loss"][0])},
-                                "hip": hip, "oracle_gpu": ora, "full_tensor_grad_rel_vs_oracle_gpu": full_rel})
+                                "hip": hip, "oracle_gpu": ora, "full_tensor_grad_rel_vs_oracle_gpu": full_rel,
+                                "n_over_grad_tol_non_qk": sum(1 for n, e in full_rel.items()
+                                                              if e > H.GRAD_TOL and not _qk_exception(n)),
+                                "max_non_qk": max(e for n, e in full_rel.items() if not _qk_exception(n))})
     summary = {k: (hip[k], ora[k]) for k in ("act", "cols", "lse", "agree_005", "agree_025", "agree_action_rows")}
     worst_n = sorted(hip["gradnorm"].items(), key=lambda kv: -kv[1])[:3]
     ratio = {n: hip["gradrow"][n] / max(ora["gradrow"][n], 5e-2 / 1.5) for n in hip["gradrow"]}
@@ -232,6 +238,12 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
     assert len(full_rel) > 700
     bad_f = {n: e for n, e in full_rel.items() if e > _full_tol(n)}
     assert not bad_f, sorted(bad_f.items(), key=lambda kv: -kv[1])[:8]
+    # drift guard: the named 4e-2 exceptions may not absorb a general loss of accuracy -- the number of
+    # non-q/k tensors above the 3e-2 bound stays at or below round 3's measured count (12 of 707, all gate_proj /
+    # norm weights, max 3.11e-2; profiles/r3n_parity4b_bf16.json), so a kernel change that adds noise fails here
+    # before it reaches a tolerance
+    over = sorted((e, n) for n, e in full_rel.items() if e > H.GRAD_TOL and not _qk_exception(n))
+    assert len(over) <= N_OVER_GRAD_TOL_R3, (len(over), over[-6:])
 
 
 @pytest.mark.timeout(600)

@@ -518,6 +518,34 @@ def test_layernorm_colsum(cuda):
     assert rel_l2(cs, dy.float().sum(0)) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,ld", [(8192, 1152, 3456), (8192, 4304, 4304), (624, 2304, 2304), (5, 8, 16)])
+def test_colsum_single_pass(cuda, M, N, ld):
+    """svla_colsum_bf16 / svla_colsum_f32 / svla_colsum2_f32 (one launch each): fp32 sums of strided bf16 and fp32
+    matrices, accumulate into the bf16 output, bitwise reproducible run to run."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(6)
+    x = _r(M, ld)[:, :N]
+    out = torch.empty(N, dtype=BF, device=cuda)
+    Kn.colsum_bf16(x, out)
+    ref = x.float().sum(0)
+    assert rel_l2(out, ref) < 5e-3
+    again = torch.empty_like(out)
+    Kn.colsum_bf16(x, again)
+    assert torch.equal(out, again)
+    base = _r(N)
+    acc = base.clone()
+    Kn.colsum_bf16(x, acc, accumulate=True)
+    assert rel_l2(acc, ref + base.float()) < 5e-3
+    part = torch.randn(2, M, N, device=cuda)
+    o1 = torch.empty(N, dtype=BF, device=cuda)
+    Kn.colsum_f32(part[0], o1)
+    assert rel_l2(o1, part[0].sum(0)) < 5e-3
+    o2a, o2b = torch.empty_like(o1), torch.empty_like(o1)
+    L.check(L.lib().svla_colsum2_f32(M, N, part.data_ptr(), o2a.data_ptr(), o2b.data_ptr(), 0,
+                                     torch.cuda.current_stream().cuda_stream), "colsum2")
+    assert torch.equal(o2a, o1) and rel_l2(o2b, part[1].sum(0)) < 5e-3
+
+
 # ------------------------------------------------------------------------------------------ attention
 def _ref_attn(q, k, v, scale, cap, kv_class, window, cos=None, sin=None):
     """fp32 eager reference in [B, L, H, D] layout with per-key classes."""

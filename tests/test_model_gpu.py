@@ -218,8 +218,18 @@ def test_predict_action_decodes(cuda):
     assert out.shape == (2, 3)
 
 
-@pytest.mark.parametrize("cached", [True, False])
-def test_predict_action_tokens_vs_reference_golden(cuda, cached):
+def _decode(model, inputs, n, mode):
+    """n greedy tokens by predict_action (KV cache + graphs), the uncached re-forward, or the HF-style
+    model.generate(...) loop over prepare_inputs_for_generation (reference modeling_spatialvla.py:445-492)."""
+    if mode == "generate":
+        P = inputs["input_ids"].shape[1]
+        return model.generate(**inputs, max_new_tokens=n, do_sample=False, eos_token_id=-1)[:, P:]
+    fn = model.predict_action if mode == "cached" else model.predict_action_uncached
+    return fn(inputs, max_new_tokens=n, eos_token_id=-1)
+
+
+@pytest.mark.parametrize("mode", ["cached", "uncached", "generate"])
+def test_predict_action_tokens_vs_reference_golden(cuda, mode):
     """Greedy decode (KV cache + HIP graphs, and the uncached re-forward) against the tokens the reference model
     itself generated (oracle/gen_golden.py gen_decode_tiny), margin-gated (harness.greedy_tokens_agree)."""
     g = _load("decode_tiny.safetensors")
@@ -229,15 +239,14 @@ def test_predict_action_tokens_vs_reference_golden(cuda, cached):
     model.predict_depth = lambda p: depth
     inputs = {"input_ids": g["in.input_ids"], "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
     n = g["out.tokens"].shape[1]
-    fn = model.predict_action if cached else model.predict_action_uncached
-    out = fn(inputs, max_new_tokens=n, eos_token_id=-1)
+    out = _decode(model, inputs, n, mode)
     n_cmp, n_ok = H.greedy_tokens_agree(out, g["out.tokens"], g["out.margins"])
     print(f"decode tokens {out.tolist()} vs ref {g['out.tokens'].tolist()}: {n_ok}/{n_cmp}")
     assert n_ok >= 2
 
 
-@pytest.mark.parametrize("cached", [True, False])
-def test_predict_action_padded_batch_vs_reference_golden(cuda, cached):
+@pytest.mark.parametrize("mode", ["cached", "uncached", "generate"])
+def test_predict_action_padded_batch_vs_reference_golden(cuda, mode):
     """Left-padded prompts of three lengths (attention_mask zeros): per-sequence RoPE positions from the mask's
     cumsum (reference generate, modeling_gemma2.py:1039-1042) and masked pad keys, against the tokens the reference
     model generated (oracle/gen_golden.py gen_decode_padded), margin-gated; the unpadded-length row and the padded
@@ -250,8 +259,7 @@ def test_predict_action_padded_batch_vs_reference_golden(cuda, cached):
     inputs = {"input_ids": g["in.input_ids"], "attention_mask": g["in.attention_mask"],
               "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
     n = g["out.tokens"].shape[1]
-    fn = model.predict_action if cached else model.predict_action_uncached
-    out = fn(inputs, max_new_tokens=n, eos_token_id=-1)
+    out = _decode(model, inputs, n, mode)
     n_cmp, n_ok = H.greedy_tokens_agree(out, g["out.tokens"], g["out.margins"])
     print(f"padded decode tokens {out.tolist()} vs ref {g['out.tokens'].tolist()}: {n_ok}/{n_cmp}")
     assert bool((out[:, 0].cpu() == g["out.tokens"][:, 0]).all())
