@@ -244,6 +244,12 @@ int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* y
  * Gemma2 post-attention + pre-feedforward norms, or post-feedforward + next input norm (modeling_gemma2.py:487-496). */
 int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1, const void* w2,
                           float eps1, float eps2, void* h, void* x, void* stream);
+/* The same pair in the training forward: also writes the per-row rstd of both norms (fp32 [rows] each) for the two
+ * svla_rmsnorm_bwd calls of the backward.  Decoder layer post-attention + pre-feedforward norms
+ * (modeling_gemma2.py:487-490); bitwise svla_add_rmsnorm_fwd followed by svla_rmsnorm_fwd. */
+int svla_add_rmsnorm2_fwd_train(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,
+                                const void* w2, float eps1, float eps2, void* h, void* x, float* rstd1, float* rstd2,
+                                void* stream);
 int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
                        void* y, float* mean, float* rstd, void* stream);
 /* dwb_partial: two planes [2][ceil(rows/rows_per_block)][N] fp32 (dw partials, then db partials), reduced by

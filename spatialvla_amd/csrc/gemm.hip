@@ -1566,48 +1566,60 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
 #endif
 
-  auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
-#if G4_STAMPS
-    const unsigned long long tm0 = __builtin_amdgcn_s_memtime();
-#endif
-    agpr_zero();
-    Op4<LA> sa;
-    Op4<LB> sb;
+  // Operand staging state of the tile being (or about to be) computed.  stage_first() sets it up and issues the
+  // LDS-DMA of the tile's first two k-tiles; the tile loop calls it for the NEXT tile right before a direct
+  // epilogue (which needs no LDS), so the next tile's prologue loads fly while this tile's outputs are stored.
+  Op4<LA> sa;
+  Op4<LB> sb;
+  const char* abase = nullptr;
+  const char* bbase = nullptr;
+  // voffsets of every piece for a k-tile that lies wholly inside both reduction extents (all but the last when
+  // K % 64 != 0): the per-piece range selects (v_cmp / s_and / v_cndmask per piece) leave the main loop
+  uint32_t vfa[8], vfb[8];
+  // piece n of the wave for the k-tile at krem = valid k extent left (KC: per-lane chunk check, RC: k-row check)
+  // (the LDS-DMA itself lives in a __device__ function: lambdas of a kernel template are instantiated for the
+  // host too, where the address-space cast would be a substitution failure and the kernel stub would vanish)
+  auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w); };
+  auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
+  auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w); };
+  auto pieceB_full = [&](const char* kb_, int n, char* img) { op4_piece(kb_, vfb[n], n * sb.rs, n, img, w); };
+  auto issue_all = [&](int kt, char* stage) {
+    const int64_t k0 = (int64_t)kt * BK;
+    const char* const ka = abase + k0 * ksa;
+    const char* const kbb = bbase + k0 * ksb;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) pieceA(ka, kvA - k0, n, stage);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) pieceB(kbb, kvB - k0, n, stage + OPB);
+  };
+  auto stage_first = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
     op4_setup<LA>(A, m0, rvA, w, lane, sa);
     op4_setup<LB>(B, n0, rvB, w, lane, sb);
-    const char* const abase = op4_base<LA>(A, m0, w >> 1);
-    const char* const bbase = op4_base<LB>(B, n0, w >> 1);
-    // piece n of the wave for the k-tile at krem = valid k extent left (KC: per-lane chunk check, RC: k-row check)
-    // (the LDS-DMA itself lives in a __device__ function: lambdas of a kernel template are instantiated for the
-    // host too, where the address-space cast would be a substitution failure and the kernel stub would vanish)
-    auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w); };
-    auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
-    // voffsets of every piece for a k-tile that lies wholly inside both reduction extents (all but the last when
-    // K % 64 != 0): the per-piece range selects (v_cmp / s_and / v_cndmask per piece) leave the main loop
-    uint32_t vfa[8], vfb[8];
+    abase = op4_base<LA>(A, m0, w >> 1);
+    bbase = op4_base<LB>(B, n0, w >> 1);
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       vfa[n] = op4_voff(sa, n, (int64_t)1 << 40);
       vfb[n] = op4_voff(sb, n, (int64_t)1 << 40);
     }
-    auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w); };
-    auto pieceB_full = [&](const char* kb_, int n, char* img) { op4_piece(kb_, vfb[n], n * sb.rs, n, img, w); };
-    auto issue_all = [&](int kt, char* stage) {
-      const int64_t k0 = (int64_t)kt * BK;
-      const char* const ka = abase + k0 * ksa;
-      const char* const kbb = bbase + k0 * ksb;
-#pragma unroll
-      for (int n = 0; n < 8; ++n) pieceA(ka, kvA - k0, n, stage);
-#pragma unroll
-      for (int n = 0; n < 8; ++n) pieceB(kbb, kvB - k0, n, stage + OPB);
-    };
-    const int nq = ke - kb;
     issue_all(kb, smem);
-    if (nq > 1) {
-      issue_all(kb + 1, smem + STAGE);
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else {
+    if (ke - kb > 1) issue_all(kb + 1, smem + STAGE);
+  };
+
+  // pre: stage_first() already ran for this tile (during the previous tile's epilogue); its loads and that
+  // epilogue's stores are then all drained here (vmcnt(0)): they have had a whole epilogue to land
+  auto mainloop = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane, bool pre) {
+#if G4_STAMPS
+    const unsigned long long tm0 = __builtin_amdgcn_s_memtime();
+#endif
+    agpr_zero();
+    const int nq = ke - kb;
+    if (pre) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      stage_first(m0, n0, kb, ke, lane);
+      if (nq > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     P8_BARRIER();
     using T = std::true_type;
@@ -2092,27 +2104,41 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   int* sflag = reinterpret_cast<int*>(smem);
   int dp_tile = L;
   int64_t it = (int64_t)L * I / G;
-#pragma unroll 1
-  while (true) {
-    int tile, kb, ke, st = 0;
+  // the block's work items in order: its data-parallel tiles, then its stream-K k-range
+  auto next_item = [&](int& tile, int& kb, int& ke, int& st) -> bool {
+    st = 0;
     if (dp_tile < sk.dp_tiles) {
       tile = dp_tile;
       dp_tile += sk.grid;
       kb = 0;
       ke = nk;
-    } else {
-      if (it >= it1) break;
-      st = (int)(it / nk);
-      kb = (int)(it - (int64_t)st * nk);
-      ke = (int)min((int64_t)nk, kb + (it1 - it));
-      it += ke - kb;
-      tile = sk.dp_tiles + st;
+      return true;
     }
+    if (it >= it1) return false;
+    st = (int)(it / nk);
+    kb = (int)(it - (int64_t)st * nk);
+    ke = (int)min((int64_t)nk, kb + (it1 - it));
+    it += ke - kb;
+    tile = sk.dp_tiles + st;
+    return true;
+  };
+  // the direct epilogue (below) stores from the accumulators and leaves LDS untouched
+  auto direct_ok = [&](int64_t m0, int64_t n0) {
+    if constexpr (F8) return false;
+    const int kind = E.kind;
+    const bool k_ok = GG ? (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE) : kind == SVLA_EPI_STORE;
+    return k_ok && m0 + BM <= M && n0 + BN <= N;
+  };
+  int tile, kb, ke, st;
+  bool have = next_item(tile, kb, ke, st), pre = false;
+#pragma unroll 1
+  while (have) {
     int t;
     asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t_in));
     int64_t m0, n0;
     coords(tile, m0, n0);
-    mainloop(m0, n0, kb, ke, t & 63);
+    mainloop(m0, n0, kb, ke, t & 63, pre);
+    pre = false;
     if (kb != 0 || ke != nk) {
       // partial tile: the stream-K hand-off of gemm8_kernel (slab per segment, last arriver reduces in k order)
       const int64_t T0 = (int64_t)st * nk, T1 = T0 + nk;
@@ -2155,7 +2181,10 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         last = sflag[0] != 0;
         __syncthreads();
       }
-      if (!last) continue;
+      if (!last) {
+        have = next_item(tile, kb, ke, st);
+        continue;
+      }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       for (int sg = (j != 0) ? 0 : 1; sg < nseg; ++sg) {
         const __amdgpu_buffer_rsrc_t rs = slab(sg);
@@ -2175,6 +2204,13 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           asm volatile("" : "+v"(vo));
         });
       }
+    }
+    have = next_item(tile, kb, ke, st);
+    if (have && direct_ok(m0, n0)) {  // LDS is free (every wave is past mainloop's closing barrier)
+      int64_t m1, n1;
+      coords(tile, m1, n1);
+      stage_first(m1, n1, kb, ke, t & 63);
+      pre = true;
     }
 #if G4_STAMPS
     const unsigned long long te0 = __builtin_amdgcn_s_memtime();

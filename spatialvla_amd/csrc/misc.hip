@@ -401,6 +401,9 @@ __global__ void adamw_kernel(int64_t n, float* __restrict__ master, bf16_t* __re
                              float b1, float b2, float eps, float wd, float bc1, float bc2,
                              const float* __restrict__ clip) {
   const float cs = clip ? clip[0] : 1.0f;
+  // the two divides and the square root as 1-ulp hardware reciprocal / sqrt: the correctly rounded forms cost ~30
+  // VALU instructions per element (the update agrees with torch.optim.AdamW to ~1e-7 relative)
+  const float ibc1 = 1.0f / bc1, ibc2 = 1.0f / bc2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n; i += stride) {
     if (i + 8 <= n) {
@@ -418,7 +421,7 @@ __global__ void adamw_kernel(int64_t n, float* __restrict__ master, bf16_t* __re
         const float gg = g[j] * cs;
         mm[j] = b1 * mm[j] + (1.f - b1) * gg;
         vv[j] = b2 * vv[j] + (1.f - b2) * gg * gg;
-        const float upd = (mm[j] / bc1) / (sqrtf(vv[j] / bc2) + eps);
+        const float upd = (mm[j] * ibc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[j] * ibc2) + eps);
         pp[j] = pp[j] - lr * (upd + wd * pp[j]);
       }
       st_stream(reinterpret_cast<f32x4*>(master + i), f32x4{pp[0], pp[1], pp[2], pp[3]});

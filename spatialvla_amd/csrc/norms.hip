@@ -68,7 +68,8 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
                                                             const bf16_t* __restrict__ res,
                                                             const bf16_t* __restrict__ w1,
                                                             const bf16_t* __restrict__ w2, float eps1, float eps2,
-                                                            bf16_t* __restrict__ h, bf16_t* __restrict__ x) {
+                                                            bf16_t* __restrict__ h, bf16_t* __restrict__ x,
+                                                            float* __restrict__ rstd1_out, float* __restrict__ rstd2_out) {
   __shared__ float red[16];
   const int64_t row = blockIdx.x;
   const int nch = (int)(N >> 3);
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
   }
   ss = block_sum(ss, red);
   const float rstd1 = rsqrtf(ss / (float)N + eps1);
+  if (threadIdx.x == 0 && rstd1_out) rstd1_out[row] = rstd1;
   float ss2 = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
@@ -104,6 +106,7 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
   __syncthreads();  // red[] is reused by the second reduction
   ss2 = block_sum(ss2, red);
   const float rstd2 = rsqrtf(ss2 / (float)N + eps2);
+  if (threadIdx.x == 0 && rstd2_out) rstd2_out[row] = rstd2;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     int ch = threadIdx.x + c * NTH;
@@ -552,8 +555,10 @@ __global__ __launch_bounds__(256) void colsum1_kernel(int64_t P, int64_t N, cons
 template <typename T>
 int launch_colsum1(int64_t P, int64_t N, const T* in, int64_t ld, int64_t plane_stride, int planes, bf16_t* out0,
                    bf16_t* out1, int acc, hipStream_t s) {
-  // 32 columns a block when that still gives >= 64 blocks, else 16 (more blocks, shorter row segments)
-  if ((N + 31) / 32 * planes >= 64)
+  // 32 columns a block when that still gives >= 64 blocks, else 16 (more blocks, shorter row segments); chosen by N
+  // alone, so a plane reduced by svla_colsum2_f32 sums in the order svla_colsum_f32 uses
+  (void)planes;
+  if ((N + 31) / 32 >= 64)
     hipLaunchKernelGGL((colsum1_kernel<T, 32>), dim3((unsigned)((N + 31) / 32), (unsigned)planes), dim3(256), 0, s, P,
                        N, in, ld, plane_stride, out0, out1, acc);
   else
@@ -671,6 +676,18 @@ extern "C" int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, c
                      al16(x), "add_rmsnorm2: null/misaligned pointer");
   hipLaunchKernelGGL(rms_add_norm2_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
                      (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
-                     (bf16_t*)h, (bf16_t*)x);
+                     (bf16_t*)h, (bf16_t*)x, (float*)nullptr, (float*)nullptr);
   return svla::check_launch("add_rmsnorm2_fwd");
+}
+
+extern "C" int svla_add_rmsnorm2_fwd_train(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,
+                                           const void* w2, float eps1, float eps2, void* h, void* x, float* rstd1,
+                                           float* rstd2, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * MAXC * 8, "add_rmsnorm2_train: bad N");
+  SVLA_CHECK_ARG(res && yin && w1 && w2 && h && x && rstd1 && rstd2 && al16(res) && al16(yin) && al16(w1) &&
+                     al16(w2) && al16(h) && al16(x), "add_rmsnorm2_train: null/misaligned pointer");
+  hipLaunchKernelGGL(rms_add_norm2_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
+                     (bf16_t*)h, (bf16_t*)x, rstd1, rstd2);
+  return svla::check_launch("add_rmsnorm2_fwd_train");
 }

@@ -62,7 +62,8 @@ __device__ __forceinline__ float fast_tanh(float x) {
   p = p * x2 - 2.f / 15.f;
   p = p * x2 + 1.f / 3.f;
   const float small = x - x * x2 * p;
-  const float big = 1.0f - 2.0f / (__expf(2.0f * ax) + 1.0f);
+  // v_rcp_f32 (1 ulp) instead of the correctly rounded divide (~10 instructions): tanh's absolute error stays ~1e-7
+  const float big = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * ax) + 1.0f);
   return ax < 0.55f ? small : copysignf(big, x);
 }
 // transformers "gelu_pytorch_tanh" == torch.nn.functional.gelu(approximate="tanh")

@@ -36,7 +36,7 @@ constexpr int HID = 80, NB = 64, CIN_MAX = 192;
 // branches per argument range, which diverges across a wave and dominated this kernel.  The GELU output is
 // rounded to bf16, far coarser than the fit error.
 __device__ __forceinline__ float erfc_pos(float z) {  // z >= 0
-  const float t = 1.0f / (1.0f + 0.5f * z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.5f * z);  // 1-ulp reciprocal: the fit's own error is 1.2e-7
   const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
                   t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
   return t * __expf(-z * z + p);
@@ -104,7 +104,7 @@ __device__ __forceinline__ void load8(const bf16_t* p, int64_t stride, bool vec,
 constexpr int KP = 192, KS = KP / 32, NT = HID / 16, HS_LD = HID + 8;
 constexpr int ZT_LDS = KS * NT * 64 * 16 + 256 * HS_LD * 2;
 
-__global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const float* __restrict__ prm) {
+__global__ __launch_bounds__(256, 2) void zoe_tail_kernel(ZoeTailArgs a, const float* __restrict__ prm) {
   extern __shared__ __attribute__((aligned(16))) char zsm[];
   bf16_t* wl = (bf16_t*)zsm;                              // [KS][NT][64 lanes][8] B fragments
   bf16_t* hs = (bf16_t*)(zsm + KS * NT * 64 * 16);         // [256 pixels][HS_LD] bf16(h + b1)
@@ -138,14 +138,14 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   }
   __syncthreads();
 
-  f32x4 hacc[4][NT];
-#pragma unroll
-  for (int pg = 0; pg < 4; ++pg)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) hacc[pg][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // one 16-pixel group at a time: its NT accumulators go to LDS as soon as its k-steps are done (20 live accumulator
+  // registers instead of 80; with every group live the kernel ran at one wave per SIMD)
   const int g4 = lane >> 4;
-#pragma unroll
+#pragma unroll 1
   for (int pg = 0; pg < 4; ++pg) {
+    f32x4 hacc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) hacc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     int64_t pix = pix0 + 64 * w + 16 * pg + (lane & 15);
     const bool pv = pix < npix;
     if (!pv) pix = npix - 1;
@@ -180,19 +180,17 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(wl + ((ks * NT + nt) * 64 + lane) * 8);
-        hacc[pg][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, hacc[pg][nt], 0, 0, 0);
+        hacc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, hacc[nt], 0, 0, 0);
       }
     }
-  }
-  // C[pixel row 4(l>>4)+i][output 16nt + (l&15)] -> hs[pixel][o] = bf16(h + b1)
+    // C[pixel row 4(l>>4)+i][output 16nt + (l&15)] -> hs[pixel][o] = bf16(h + b1)
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int o = 16 * nt + (lane & 15);
-    const float bias = pb1[o];
+    for (int nt = 0; nt < NT; ++nt) {
+      const int o = 16 * nt + (lane & 15);
+      const float bias = pb1[o];
 #pragma unroll
-    for (int pg = 0; pg < 4; ++pg)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hs[(64 * w + 16 * pg + 4 * g4 + i) * HS_LD + o] = f2bf(hacc[pg][nt][i] + bias);
+      for (int i = 0; i < 4; ++i) hs[(64 * w + 16 * pg + 4 * g4 + i) * HS_LD + o] = f2bf(hacc[nt][i] + bias);
+    }
   }
   __syncthreads();
 
@@ -202,16 +200,18 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   const int y = (int)((pix / a.W) % a.H);
   const int b = (int)(pix / ((int64_t)a.W * a.H));
   const Tap ty = tap(y, a.h, a.H), tx = tap(x, a.w, a.W);
-  float h[HID];
-#pragma unroll
-  for (int o8 = 0; o8 < HID / 8; ++o8) unpack8(*reinterpret_cast<const u32x4*>(hs + t * HS_LD + 8 * o8), h + 8 * o8);
-
   float s4[4] = {pb2[0], pb2[1], pb2[2], pb2[3]};
+#pragma unroll 2
+  for (int o8 = 0; o8 < HID / 8; ++o8) {  // the hidden row in 8-channel pieces (not 80 registers at once)
+    float h[8];
+    unpack8(*reinterpret_cast<const u32x4*>(hs + t * HS_LD + 8 * o8), h);
 #pragma unroll
-  for (int o = 0; o < HID; ++o) {
-    const float g = round_bf(gelu_erf(round_bf(h[o])));
+    for (int j = 0; j < 8; ++j) {
+      const int o = 8 * o8 + j;
+      const float g = round_bf(gelu_erf(round_bf(h[j])));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s4[q] += pw2[q * HID + o] * g;
+      for (int q = 0; q < 4; ++q) s4[q] += pw2[q * HID + o] * g;
+    }
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) s4[q] = round_bf(softplus_f(round_bf(s4[q])));
@@ -225,9 +225,8 @@ __global__ __launch_bounds__(256) void zoe_tail_kernel(ZoeTailArgs a, const floa
   const float om = round_bf(fminf(fmaxf(round_bf(1.f - p), a.clamp_eps), 1.f));
   p = round_bf(fminf(fmaxf(p, a.clamp_eps), 1.f));
   const float lp = round_bf(__logf(p)), lom = round_bf(__logf(om));
-  auto zk = [&](int k) {
-    return __fdividef(plb[k] + round_bf((float)k * lp) + round_bf((float)(NB - 1 - k) * lom), temp);
-  };
+  const float itemp = __builtin_amdgcn_rcpf(temp);
+  auto zk = [&](int k) { return (plb[k] + round_bf((float)k * lp) + round_bf((float)(NB - 1 - k) * lom)) * itemp; };
   float zmax = -INFINITY;
 #pragma unroll 8
   for (int k = 0; k < NB; ++k) zmax = fmaxf(zmax, zk(k));

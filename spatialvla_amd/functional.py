@@ -109,6 +109,47 @@ class AddRMSNormFn(torch.autograd.Function):
         return dh, dy, ret, None, None
 
 
+class AddRMSNorm2Fn(torch.autograd.Function):
+    """(h, x) = (res + Gemma2RMSNorm_1(y), Gemma2RMSNorm_2(h)): the decoder layer's post-attention norm + residual
+    and its pre-feedforward norm (modeling_gemma2.py:487-490) in one forward launch (svla_add_rmsnorm2_fwd_train,
+    bitwise AddRMSNormFn then RMSNormFn).  Backward: dh_total = rms_bwd_2(dx) + dh (dh: h's residual-branch
+    gradient, from slot_h when its consumer parks it there), then dy = rms_bwd_1(dh_total); dh_total is the gradient
+    of res (parked in slot_res for the pre-norm that also reads res, as AddRMSNormFn does)."""
+
+    @staticmethod
+    def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None):
+        res, y = _c(res), _c(y)
+        h, x = torch.empty_like(y), torch.empty_like(y)
+        r1 = _empty(y.shape[0], dtype=F32, like=y)
+        r2 = _empty(y.shape[0], dtype=F32, like=y)
+        K.add_rmsnorm2_fwd_train(res, y, w1, w2, eps1, eps2, h, x, r1, r2)
+        ctx.save_for_backward(y, h, w1, w2, r1, r2)
+        ctx.slots = (slot_res, slot_h)
+        ctx.set_materialize_grads(False)  # h's residual gradient usually arrives through slot_h: no zero tensor
+        return h, x
+
+    @staticmethod
+    def backward(ctx, dh, dx):
+        y, h, w1, w2, r1, r2 = ctx.saved_tensors
+        slot_res, slot_h = ctx.slots
+        if slot_h is not None:
+            parked = slot_h.take()
+            if parked is not None:
+                dh = parked if dh is None else dh + parked
+        dw2, acc2, ret2 = _grad_dest(w2, ctx.needs_input_grad[3])
+        dht = torch.empty_like(h)
+        if dx is None:
+            dx = torch.zeros_like(h)
+        K.rmsnorm_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), dht, dw2, dw_accumulate=acc2)
+        dw1, acc1, ret1 = _grad_dest(w1, ctx.needs_input_grad[2])
+        dy = torch.empty_like(y)
+        K.rmsnorm_bwd(y, w1, r1, dht, None, dy, dw1, dw_accumulate=acc1)
+        if slot_res is not None:
+            slot_res.put(dht)
+            return None, dy, ret1, ret2, None, None, None, None
+        return dht, dy, ret1, ret2, None, None, None, None
+
+
 class LayerNormFn(torch.autograd.Function):
     """nn.LayerNorm (SigLIP layer_norm1/2/post_layernorm [3p]; Ego3D head.1, modeling_spatialvla.py:61)."""
 

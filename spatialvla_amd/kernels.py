@@ -363,6 +363,20 @@ def add_rmsnorm_fwd(res, yin, w, eps, h, rstd):
                                          rstd.data_ptr(), _stream()), "add_rmsnorm_fwd")
 
 
+def add_rmsnorm2_fwd_train(res, yin, w1, w2, eps1, eps2, h, x, rstd1, rstd2):
+    """h = bf16(res + rms(yin; w1)), x = rms(h; w2) and both rows' rstd (svla_add_rmsnorm2_fwd_train)."""
+    rows, N = yin.shape
+    for t, n in ((res, "res"), (yin, "yin"), (w1, "w1"), (w2, "w2"), (h, "h"), (x, "x")):
+        _chk_bf16(t, n)
+    _req(res.shape == yin.shape == h.shape == x.shape and res.is_contiguous() and yin.is_contiguous()
+         and h.is_contiguous() and x.is_contiguous(), "add_rmsnorm2_train: shapes")
+    _req(rstd1.numel() >= rows and rstd2.numel() >= rows and rstd1.dtype == rstd2.dtype == torch.float32,
+         "add_rmsnorm2_train: rstd buffers")
+    L.check(L.lib().svla_add_rmsnorm2_fwd_train(rows, N, res.data_ptr(), yin.data_ptr(), w1.data_ptr(), w2.data_ptr(),
+                                                float(eps1), float(eps2), h.data_ptr(), x.data_ptr(),
+                                                rstd1.data_ptr(), rstd2.data_ptr(), _stream()), "add_rmsnorm2_fwd_train")
+
+
 RPB = 16  # rows per block of the norm backward kernels (norms.hip)
 
 

@@ -12,6 +12,7 @@ path (QKV GEMM -> attention with RoPE on load -> O GEMM) is used; the plug-in is
 hand in already-rotated q/k/v as the reference does.
 """
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -224,6 +225,11 @@ def _rope_theta(config):
     return float(th)
 
 
+# training forward: the post-attention + pre-feedforward norm pair as one launch (Fn.AddRMSNorm2Fn); False = the two
+# separate Functions (A/B and bitwise tests)
+FUSED_NORM_PAIR = [os.environ.get("SVLA_FUSED_NORM_PAIR", "1") != "0"]
+
+
 class Gemma2DecoderLayer(nn.Module):
     def __init__(self, config, layer_idx: int):
         super().__init__()
@@ -254,8 +260,17 @@ class Gemma2DecoderLayer(nn.Module):
         s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
         x = self.input_layernorm(hidden_states, s1)
         a = self.self_attn(x, attention_mask, rope, cache, attn_sink)
-        h = self.post_attention_layernorm.add_forward(hidden_states, a, s1)
-        x = self.pre_feedforward_layernorm(h, s2)
+        pa, pf = self.post_attention_layernorm, self.pre_feedforward_layernorm
+        if FUSED_NORM_PAIR[0]:
+            # post-attention norm + residual and the pre-feedforward norm in one launch (AddRMSNorm2Fn); h's
+            # residual-branch gradient arrives through s2 (post_feedforward's add parks it there)
+            shp = a.shape
+            h, x = Fn.AddRMSNorm2Fn.apply(hidden_states.reshape(-1, shp[-1]), a.reshape(-1, shp[-1]), pa.weight,
+                                          pf.weight, pa.eps, pf.eps, s1, s2)
+            h, x = h.view(shp), x.view(shp)
+        else:
+            h = pa.add_forward(hidden_states, a, s1)
+            x = pf(h, s2)
         m = self.mlp(x)
         return self.post_feedforward_layernorm.add_forward(h, m, s2)
 

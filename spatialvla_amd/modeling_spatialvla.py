@@ -135,7 +135,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
         self.vocab_size = config.text_config.vocab_size
         self.language_model = language_model or Gemma2ForCausalLM(config.text_config)
         if config.use_vision_zoe:
-            from transformers import ZoeDepthForDepthEstimation  # frozen 3p depth estimator (stock torch ops)
+            from transformers import ZoeDepthForDepthEstimation  # frozen 3p module tree; compute patched by zoe_fast
             self.vision_zoe_model = vision_zoe_model or ZoeDepthForDepthEstimation(config.vision_zoe_config)
             zoe_fast.install(self.vision_zoe_model)
             self.position_embedding_3d = Ego3DPositionEmbeddingMLP(

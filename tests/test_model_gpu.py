@@ -145,6 +145,28 @@ def test_tiny_vs_oracle_random_batch(cuda):
     assert res["argmax_agree_confident"] == 1.0
 
 
+def test_fused_norm_pair_bitwise(cuda):
+    """The training forward's post-attention + pre-feedforward norm pair in one launch (AddRMSNorm2Fn) gives the
+    loss, logits and every gradient of the two separate Functions bit for bit."""
+    from spatialvla_amd import modeling_gemma2 as MG, presets
+    cfgd = H.cfg_dict("tiny")
+    b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=2, seed=5), cuda)
+    depth = torch.rand(2, 1, 224, 224, generator=torch.Generator().manual_seed(3)).mul(3).add(0.5).to(cuda)
+    out = {}
+    for fused in (True, False):
+        MG.FUSED_NORM_PAIR[0] = fused
+        try:
+            model = H.build_hip_model(cfgd, "cuda:0")
+            out[fused] = H.run_hip(model, b, depth=depth)
+        finally:
+            MG.FUSED_NORM_PAIR[0] = True
+    (l1, lg1, g1, _), (l0, lg0, g0, _) = out[True], out[False]
+    assert torch.equal(l1, l0) and torch.equal(lg1, lg0)
+    assert g1.keys() == g0.keys()
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n
+
+
 def _layer4b_model(li, cuda):
     from spatialvla_amd import SpatialVLAConfig
     from spatialvla_amd import presets

@@ -1,20 +1,32 @@
-# Measurement on one MI355X: bench line, rocprofv3 kernel-trace/stats, PMC HBM traffic passes.
-# Raw rocprof output is condensed on the box (tools/summarize_profile.py) and then deleted.
+#!/bin/bash
+# One GPU-box call (round 3, reused in round 4): GPU tests, the bench line, a rocprofv3 kernel trace of the training step, the HBM
+# PMC passes of the dominant kernel and the isolated Gemma2 block breakdown.  Every GPU step has its own time limit;
+# the script stops at the first step that crashed or timed out (exit status > 1; 1 = pytest test failures).
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${TAG:-r2}
+TAG=${TAG:-r4}
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-decode > $O/bench_prof.json 2> $O/bench_prof.err && \
-python tools/summarize_profile.py trace /tmp/prof_$TAG $O/$TAG > $O/trace_summary.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d /tmp/pmc_fetch -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode > $O/pmc_fetch.json 2> $O/pmc_fetch.err && \
-python tools/summarize_profile.py pmc /tmp/pmc_fetch $O/${TAG}_pmc_fetch > $O/pmc_fetch_summary.log 2>&1 && \
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d /tmp/pmc_write -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode > $O/pmc_write.json 2> $O/pmc_write.err && \
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 $secs "$@"
+  local rc=$?
+  echo "[$name] rc=$rc"
+  if [ $rc -gt 1 ]; then echo "[$name] stopping: crash or timeout"; exit $rc; fi
+  return 0
+}
+if [ -z "$SKIP_TESTS" ]; then
+  step pytest 900 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $O/pytest_gpu.txt 2>&1
+  tail -3 $O/pytest_gpu.txt
+fi
+step bench 900 python -u bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err
+cat $O/bench.json | head -c 3000; echo
+step trace 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_$TAG -o trace --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-decode --no-fp8-leg > $O/bench_prof.json 2> $O/bench_prof.err
+python tools/summarize_profile.py trace /tmp/prof_$TAG $O/$TAG > $O/trace_summary.log 2>&1
+step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d /tmp/pmc_fetch -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode --no-fp8-leg > $O/pmc_fetch.json 2> $O/pmc_fetch.err
+python tools/summarize_profile.py pmc /tmp/pmc_fetch $O/${TAG}_pmc_fetch > $O/pmc_fetch_summary.log 2>&1
+step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d /tmp/pmc_write -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-decode --no-fp8-leg > $O/pmc_write.json 2> $O/pmc_write.err
 python tools/summarize_profile.py pmc /tmp/pmc_write $O/${TAG}_pmc_write > $O/pmc_write_summary.log 2>&1
-rc=$?
-[ $rc -eq 0 ] && timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/blk_$TAG -o blk --output-format csv -- python3 tools/block_ab.py 1 1 5 > $O/block.log 2>&1 && \
+step block 300 rocprofv3 --kernel-trace -d /tmp/blk_$TAG -o blk --output-format csv -- python3 tools/block_ab.py 1 1 5 > $O/block.log 2>&1
 python tools/block_trace.py /tmp/blk_$TAG > $O/${TAG}_block_breakdown.txt 2>&1
-rc=$?
 ls -la $O
-exit $rc
