@@ -177,9 +177,15 @@ def gemma2_block_roofline(model, B, L, device, iters=20):
     flops = 3 * 2.0 * mac_tok * B * L
     stream = torch.cuda.current_stream()
     fwd_ms, tot_ms = [], []
+    # the layer's ~28 launches (and autograd's backward dispatch) are queued behind a GPU-side spin, so the events
+    # bracket the kernels' back-to-back execution rather than the Python dispatch of the first launches; the training
+    # step this layer sits in is GPU-bound (its ~2000 launches queue ahead of the GPU)
+    spin = getattr(torch.cuda, "_sleep", None)
     for it in range(iters + 2):
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         x.grad = None
+        if spin is not None:
+            spin(int(20e6))  # ~10 ms of GPU cycles
         e0.record(stream)
         y = layer(x, mask, rope)
         e1.record(stream)

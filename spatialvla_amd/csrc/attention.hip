@@ -510,565 +510,6 @@ __global__ __launch_bounds__(256 * NH, (D == 64 && SVLA_ATT_RS64) ? SVLA_ATT_WPE
   }
 }
 
-// ================================================================== forward, head_dim 256, 32x32x16 MFMA
-// The Gemma2 forward (softcap, GQA pairs) on v_mfma_f32_32x32x16_bf16: every K / V fragment read from LDS feeds 32
-// queries (the 16x16x32 kernel above feeds 16, so its LDS reads ran at the MFMA rate: LDS-bound).
-//  * Block = 4 waves, one per SIMD (the whole 512-register file: O^T 256 x 32 accumulators + Q^T fragments) =
-//    (64 queries, the 2 query heads sharing a kv head, batch); wave w: head 2hg + (w >> 1), queries
-//    q0 + 32 (w & 1) + (lane & 31).
-//  * S^T = K Q^T per 32-key half tile: A = K rows (ds_read_b128), B = Q^T held in registers; the accumulator's column
-//    is the lane's query and its 16 registers 16 keys.  Those registers, packed to bf16, ARE the B operand P^T of
-//    O^T += V^T P^T (cdna_hip_programming.md §3, k order permuted: element j of lane half h is key
-//    16s + 8(j>>2) + 4h + (j&3)); V^T is read with ds_read_b64_tr_b16 in that key order.
-//  * Softcap without a running max (CapExp above): p = exp(cap tanh(s scale / cap)), no rescale of O.
-//  * K / V tiles by LDS-DMA into two stages (tile kt+1 lands during tile kt), 512-B rows with the chunk swizzle
-//    sw32, conflict-free for the 32-row b128 reads and the 4-row x 32-column transposed reads.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef short v8s __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ int sw32(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-
-// [64 rows][256] bf16 tile -> LDS (512-B rows, chunk p of row r holds global chunk p ^ sw32(r)), 4 waves x 8 pieces.
-// Piece i of wave w holds rows r0 + 8i (r0 = 2w + lane/32): the row step is the wave-uniform soffset, and the lane
-// offset takes one of two values (sw32 depends on r mod 16), so no per-piece offsets are kept live across the loop
-// (hoisted, they spill, and each reload's vmcnt(0) serialises the DMA issue)
-__device__ __forceinline__ void glds_tile32(char* lds, const bf16_t* base, int64_t ld, int nrows, int w, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(base);
-  const int r0 = 2 * w + (lane >> 5), c = lane & 31;
-  const uint32_t rb = (uint32_t)(r0 * ld * 2);
-  const uint32_t a0 = rb + ((c ^ sw32(r0)) << 4), a1 = rb + ((c ^ sw32(r0 + 8)) << 4);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t voff = r0 + 8 * i < nrows ? ((i & 1) ? a1 : a0) : SVLA_OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(lds + (w + 4 * i) * 1024), 16, voff,
-                                             (int)(16 * i * ld), 0, 0);
-  }
-}
-
-// The O^T accumulators of attn_fwd32_kernel live in the fixed AGPRs a[16d : 16d+15] (d-tile d = 0..7) and are
-// touched only by these statements (the gemm4 scheme, gemm.hip agpr_mfma): compiler-allocated, they became
-// branch-merged / loop-carried values that hipcc parked in arch VGPRs and copied into AGPRs around every MFMA.
-// Each MFMA names exactly its 16 AGPRs as clobbers (a whole-file clobber would make the hazard recognizer pad every
-// MFMA with s_nops); MFMA -> v_accvgpr_read is fenced with o_fence().
-template <int X, int N, typename Fn>
-__device__ __forceinline__ void a_static_for(Fn&& f) {
-  if constexpr (X < N) {
-    f(std::integral_constant<int, X>{});
-    a_static_for<X + 1, N>(f);
-  }
-}
-template <int DT>
-__device__ __forceinline__ void o_mfma(const bf16x8& a, const bf16x8& b);
-template <>
-__device__ __forceinline__ void o_mfma<0>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b)
-               : "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15");
-}
-template <>
-__device__ __forceinline__ void o_mfma<1>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[16:31], %0, %1, a[16:31]" ::"v"(a), "v"(b)
-               : "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31");
-}
-template <>
-__device__ __forceinline__ void o_mfma<2>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[32:47], %0, %1, a[32:47]" ::"v"(a), "v"(b)
-               : "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47");
-}
-template <>
-__device__ __forceinline__ void o_mfma<3>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[48:63], %0, %1, a[48:63]" ::"v"(a), "v"(b)
-               : "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63");
-}
-template <>
-__device__ __forceinline__ void o_mfma<4>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[64:79], %0, %1, a[64:79]" ::"v"(a), "v"(b)
-               : "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79");
-}
-template <>
-__device__ __forceinline__ void o_mfma<5>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[80:95], %0, %1, a[80:95]" ::"v"(a), "v"(b)
-               : "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95");
-}
-template <>
-__device__ __forceinline__ void o_mfma<6>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[96:111], %0, %1, a[96:111]" ::"v"(a), "v"(b)
-               : "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111");
-}
-template <>
-__device__ __forceinline__ void o_mfma<7>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[112:127], %0, %1, a[112:127]" ::"v"(a), "v"(b)
-               : "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127");
-}
-__device__ __forceinline__ void o_zero() {
-  asm volatile("v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\tv_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\tv_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\tv_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\tv_accvgpr_write_b32 a16, 0\n\tv_accvgpr_write_b32 a17, 0\n\tv_accvgpr_write_b32 a18, 0\n\tv_accvgpr_write_b32 a19, 0\n\tv_accvgpr_write_b32 a20, 0\n\tv_accvgpr_write_b32 a21, 0\n\tv_accvgpr_write_b32 a22, 0\n\tv_accvgpr_write_b32 a23, 0\n\tv_accvgpr_write_b32 a24, 0\n\tv_accvgpr_write_b32 a25, 0\n\tv_accvgpr_write_b32 a26, 0\n\tv_accvgpr_write_b32 a27, 0\n\tv_accvgpr_write_b32 a28, 0\n\tv_accvgpr_write_b32 a29, 0\n\tv_accvgpr_write_b32 a30, 0\n\tv_accvgpr_write_b32 a31, 0\n\tv_accvgpr_write_b32 a32, 0\n\tv_accvgpr_write_b32 a33, 0\n\tv_accvgpr_write_b32 a34, 0\n\tv_accvgpr_write_b32 a35, 0\n\tv_accvgpr_write_b32 a36, 0\n\tv_accvgpr_write_b32 a37, 0\n\tv_accvgpr_write_b32 a38, 0\n\tv_accvgpr_write_b32 a39, 0\n\tv_accvgpr_write_b32 a40, 0\n\tv_accvgpr_write_b32 a41, 0\n\tv_accvgpr_write_b32 a42, 0\n\tv_accvgpr_write_b32 a43, 0\n\tv_accvgpr_write_b32 a44, 0\n\tv_accvgpr_write_b32 a45, 0\n\tv_accvgpr_write_b32 a46, 0\n\tv_accvgpr_write_b32 a47, 0\n\tv_accvgpr_write_b32 a48, 0\n\tv_accvgpr_write_b32 a49, 0\n\tv_accvgpr_write_b32 a50, 0\n\tv_accvgpr_write_b32 a51, 0\n\tv_accvgpr_write_b32 a52, 0\n\tv_accvgpr_write_b32 a53, 0\n\tv_accvgpr_write_b32 a54, 0\n\tv_accvgpr_write_b32 a55, 0\n\tv_accvgpr_write_b32 a56, 0\n\tv_accvgpr_write_b32 a57, 0\n\tv_accvgpr_write_b32 a58, 0\n\tv_accvgpr_write_b32 a59, 0\n\tv_accvgpr_write_b32 a60, 0\n\tv_accvgpr_write_b32 a61, 0\n\tv_accvgpr_write_b32 a62, 0\n\tv_accvgpr_write_b32 a63, 0\n\tv_accvgpr_write_b32 a64, 0\n\tv_accvgpr_write_b32 a65, 0\n\tv_accvgpr_write_b32 a66, 0\n\tv_accvgpr_write_b32 a67, 0\n\tv_accvgpr_write_b32 a68, 0\n\tv_accvgpr_write_b32 a69, 0\n\tv_accvgpr_write_b32 a70, 0\n\tv_accvgpr_write_b32 a71, 0\n\tv_accvgpr_write_b32 a72, 0\n\tv_accvgpr_write_b32 a73, 0\n\tv_accvgpr_write_b32 a74, 0\n\tv_accvgpr_write_b32 a75, 0\n\tv_accvgpr_write_b32 a76, 0\n\tv_accvgpr_write_b32 a77, 0\n\tv_accvgpr_write_b32 a78, 0\n\tv_accvgpr_write_b32 a79, 0\n\tv_accvgpr_write_b32 a80, 0\n\tv_accvgpr_write_b32 a81, 0\n\tv_accvgpr_write_b32 a82, 0\n\tv_accvgpr_write_b32 a83, 0\n\tv_accvgpr_write_b32 a84, 0\n\tv_accvgpr_write_b32 a85, 0\n\tv_accvgpr_write_b32 a86, 0\n\tv_accvgpr_write_b32 a87, 0\n\tv_accvgpr_write_b32 a88, 0\n\tv_accvgpr_write_b32 a89, 0\n\tv_accvgpr_write_b32 a90, 0\n\tv_accvgpr_write_b32 a91, 0\n\tv_accvgpr_write_b32 a92, 0\n\tv_accvgpr_write_b32 a93, 0\n\tv_accvgpr_write_b32 a94, 0\n\tv_accvgpr_write_b32 a95, 0\n\tv_accvgpr_write_b32 a96, 0\n\tv_accvgpr_write_b32 a97, 0\n\tv_accvgpr_write_b32 a98, 0\n\tv_accvgpr_write_b32 a99, 0\n\tv_accvgpr_write_b32 a100, 0\n\tv_accvgpr_write_b32 a101, 0\n\tv_accvgpr_write_b32 a102, 0\n\tv_accvgpr_write_b32 a103, 0\n\tv_accvgpr_write_b32 a104, 0\n\tv_accvgpr_write_b32 a105, 0\n\tv_accvgpr_write_b32 a106, 0\n\tv_accvgpr_write_b32 a107, 0\n\tv_accvgpr_write_b32 a108, 0\n\tv_accvgpr_write_b32 a109, 0\n\tv_accvgpr_write_b32 a110, 0\n\tv_accvgpr_write_b32 a111, 0\n\tv_accvgpr_write_b32 a112, 0\n\tv_accvgpr_write_b32 a113, 0\n\tv_accvgpr_write_b32 a114, 0\n\tv_accvgpr_write_b32 a115, 0\n\tv_accvgpr_write_b32 a116, 0\n\tv_accvgpr_write_b32 a117, 0\n\tv_accvgpr_write_b32 a118, 0\n\tv_accvgpr_write_b32 a119, 0\n\tv_accvgpr_write_b32 a120, 0\n\tv_accvgpr_write_b32 a121, 0\n\tv_accvgpr_write_b32 a122, 0\n\tv_accvgpr_write_b32 a123, 0\n\tv_accvgpr_write_b32 a124, 0\n\tv_accvgpr_write_b32 a125, 0\n\tv_accvgpr_write_b32 a126, 0\n\tv_accvgpr_write_b32 a127, 0\n\ts_nop 1" ::: "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127");
-}
-// XDL write -> v_accvgpr_read: 18 wait states for the 16-pass 32x32x16 (24 given)
-__device__ __forceinline__ void o_fence() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-template <int R>
-__device__ __forceinline__ float o_get();
-template <> __device__ __forceinline__ float o_get<0>() { float x; asm volatile("v_accvgpr_read_b32 %0, a0" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<1>() { float x; asm volatile("v_accvgpr_read_b32 %0, a1" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<2>() { float x; asm volatile("v_accvgpr_read_b32 %0, a2" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<3>() { float x; asm volatile("v_accvgpr_read_b32 %0, a3" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<4>() { float x; asm volatile("v_accvgpr_read_b32 %0, a4" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<5>() { float x; asm volatile("v_accvgpr_read_b32 %0, a5" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<6>() { float x; asm volatile("v_accvgpr_read_b32 %0, a6" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<7>() { float x; asm volatile("v_accvgpr_read_b32 %0, a7" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<8>() { float x; asm volatile("v_accvgpr_read_b32 %0, a8" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<9>() { float x; asm volatile("v_accvgpr_read_b32 %0, a9" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<10>() { float x; asm volatile("v_accvgpr_read_b32 %0, a10" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<11>() { float x; asm volatile("v_accvgpr_read_b32 %0, a11" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<12>() { float x; asm volatile("v_accvgpr_read_b32 %0, a12" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<13>() { float x; asm volatile("v_accvgpr_read_b32 %0, a13" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<14>() { float x; asm volatile("v_accvgpr_read_b32 %0, a14" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<15>() { float x; asm volatile("v_accvgpr_read_b32 %0, a15" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<16>() { float x; asm volatile("v_accvgpr_read_b32 %0, a16" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<17>() { float x; asm volatile("v_accvgpr_read_b32 %0, a17" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<18>() { float x; asm volatile("v_accvgpr_read_b32 %0, a18" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<19>() { float x; asm volatile("v_accvgpr_read_b32 %0, a19" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<20>() { float x; asm volatile("v_accvgpr_read_b32 %0, a20" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<21>() { float x; asm volatile("v_accvgpr_read_b32 %0, a21" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<22>() { float x; asm volatile("v_accvgpr_read_b32 %0, a22" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<23>() { float x; asm volatile("v_accvgpr_read_b32 %0, a23" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<24>() { float x; asm volatile("v_accvgpr_read_b32 %0, a24" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<25>() { float x; asm volatile("v_accvgpr_read_b32 %0, a25" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<26>() { float x; asm volatile("v_accvgpr_read_b32 %0, a26" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<27>() { float x; asm volatile("v_accvgpr_read_b32 %0, a27" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<28>() { float x; asm volatile("v_accvgpr_read_b32 %0, a28" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<29>() { float x; asm volatile("v_accvgpr_read_b32 %0, a29" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<30>() { float x; asm volatile("v_accvgpr_read_b32 %0, a30" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<31>() { float x; asm volatile("v_accvgpr_read_b32 %0, a31" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<32>() { float x; asm volatile("v_accvgpr_read_b32 %0, a32" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<33>() { float x; asm volatile("v_accvgpr_read_b32 %0, a33" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<34>() { float x; asm volatile("v_accvgpr_read_b32 %0, a34" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<35>() { float x; asm volatile("v_accvgpr_read_b32 %0, a35" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<36>() { float x; asm volatile("v_accvgpr_read_b32 %0, a36" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<37>() { float x; asm volatile("v_accvgpr_read_b32 %0, a37" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<38>() { float x; asm volatile("v_accvgpr_read_b32 %0, a38" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<39>() { float x; asm volatile("v_accvgpr_read_b32 %0, a39" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<40>() { float x; asm volatile("v_accvgpr_read_b32 %0, a40" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<41>() { float x; asm volatile("v_accvgpr_read_b32 %0, a41" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<42>() { float x; asm volatile("v_accvgpr_read_b32 %0, a42" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<43>() { float x; asm volatile("v_accvgpr_read_b32 %0, a43" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<44>() { float x; asm volatile("v_accvgpr_read_b32 %0, a44" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<45>() { float x; asm volatile("v_accvgpr_read_b32 %0, a45" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<46>() { float x; asm volatile("v_accvgpr_read_b32 %0, a46" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<47>() { float x; asm volatile("v_accvgpr_read_b32 %0, a47" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<48>() { float x; asm volatile("v_accvgpr_read_b32 %0, a48" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<49>() { float x; asm volatile("v_accvgpr_read_b32 %0, a49" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<50>() { float x; asm volatile("v_accvgpr_read_b32 %0, a50" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<51>() { float x; asm volatile("v_accvgpr_read_b32 %0, a51" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<52>() { float x; asm volatile("v_accvgpr_read_b32 %0, a52" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<53>() { float x; asm volatile("v_accvgpr_read_b32 %0, a53" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<54>() { float x; asm volatile("v_accvgpr_read_b32 %0, a54" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<55>() { float x; asm volatile("v_accvgpr_read_b32 %0, a55" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<56>() { float x; asm volatile("v_accvgpr_read_b32 %0, a56" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<57>() { float x; asm volatile("v_accvgpr_read_b32 %0, a57" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<58>() { float x; asm volatile("v_accvgpr_read_b32 %0, a58" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<59>() { float x; asm volatile("v_accvgpr_read_b32 %0, a59" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<60>() { float x; asm volatile("v_accvgpr_read_b32 %0, a60" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<61>() { float x; asm volatile("v_accvgpr_read_b32 %0, a61" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<62>() { float x; asm volatile("v_accvgpr_read_b32 %0, a62" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<63>() { float x; asm volatile("v_accvgpr_read_b32 %0, a63" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<64>() { float x; asm volatile("v_accvgpr_read_b32 %0, a64" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<65>() { float x; asm volatile("v_accvgpr_read_b32 %0, a65" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<66>() { float x; asm volatile("v_accvgpr_read_b32 %0, a66" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<67>() { float x; asm volatile("v_accvgpr_read_b32 %0, a67" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<68>() { float x; asm volatile("v_accvgpr_read_b32 %0, a68" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<69>() { float x; asm volatile("v_accvgpr_read_b32 %0, a69" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<70>() { float x; asm volatile("v_accvgpr_read_b32 %0, a70" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<71>() { float x; asm volatile("v_accvgpr_read_b32 %0, a71" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<72>() { float x; asm volatile("v_accvgpr_read_b32 %0, a72" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<73>() { float x; asm volatile("v_accvgpr_read_b32 %0, a73" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<74>() { float x; asm volatile("v_accvgpr_read_b32 %0, a74" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<75>() { float x; asm volatile("v_accvgpr_read_b32 %0, a75" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<76>() { float x; asm volatile("v_accvgpr_read_b32 %0, a76" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<77>() { float x; asm volatile("v_accvgpr_read_b32 %0, a77" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<78>() { float x; asm volatile("v_accvgpr_read_b32 %0, a78" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<79>() { float x; asm volatile("v_accvgpr_read_b32 %0, a79" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<80>() { float x; asm volatile("v_accvgpr_read_b32 %0, a80" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<81>() { float x; asm volatile("v_accvgpr_read_b32 %0, a81" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<82>() { float x; asm volatile("v_accvgpr_read_b32 %0, a82" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<83>() { float x; asm volatile("v_accvgpr_read_b32 %0, a83" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<84>() { float x; asm volatile("v_accvgpr_read_b32 %0, a84" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<85>() { float x; asm volatile("v_accvgpr_read_b32 %0, a85" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<86>() { float x; asm volatile("v_accvgpr_read_b32 %0, a86" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<87>() { float x; asm volatile("v_accvgpr_read_b32 %0, a87" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<88>() { float x; asm volatile("v_accvgpr_read_b32 %0, a88" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<89>() { float x; asm volatile("v_accvgpr_read_b32 %0, a89" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<90>() { float x; asm volatile("v_accvgpr_read_b32 %0, a90" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<91>() { float x; asm volatile("v_accvgpr_read_b32 %0, a91" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<92>() { float x; asm volatile("v_accvgpr_read_b32 %0, a92" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<93>() { float x; asm volatile("v_accvgpr_read_b32 %0, a93" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<94>() { float x; asm volatile("v_accvgpr_read_b32 %0, a94" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<95>() { float x; asm volatile("v_accvgpr_read_b32 %0, a95" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<96>() { float x; asm volatile("v_accvgpr_read_b32 %0, a96" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<97>() { float x; asm volatile("v_accvgpr_read_b32 %0, a97" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<98>() { float x; asm volatile("v_accvgpr_read_b32 %0, a98" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<99>() { float x; asm volatile("v_accvgpr_read_b32 %0, a99" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<100>() { float x; asm volatile("v_accvgpr_read_b32 %0, a100" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<101>() { float x; asm volatile("v_accvgpr_read_b32 %0, a101" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<102>() { float x; asm volatile("v_accvgpr_read_b32 %0, a102" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<103>() { float x; asm volatile("v_accvgpr_read_b32 %0, a103" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<104>() { float x; asm volatile("v_accvgpr_read_b32 %0, a104" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<105>() { float x; asm volatile("v_accvgpr_read_b32 %0, a105" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<106>() { float x; asm volatile("v_accvgpr_read_b32 %0, a106" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<107>() { float x; asm volatile("v_accvgpr_read_b32 %0, a107" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<108>() { float x; asm volatile("v_accvgpr_read_b32 %0, a108" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<109>() { float x; asm volatile("v_accvgpr_read_b32 %0, a109" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<110>() { float x; asm volatile("v_accvgpr_read_b32 %0, a110" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<111>() { float x; asm volatile("v_accvgpr_read_b32 %0, a111" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<112>() { float x; asm volatile("v_accvgpr_read_b32 %0, a112" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<113>() { float x; asm volatile("v_accvgpr_read_b32 %0, a113" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<114>() { float x; asm volatile("v_accvgpr_read_b32 %0, a114" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<115>() { float x; asm volatile("v_accvgpr_read_b32 %0, a115" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<116>() { float x; asm volatile("v_accvgpr_read_b32 %0, a116" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<117>() { float x; asm volatile("v_accvgpr_read_b32 %0, a117" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<118>() { float x; asm volatile("v_accvgpr_read_b32 %0, a118" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<119>() { float x; asm volatile("v_accvgpr_read_b32 %0, a119" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<120>() { float x; asm volatile("v_accvgpr_read_b32 %0, a120" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<121>() { float x; asm volatile("v_accvgpr_read_b32 %0, a121" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<122>() { float x; asm volatile("v_accvgpr_read_b32 %0, a122" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<123>() { float x; asm volatile("v_accvgpr_read_b32 %0, a123" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<124>() { float x; asm volatile("v_accvgpr_read_b32 %0, a124" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<125>() { float x; asm volatile("v_accvgpr_read_b32 %0, a125" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<126>() { float x; asm volatile("v_accvgpr_read_b32 %0, a126" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<127>() { float x; asm volatile("v_accvgpr_read_b32 %0, a127" : "=v"(x)); return x; }
-
-// S^T accumulators of the two key halves: a[128:143] (half 0) and a[144:159] (half 1); the first k-step starts
-// from 0.  No MFMA of hipcc's own remains in the kernel, so nothing else is placed in the accumulator file
-// (audit: no v_accvgpr_* outside ;;#ASMSTART blocks).
-template <int S, bool FIRST>
-__device__ __forceinline__ void s_mfma(const bf16x8& a, const bf16x8& b);
-template <>
-__device__ __forceinline__ void s_mfma<0, true>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 a[128:143], %0, %1, 0" ::"v"(a), "v"(b) : "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143");
-}
-template <>
-__device__ __forceinline__ void s_mfma<0, false>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 a[128:143], %0, %1, a[128:143]" ::"v"(a), "v"(b) : "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143");
-}
-template <>
-__device__ __forceinline__ void s_mfma<1, true>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 a[144:159], %0, %1, 0" ::"v"(a), "v"(b) : "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159");
-}
-template <>
-__device__ __forceinline__ void s_mfma<1, false>(const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 a[144:159], %0, %1, a[144:159]" ::"v"(a), "v"(b) : "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159");
-}
-template <> __device__ __forceinline__ float o_get<128>() { float x; asm volatile("v_accvgpr_read_b32 %0, a128" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<129>() { float x; asm volatile("v_accvgpr_read_b32 %0, a129" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<130>() { float x; asm volatile("v_accvgpr_read_b32 %0, a130" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<131>() { float x; asm volatile("v_accvgpr_read_b32 %0, a131" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<132>() { float x; asm volatile("v_accvgpr_read_b32 %0, a132" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<133>() { float x; asm volatile("v_accvgpr_read_b32 %0, a133" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<134>() { float x; asm volatile("v_accvgpr_read_b32 %0, a134" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<135>() { float x; asm volatile("v_accvgpr_read_b32 %0, a135" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<136>() { float x; asm volatile("v_accvgpr_read_b32 %0, a136" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<137>() { float x; asm volatile("v_accvgpr_read_b32 %0, a137" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<138>() { float x; asm volatile("v_accvgpr_read_b32 %0, a138" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<139>() { float x; asm volatile("v_accvgpr_read_b32 %0, a139" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<140>() { float x; asm volatile("v_accvgpr_read_b32 %0, a140" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<141>() { float x; asm volatile("v_accvgpr_read_b32 %0, a141" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<142>() { float x; asm volatile("v_accvgpr_read_b32 %0, a142" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<143>() { float x; asm volatile("v_accvgpr_read_b32 %0, a143" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<144>() { float x; asm volatile("v_accvgpr_read_b32 %0, a144" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<145>() { float x; asm volatile("v_accvgpr_read_b32 %0, a145" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<146>() { float x; asm volatile("v_accvgpr_read_b32 %0, a146" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<147>() { float x; asm volatile("v_accvgpr_read_b32 %0, a147" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<148>() { float x; asm volatile("v_accvgpr_read_b32 %0, a148" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<149>() { float x; asm volatile("v_accvgpr_read_b32 %0, a149" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<150>() { float x; asm volatile("v_accvgpr_read_b32 %0, a150" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<151>() { float x; asm volatile("v_accvgpr_read_b32 %0, a151" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<152>() { float x; asm volatile("v_accvgpr_read_b32 %0, a152" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<153>() { float x; asm volatile("v_accvgpr_read_b32 %0, a153" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<154>() { float x; asm volatile("v_accvgpr_read_b32 %0, a154" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<155>() { float x; asm volatile("v_accvgpr_read_b32 %0, a155" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<156>() { float x; asm volatile("v_accvgpr_read_b32 %0, a156" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<157>() { float x; asm volatile("v_accvgpr_read_b32 %0, a157" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<158>() { float x; asm volatile("v_accvgpr_read_b32 %0, a158" : "=v"(x)); return x; }
-template <> __device__ __forceinline__ float o_get<159>() { float x; asm volatile("v_accvgpr_read_b32 %0, a159" : "=v"(x)); return x; }
-
-#ifndef ATT32_STAMPS
-#define ATT32_STAMPS 0
-#endif
-#if ATT32_STAMPS
-// diagnostic build only: per block (wave 0) cycles of prologue / tile-top wait / phases A-D / epilogue
-__device__ unsigned long long att32_stamps[4096][8];
-#define A32_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define A32_T(v)
-#endif
-template <bool CAP>
-__global__ __launch_bounds__(256, 1) void attn_fwd32_kernel(svla_attn_args a, bf16_t* __restrict__ out, int64_t ldo,
-                                                             float* __restrict__ lse) {
-  constexpr int D = 256, TB = 64 * 512, STAGE = 2 * TB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint8_t* lcls = (uint8_t*)(smem + 2 * STAGE);
-  const int L = a.L;
-  int qt, hg, b;
-  block_coords((L + 63) / 64, a.Hq / 2, qt, hg, b);
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int h = 2 * hg + (w >> 1);
-  const int grp = a.Hq / a.Hkv, hk = h / grp;
-  const int qi = qt * 64 + 32 * (w & 1) + r;
-  const bool qvalid = qi < L;
-  const bool window_free = a.sliding_window <= 0 || a.sliding_window >= L;
-  const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
-  const bf16_t* vbase = (const bf16_t*)a.v + (int64_t)b * L * a.ldv + (int64_t)hk * D;
-
-#if ATT32_STAMPS
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  A32_T(tk0);
-#endif
-  load_classes(lcls, a.kv_class ? a.kv_class + (int64_t)b * L : nullptr, L, t, 256);
-  // Q^T fragments: B[k = d][col = q], lane (r, hh) holds Q[qi][16 ks + 8 hh + j]
-  bf16x8 qf[16];
-  {
-    const bf16_t* qrow = (const bf16_t*)a.q + ((int64_t)b * L + (qvalid ? qi : 0)) * a.ldq + (int64_t)h * D + 8 * hh;
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (qvalid) v = *reinterpret_cast<const u32x4*>(qrow + 16 * ks);
-      qf[ks] = __builtin_bit_cast(bf16x8, v);
-    }
-  }
-  const int nkt = (L + 63) / 64;
-  glds_tile32(smem, kbase, a.ldk, L, w, lane);
-  glds_tile32(smem + TB, vbase, a.ldv, L, w, lane);
-
-  o_zero();
-  float lsum = 0.f;
-  const CapExp ce(a.scale, CAP ? a.softcap : 1.f);
-  // per-lane LDS addressing: K row reads (row 32 kb + r, chunk 2 ks + hh); V transposed reads (lane 4q + p of its
-  // 16-lane group g: rows 16 s + 4 hh + q (+8), columns 32 dt + 16 (g & 1) + 4 p)
-  const int swr = sw32(r);
-  const int q4 = (lane >> 2) & 3, p4 = lane & 3, g1 = (lane >> 4) & 1;
-
-  // p = exp(softcapped score) of score e of a half, unmasked; register e holds key
-  // k0 + 32 kb + (e & 3) + 8 (e >> 2) + 4 hh
-  // The score -> p chain (CAP: exp2, add, rcp, fma, exp2) is three dependent transcendentals long: run one chain
-  // per MFMA gap and the in-order wave stalls the matrix pipe for its whole latency (phase stamps: the two softmax
-  // phases took 3-4x their MFMA time).  So the 16 chains of a half are skewed over the gaps: gap g runs stage 1 of
-  // score g, stage 2 of score g-2 and stage 3 of score g-4 (one transcendental each), four gaps of drain after.
-  struct SmState {
-    float t[16];
-  };
-  // pin(): an empty volatile asm on the value -- volatile asm keeps its order against the asm MFMAs, so a stage's
-  // inputs pinned at its start and outputs pinned at its end hold its instructions inside its own gap
-  auto pin = [](float& x) { asm volatile("" : "+v"(x)); };
-  auto sm_stage = [&](int g, float* sv, SmState& st, float* p) {
-    if constexpr (CAP) {
-      if (g < 16) pin(sv[g]);
-      if (g >= 2 && g - 2 < 16) pin(st.t[g - 2]);
-      if (g >= 4 && g - 4 < 16) pin(st.t[g - 4]);
-      if (g < 16) st.t[g] = __builtin_amdgcn_exp2f(sv[g] * ce.c2);
-      if (g >= 2 && g - 2 < 16) st.t[g - 2] = __builtin_amdgcn_rcpf(1.f + st.t[g - 2]);
-      if (g >= 4 && g - 4 < 16) p[g - 4] = __builtin_amdgcn_exp2f(ce.lg2p(st.t[g - 4]));
-      if (g < 16) pin(st.t[g]);
-      if (g >= 2 && g - 2 < 16) pin(st.t[g - 2]);
-      if (g >= 4 && g - 4 < 16) pin(p[g - 4]);
-    } else {
-      if (g < 16) {
-        pin(sv[g]);
-        p[g] = __builtin_amdgcn_exp2f(sv[g] * (a.scale * 1.4426950408889634f));
-        pin(p[g]);
-      }
-    }
-  };
-  auto sm_drain = [&](float* sv, SmState& st, float* p) {
-#pragma unroll
-    for (int g = 16; g < 20; ++g) sm_stage(g, sv, st, p);
-  };
-  // the mask of a tile that is not plain, applied to the 16 p of a half after the fact (p = 2^-120 for a hidden
-  // key, 0 past L): the branch around it holds only these 16 values, so the O^T accumulators never become
-  // branch-merged values (hipcc then parks them in arch VGPRs and copies them into AGPRs for every MFMA).  The
-  // lane's 16 key classes arrive as 4 dwords (byte j of dword m = key 8m + j)
-  auto mask_fix = [&](float* p, int k0, int kb) {
-    uint32_t cw[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) cw[m] = *reinterpret_cast<const uint32_t*>(lcls + k0 + 32 * kb + 8 * m + 4 * hh);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kj = k0 + 32 * kb + (e & 3) + 8 * (e >> 2) + 4 * hh;
-      const int c = (cw[e >> 2] >> (8 * (e & 3))) & 0xff;
-      bool vis = (c == 0) | ((c == 1) & (kj <= qi));
-      if (a.sliding_window > 0) vis = vis & (qi - kj < a.sliding_window);
-      p[e] = vis ? p[e] : MASKED_P;
-      p[e] = kj < L ? p[e] : 0.f;
-    }
-  };
-  // S^T of one 32-key half: K fragment reads 6 k-steps ahead of the MFMA chain (compiler-counted lgkmcnt);
-  // fill(ks) is issued after MFMA ks (the other half's softmax, one score per gap)
-  auto qk = [&](const char* ldsK, auto KB, auto fill) {
-    constexpr int kb = decltype(KB)::value;
-    const char* krow = ldsK + (32 * kb + r) * 512;
-    bf16x8 kf[16];
-#pragma unroll
-    for (int ks = 0; ks < 6; ++ks) kf[ks] = *reinterpret_cast<const bf16x8*>(krow + (((2 * ks + hh) ^ swr) << 4));
-    a_static_for<0, 16>([&](auto KS) {
-      constexpr int ks = decltype(KS)::value;
-      if constexpr (ks + 6 < 16)
-        kf[ks + 6] = *reinterpret_cast<const bf16x8*>(krow + (((2 * (ks + 6) + hh) ^ swr) << 4));
-      s_mfma<kb, ks == 0>(kf[ks], qf[ks]);
-      fill(ks);
-    });
-    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-  };
-  // the 16 scores of half S out of the accumulator file (after the XDL write -> read wait states)
-  auto s_read = [&](auto S, float* sv) {
-    o_fence();
-    a_static_for<0, 16>([&](auto E) { sv[decltype(E)::value] = o_get<128 + 16 * decltype(S)::value + decltype(E)::value>(); });
-  };
-  // O^T += V^T P^T for one half: per k-step s (16 keys) and d-tile dt two transposed 4-key x 16-column reads
-  // (lane 4q + p of its 16-lane group g: rows 16 s + 4 hh + q (+8), columns 32 dt + 16 (g & 1) + 4 p).
-  // Inline asm, not the tr16 builtin: hipcc puts a vmcnt(0) (the next tile's LDS-DMA) before a builtin read it
-  // cannot tell from the DMA target.  Reads run DEPTH k-steps ahead; each wait names the registers it guards so the
-  // MFMA cannot be scheduled above it; fill(u) follows MFMA u
-  auto pv_half = [&](const char* ldsV, int kb, const bf16x8* pf, auto fill) {
-    constexpr int DEPTH = 3;
-    const int ra0 = 32 * kb + 4 * hh + q4;
-    auto vaddr = [&](int it, int half) {
-      const int row = ra0 + 16 * (it >> 3) + 8 * half;
-      const int ch = 4 * (it & 7) + 2 * g1 + (p4 >> 1);
-      return (uint32_t)(uintptr_t)(const LDS_AS char*)(ldsV + row * 512 + ((ch ^ sw32(row)) << 4) + (p4 & 1) * 8);
-    };
-    u32x2 lo[DEPTH + 1], hi[DEPTH + 1];
-#pragma unroll
-    for (int it = 0; it < 16 + DEPTH; ++it) {
-      if (it < 16)
-        asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3"
-                     : "=&v"(lo[it % (DEPTH + 1)]), "=&v"(hi[it % (DEPTH + 1)])
-                     : "v"(vaddr(it, 0)), "v"(vaddr(it, 1)));
-      const int u = it - DEPTH;
-      if (u >= 0) {
-        const int sl = u % (DEPTH + 1);
-        const int ahead = 2 * (15 - u < DEPTH ? 15 - u : DEPTH);  // reads issued after step u's pair
-        switch (ahead) {
-          case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(lo[sl]), "+v"(hi[sl])); break;
-          case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(lo[sl]), "+v"(hi[sl])); break;
-          case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(lo[sl]), "+v"(hi[sl])); break;
-          default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[sl]), "+v"(hi[sl])); break;
-        }
-        const u32x4 vv = {lo[sl][0], lo[sl][1], hi[sl][0], hi[sl][1]};
-        a_static_for<0, 8>([&](auto DC) {
-          if (decltype(DC)::value == (u & 7)) o_mfma<decltype(DC)::value>(__builtin_bit_cast(bf16x8, vv), pf[u >> 3]);
-        });
-        fill(u);
-      }
-    }
-  };
-  // one 64-key tile in four phases fenced by sched barriers: QK(0) | QK(1) + softmax(0) | PV(0) + softmax(1) | PV(1)
-  auto tile = [&](const char* ldsK, int k0, bool plain) {
-    const char* ldsV = ldsK + TB;
-    auto none = [](int) {};
-    using Z = std::integral_constant<int, 0>;
-    using O = std::integral_constant<int, 1>;
-    A32_T(ta);
-    qk(ldsK, Z{}, none);
-    __builtin_amdgcn_sched_barrier(0);
-    A32_T(tb);
-    float p[16], sv[16];
-    SmState sms;
-    s_read(Z{}, sv);
-    qk(ldsK, O{}, [&](int e) { sm_stage(e, sv, sms, p); });
-    sm_drain(sv, sms, p);
-    if (!plain) mask_fix(p, k0, 0);
-    auto finish = [&](bf16x8* pf) {
-      float l0 = 0.f, l1 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        l0 += p[e];
-        l1 += p[e + 1];
-      }
-      lsum += l0 + l1;
-      pf[0] = pack_frag(p);
-      pf[1] = pack_frag(p + 8);
-    };
-    bf16x8 pf0[2], pf1[2];
-    finish(pf0);
-    __builtin_amdgcn_sched_barrier(0);
-    A32_T(tc);
-    pv_half(ldsV, 0, pf0, [&](int e) {
-      if (e == 0) s_read(O{}, sv);  // behind PV(0)'s first MFMA: the wait states overlap the matrix pipe
-      sm_stage(e, sv, sms, p);
-    });
-    sm_drain(sv, sms, p);
-    if (!plain) mask_fix(p, k0, 1);
-    finish(pf1);
-    __builtin_amdgcn_sched_barrier(0);
-    A32_T(td);
-    pv_half(ldsV, 1, pf1, none);
-#if ATT32_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    A32_T(te);
-    st[2] += tb - ta;
-    st[3] += tc - tb;
-    st[4] += td - tc;
-    st[5] += te - td;
-#endif
-  };
-
-  for (int kt = 0; kt < nkt; ++kt) {
-    A32_T(tw0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#if ATT32_STAMPS
-    A32_T(tw1);
-    if (kt == 0) st[0] = tw1 - tk0;
-    else st[1] += tw1 - tw0;
-#endif
-    const char* ldsK = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nkt) {
-      char* nx = smem + ((kt + 1) & 1) * STAGE;
-      const int r0 = (kt + 1) * 64;
-      glds_tile32(nx, kbase + (int64_t)r0 * a.ldk, a.ldk, L - r0, w, lane);
-      glds_tile32(nx + TB, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, w, lane);
-    }
-    tile(ldsK, kt * 64, tile_plain(lcls, kt * 64, L, window_free, lane));
-  }
-  A32_T(tep);
-  // ---- epilogue: O^T (d = 32 dt + (e & 3) + 8 (e >> 2) + 4 hh, q = lane col) / l -> per-wave LDS image
-  // [32 q][260] bf16 (row stride 130 dwords: the 8-B stores of a half-wave hit distinct banks) -> 16-B row stores
-  lsum += __shfl_xor(lsum, 32, 64);
-  const float inv = 1.0f / lsum;
-  if (qvalid && hh == 0) lse[((int64_t)b * a.Hq + h) * L + qi] = CAP ? __logf(lsum) : __logf(lsum);
-  constexpr int IS = 260;
-  __syncthreads();
-  bf16_t* img = (bf16_t*)smem + w * 32 * IS;
-  o_fence();
-  a_static_for<0, 32>([&](auto DM) {
-    constexpr int dt = decltype(DM)::value >> 2, m = decltype(DM)::value & 3, q = 16 * dt + 4 * m;
-    const uint32_t lo = pack2(o_get<q>() * inv, o_get<q + 1>() * inv);
-    const uint32_t hi = pack2(o_get<q + 2>() * inv, o_get<q + 3>() * inv);
-    *reinterpret_cast<u32x2*>(img + r * IS + 32 * dt + 8 * m + 4 * hh) = u32x2{lo, hi};
-  });
-  __syncthreads();
-  for (int idx = lane; idx < 32 * 32; idx += 64) {
-    const int row = idx >> 5, ch = idx & 31;
-    const int q = qt * 64 + 32 * (w & 1) + row;
-    if (q < L) {
-      const u32x2 lo = *reinterpret_cast<const u32x2*>(img + row * IS + ch * 8);
-      const u32x2 hi = *reinterpret_cast<const u32x2*>(img + row * IS + ch * 8 + 4);
-      *reinterpret_cast<u32x4*>(out + ((int64_t)b * L + q) * ldo + (int64_t)h * D + ch * 8) = u32x4{lo[0], lo[1], hi[0], hi[1]};
-    }
-  }
-#if ATT32_STAMPS
-  A32_T(tend);
-  st[6] = tend - tep;
-  st[7] = tend - tk0;
-  if (t == 0 && blockIdx.x < 4096)
-    for (int i = 0; i < 8; ++i) att32_stamps[blockIdx.x][i] = st[i];
-#endif
-}
-
 // ================================================================== backward: delta = rowsum(dO * O)
 __global__ void attn_delta_kernel(int B, int L, int H, int D, const bf16_t* __restrict__ o, int64_t ldo,
                                   const bf16_t* __restrict__ dout, int64_t lddo, float* __restrict__ delta) {
@@ -1176,6 +617,8 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // classes visible to tile_plain
   const int kcls = kj < L ? lcls[kj] : 3;  // this lane's key class (3: beyond L)
+  const bool window_free = a.sliding_window <= 0 || a.sliding_window >= L;
+  const bool keys_plain = window_free && __ballot(kcls != 0) == 0ull;  // the wave's 16 keys: all in range, class 0
   glds_tile<RS, 64, 4>(ldsV, vbase + (int64_t)r0 * a.ldv, a.ldv, L - r0, D, w, lane);
 
   const int nqt = (L + 31) / 32, nsteps = grp * nqt;
@@ -1231,28 +674,36 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
     }
     // element (mt, j): query q0 + 16mt + 4g + j, key = lane col (kl)
     float pv[8], zv[8];
+    // wave-uniform fast path: every key of the wave visible to every query (class 0, no effective window) and all
+    // 32 queries in range -- no per-score mask test (the prefix keys of the Gemma2 training mask, 299 of 312)
+    const bool plain = keys_plain && q0 + 32 <= L;
+    auto scores = [&](auto PLAIN) {
+      constexpr bool PL = decltype(PLAIN)::value;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(sl + q0 + 16 * mt + 4 * g);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(sd + q0 + 16 * mt + 4 * g);
+      for (int mt = 0; mt < 2; ++mt) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(sl + q0 + 16 * mt + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(sd + q0 + 16 * mt + 4 * g);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int qi = q0 + 16 * mt + 4 * g + j;
-        const bool live = qi < L && kcls != 3;
-        const bool masked = !visible(kcls, kj, qi, a.sliding_window);
-        float p, z;
-        if constexpr (CAP) {
-          const float r = ce.r(s[mt][j]);
-          p = __builtin_amdgcn_exp2f((masked ? MASKED_LG2P : ce.lg2p(r)) - l4[j]);
-          z = p * (dp[mt][j] - d4[j]) * (4.f * r * (1.f - r)) * a.scale;
-        } else {
-          p = __builtin_amdgcn_exp2f((masked ? MASKVAL : s[mt][j] * (a.scale * LOG2E)) - l4[j]);
-          z = p * (dp[mt][j] - d4[j]) * a.scale;
+        for (int j = 0; j < 4; ++j) {
+          const int qi = q0 + 16 * mt + 4 * g + j;
+          const bool live = PL || (qi < L && kcls != 3);
+          const bool masked = !PL && !visible(kcls, kj, qi, a.sliding_window);
+          float p, z;
+          if constexpr (CAP) {
+            const float r = ce.r(s[mt][j]);
+            p = __builtin_amdgcn_exp2f((masked ? MASKED_LG2P : ce.lg2p(r)) - l4[j]);
+            z = p * (dp[mt][j] - d4[j]) * (4.f * r * (1.f - r)) * a.scale;
+          } else {
+            p = __builtin_amdgcn_exp2f((masked ? MASKVAL : s[mt][j] * (a.scale * LOG2E)) - l4[j]);
+            z = p * (dp[mt][j] - d4[j]) * a.scale;
+          }
+          pv[4 * mt + j] = live ? p : 0.f;
+          zv[4 * mt + j] = live ? z : 0.f;
         }
-        pv[4 * mt + j] = live ? p : 0.f;
-        zv[4 * mt + j] = live ? z : 0.f;
       }
-    }
+    };
+    if (plain) scores(std::true_type{});
+    else scores(std::false_type{});
     const bf16x8 pa = pack_frag(pv), za = pack_frag(zv);
     mfma_tr_sweep<RS, NDT, false>(adv, ldsO, 0, pa, lane);
     mfma_tr_sweep<RS, NDT, false>(adk, ldsQ, 0, za, lane);
@@ -1434,46 +885,18 @@ int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hi
   return svla::check_launch("attn_fwd");
 }
 
-template <bool CAP>
-int fwd32_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hipStream_t s) {
-  const int lds = 4 * 64 * 512 + round16(a.L + 64);  // class dwords of the last tile read up to 63 bytes past L
-  SVLA_CHECK_ARG(lds <= 160 * 1024, "attn_fwd: L too large for the LDS-resident key classes");
-  const int64_t nblk = (int64_t)((a.L + 63) / 64) * (a.Hq / 2) * a.B;
-  SVLA_CHECK_ARG(nblk < (1LL << 31), "attn_fwd: grid too large");
-  set_lds_once<attn_fwd32_kernel<CAP>>(lds);
-  hipLaunchKernelGGL((attn_fwd32_kernel<CAP>), dim3((unsigned)nblk), dim3(256), lds, s, a, out, ldo, lse);
-  return svla::check_launch("attn_fwd32");
-}
-
-#if ATT32_STAMPS
-}  // namespace
-extern "C" int svla_diag_att32_stamps(void* host, size_t bytes) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(att32_stamps), bytes < sizeof(att32_stamps) ? bytes : sizeof(att32_stamps)) ==
-                 hipSuccess ? 0 : 2;
-}
-namespace {
-#endif
-int attn32_mode() {  // SVLA_ATTN32=1 selects the 32x32x16 head_dim-256 forward (A/B; not yet ahead of 16x16x32)
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("SVLA_ATTN32");
-    m = (e && e[0] == '1') ? 1 : 0;
-  }
-  return m;
-}
-
 template <int D, int NH, bool ROPE, bool CAP>
 int bwd_launch(const svla_attn_args& a, const bf16_t* dout, int64_t lddo, const float* lse, const float* delta,
                bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv, int64_t lddv, hipStream_t s) {
   const int grp = a.Hq / a.Hkv;
   const int LP = (a.L + 35) / 32 * 32;
+  const int nt = (a.L + 63) / 64;
   const int lds_kv = tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
   SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
-  const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
-  const int nt = (a.L + 63) / 64;
   set_lds_once<attn_bwd_dkv_kernel<D, ROPE, CAP>>(lds_kv);
   hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE, CAP>), dim3((unsigned)(nt * a.Hkv * a.B)), dim3(256), lds_kv, s, a,
                      dout, lddo, lse, delta, dk, lddk, dv, lddv);
+  const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
   set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE, CAP>>(lds_q);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE, CAP>), dim3((unsigned)(nt * (a.Hq / NH) * a.B)), dim3(256 * NH),
                      lds_q, s, a, dout, lddo, lse, delta, dq, lddq);
@@ -1492,7 +915,6 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
   bf16_t* o = (bf16_t*)out;
   SVLA_CHECK_ARG(!a->bias || a->D == 64, "attn_fwd: an additive bias is only supported with head_dim 64");
   if (a->D == 256) {
-    if (pair && cap && attn32_mode()) return fwd32_launch<true>(*a, o, ldo, lse, s);
     if (SVLA_ATT_QW256 == 2)
       return cap ? fwd_launch<256, 1, true, false, 2>(*a, o, ldo, lse, s)
                  : fwd_launch<256, 1, false, false, 2>(*a, o, ldo, lse, s);
