@@ -221,7 +221,7 @@ int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t
                          int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0, void* stream);
 
 /* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
- * workspace: B*Hq*L fp32 (row dot(dO, O)). */
+ * workspace: B*Hq*L fp32 (row dot(dO, O), formed by the dQ kernel and read by the dK/dV kernel). */
 int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                   const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
                   float* workspace, void* stream);
@@ -240,6 +240,13 @@ int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const void* w, cons
                      void* stream);
 int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w, float eps,
                          void* h, float* rstd, void* stream);
+/* Backward of the training pair svla_add_rmsnorm2_fwd_train (h = res + rms(y; w1), x = rms(h; w2)) in one pass:
+ * dh_out = bf16(bf16(rms_bwd(h; dx)) + dres) (dres may be NULL), dy_out = bf16(rms_bwd(y; dh_out)); dw_partial: two
+ * planes [2][ceil(rows/rows_per_block)][N] fp32 (w2's partials, then w1's) for svla_colsum2_f32.  Bitwise two
+ * svla_rmsnorm_bwd calls. */
+int svla_rmsnorm2_bwd(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2, const void* dx,
+                      const void* dres, const void* y, const void* w1, const float* rstd1, void* dh_out, void* dy_out,
+                      float* dw_partial, int64_t* n_partial, void* stream);
 /* h = res + rmsnorm(yin; w1), x = rmsnorm(h; w2) in one pass (inference; bitwise the two separate calls):
  * Gemma2 post-attention + pre-feedforward norms, or post-feedforward + next input norm (modeling_gemma2.py:487-496). */
 int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1, const void* w2,
@@ -364,6 +371,20 @@ int svla_adamw(int64_t n, float* master, void* param_bf16, const void* grad_bf16
 /* clip_scale[0] = min(1, max_norm / (sqrt(sumsq[0]) + 1e-6)); norm_out[0] = sqrt(sumsq[0]). */
 int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float* norm_out, void* stream);
 
+/* ZoeDepthAttractorLayerUnnormed bin update (transformers zoedepth [3p], the frozen estimator of
+ * model/modeling_spatialvla.py:314-323): out = bf16(c + bf16(sum_i bf16(inv(bf16(A_i - c))) [/ n_att])) with the
+ * eager bf16 rounding of each op, inv(dx) = dx / (1 + alpha dx^gamma) in fp32.  Maps [B, C, H, W] by element strides
+ * (b, c, y, x); n_bins % 8 == 0. */
+int svla_zoe_attractor(int B, int H, int W, int n_att, int n_bins, const void* attractors, const int64_t* a_strides,
+                       const void* centres, const int64_t* c_strides, float alpha, int gamma, int mean, void* out,
+                       const int64_t* out_strides, void* stream);
+/* Bilinear resize of a channels-last bf16 map [B, H1, W1, C] -> [B, H2, W2, C] with torch's
+ * upsample_bilinear2d semantics (transformers ZoeDepthFeatureFusionLayer.forward interpolate(scale_factor=2,
+ * align_corners=True) and the relative head's nn.Upsample, called from modeling_spatialvla.py:317-323's Zoe
+ * forward).  rh/rw = torch's area_pixel_compute_scale: (in-1)/(out-1) with align_corners, else 1/scale_factor or
+ * in/out.  C multiple of 8, 16-B aligned buffers. */
+int svla_upsample_bilinear_nhwc(int B, int C, int H1, int W1, int H2, int W2, int align_corners, float rh, float rw,
+                                const void* in, void* out, void* stream);
 /* ------------------------------------------------------------------------------------------
  * ZoeDepth metric head tail, fused (frozen depth estimator; reference model/modeling_spatialvla.py:314-323
  * calls transformers ZoeDepthMetricDepthEstimationHead.forward [3p], whose tail after the last attractor is
@@ -373,13 +394,6 @@ int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float
  * element strides (b, c, y, x) / (b, y, x) (channel stride 1 = channels-last, 16-B aligned).  params fp32:
  * W1^T [CF+1+CE][Hid], W2 [4][Hid], b1 [Hid], b2 [4], log_binom(NBins-1, k) [NBins] (as the reference computes
  * it).  out [B, H, W] fp32.  Built for NBins = 64, Hid = 80, CF and CE multiples of 8. */
-/* Bilinear resize of a channels-last bf16 map [B, H1, W1, C] -> [B, H2, W2, C] with torch's
- * upsample_bilinear2d semantics (transformers ZoeDepthFeatureFusionLayer.forward interpolate(scale_factor=2,
- * align_corners=True) and the relative head's nn.Upsample, called from modeling_spatialvla.py:317-323's Zoe
- * forward).  rh/rw = torch's area_pixel_compute_scale: (in-1)/(out-1) with align_corners, else 1/scale_factor or
- * in/out.  C multiple of 8, 16-B aligned buffers. */
-int svla_upsample_bilinear_nhwc(int B, int C, int H1, int W1, int H2, int W2, int align_corners, float rh, float rw,
-                                const void* in, void* out, void* stream);
 int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
                          const void* feat, const int64_t* feat_strides, const void* rel, const int64_t* rel_strides,
                          const void* emb, const int64_t* emb_strides, const void* ctr, const int64_t* ctr_strides,

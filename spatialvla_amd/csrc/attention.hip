@@ -16,8 +16,8 @@
 //  * RoPE (rotate_half, modeling_gemma2.py:123-154) is not applied here on the way in: q / k arrive rotated
 //    (the QKV GEMM's SVLA_EPI_ROPE epilogue).  The backward applies its transpose to dQ / dK in the accumulators
 //    before the store, so the gradients leave w.r.t. the pre-rotation q / k.
-//  * Backward is two deterministic kernels (dK/dV per key tile looping over the GQA query heads,
-//    dQ per query tile) — no float atomics.
+//  * Backward is two deterministic kernels (dQ per query tile, which also forms delta = rowsum(dO * O); then dK/dV
+//    per key tile looping over the GQA query heads) — no float atomics.
 #include <atomic>
 #include <type_traits>
 
@@ -510,29 +510,6 @@ __global__ __launch_bounds__(256 * NH, (D == 64 && SVLA_ATT_RS64) ? SVLA_ATT_WPE
   }
 }
 
-// ================================================================== backward: delta = rowsum(dO * O)
-__global__ void attn_delta_kernel(int B, int L, int H, int D, const bf16_t* __restrict__ o, int64_t ldo,
-                                  const bf16_t* __restrict__ dout, int64_t lddo, float* __restrict__ delta) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, q, h) rows
-  const int lane = threadIdx.x & 63;
-  if (row >= (int64_t)B * L * H) return;
-  const int h = (int)(row % H);
-  const int64_t bq = row / H;
-  const int q = (int)(bq % L), b = (int)(bq / L);
-  const bf16_t* po = o + bq * ldo + (int64_t)h * D;
-  const bf16_t* pd = dout + bq * lddo + (int64_t)h * D;
-  float s = 0.f;
-  for (int d = lane * 8; d < D; d += 512) {
-    float x[8], y[8];
-    unpack8(*reinterpret_cast<const u32x4*>(po + d), x);
-    unpack8(*reinterpret_cast<const u32x4*>(pd + d), y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
-  }
-  s = wave_sum(s);
-  if (lane == 0) delta[((int64_t)b * H + h) * L + q] = s;
-}
-
 // transpose of rotate_half RoPE on a [rows x 16dt+c] accumulator layout (lo half dt < 8, hi half dt + 8)
 template <int NDT>
 __device__ __forceinline__ void rope_t_acc(f32x4 (&acc)[NDT], const svla_attn_args& a, int row0, int L, int g,
@@ -741,8 +718,9 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
 // through two LDS stages by LDS-DMA.
 template <int D, int NH, bool ROPE, bool CAP>
 __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
-                                                                  int64_t lddo, const float* __restrict__ lse,
-                                                                  const float* __restrict__ delta,
+                                                                  int64_t lddo, const bf16_t* __restrict__ out,
+                                                                  int64_t ldo, const float* __restrict__ lse,
+                                                                  float* __restrict__ delta,
                                                                   bf16_t* __restrict__ dq, int64_t lddq) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
   constexpr int NKS = DP / 32, NDT = DV / 16, NW = 4 * NH;
@@ -771,7 +749,24 @@ __global__ __launch_bounds__(256 * NH, 1) void attn_bwd_dq_kernel(svla_attn_args
   load_row_frags<D>(qf, qbase + (int64_t)qi * a.ldq, qvalid, lane);
   load_row_frags<D>(of, obase + (int64_t)qi * lddo, qvalid, lane);
   const float lq = qvalid ? lse[((int64_t)b * a.Hq + h) * L + qi] * LOG2E : 0.f;
-  const float dq_ = qvalid ? delta[((int64_t)b * a.Hq + h) * L + qi] : 0.f;
+  // delta = rowsum(dO * O) of this lane's query, here instead of a separate pass: the four lanes holding the query's
+  // row chunks (g = 0..3) sum their halves and combine by two shuffles; written out for the dK/dV kernel that follows
+  float dq_ = 0.f;
+  {
+    bf16x8 orow[NKS];
+    load_row_frags<D>(orow, out + ((int64_t)b * L + qi) * ldo + (int64_t)h * D, qvalid, lane);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      float x[8], y[8];
+      unpack8(__builtin_bit_cast(u32x4, of[ks]), x);
+      unpack8(__builtin_bit_cast(u32x4, orow[ks]), y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dq_ += x[e] * y[e];
+    }
+    dq_ += __shfl_xor(dq_, 16, 64);
+    dq_ += __shfl_xor(dq_, 32, 64);
+    if (g == 0 && qvalid) delta[((int64_t)b * a.Hq + h) * L + qi] = dq_;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int nkt = (L + 63) / 64;
   glds_tile<RS, 64, NW>(smem, kbase, a.ldk, L, D, w, lane);
@@ -886,20 +881,23 @@ int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hi
 }
 
 template <int D, int NH, bool ROPE, bool CAP>
-int bwd_launch(const svla_attn_args& a, const bf16_t* dout, int64_t lddo, const float* lse, const float* delta,
-               bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv, int64_t lddv, hipStream_t s) {
+int bwd_launch(const svla_attn_args& a, const bf16_t* out, int64_t ldo, const bf16_t* dout, int64_t lddo,
+               const float* lse, float* delta, bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv,
+               int64_t lddv, hipStream_t s) {
   const int grp = a.Hq / a.Hkv;
   const int LP = (a.L + 35) / 32 * 32;
   const int nt = (a.L + 63) / 64;
+  // dQ first: it forms delta = rowsum(dO * O) for its queries (no separate pass) and leaves it for dK/dV
+  const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
+  set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE, CAP>>(lds_q);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE, CAP>), dim3((unsigned)(nt * (a.Hq / NH) * a.B)), dim3(256 * NH),
+                     lds_q, s, a, dout, lddo, out, ldo, lse, delta, dq, lddq);
+  if (int rc = svla::check_launch("attn_bwd_dq")) return rc;
   const int lds_kv = tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
   SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
   set_lds_once<attn_bwd_dkv_kernel<D, ROPE, CAP>>(lds_kv);
   hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE, CAP>), dim3((unsigned)(nt * a.Hkv * a.B)), dim3(256), lds_kv, s, a,
                      dout, lddo, lse, delta, dk, lddk, dv, lddv);
-  const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
-  set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE, CAP>>(lds_q);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NH, ROPE, CAP>), dim3((unsigned)(nt * (a.Hq / NH) * a.B)), dim3(256 * NH),
-                     lds_q, s, a, dout, lddo, lse, delta, dq, lddq);
   return svla::check_launch("attn_bwd");
 }
 
@@ -936,14 +934,14 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
 }
 
 template <int D, int NH>
-static int bwd_dispatch(const svla_attn_args& a, bool rope, bool cap, const bf16_t* d_o, int64_t lddo,
-                        const float* lse, const float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv,
-                        int64_t lddv, hipStream_t s) {
+static int bwd_dispatch(const svla_attn_args& a, bool rope, bool cap, const bf16_t* o, int64_t ldo, const bf16_t* d_o,
+                        int64_t lddo, const float* lse, float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk,
+                        void* dv, int64_t lddv, hipStream_t s) {
   bf16_t *q = (bf16_t*)dq, *k = (bf16_t*)dk, *v = (bf16_t*)dv;
-  if (rope) return cap ? bwd_launch<D, NH, true, true>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
-                       : bwd_launch<D, NH, true, false>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
-  return cap ? bwd_launch<D, NH, false, true>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
-             : bwd_launch<D, NH, false, false>(a, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
+  if (rope) return cap ? bwd_launch<D, NH, true, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
+                       : bwd_launch<D, NH, true, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
+  return cap ? bwd_launch<D, NH, false, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
+             : bwd_launch<D, NH, false, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
 }
 
 extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
@@ -957,16 +955,12 @@ extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t l
   SVLA_CHECK_ARG(ldo % 8 == 0 && lddo % 8 == 0 && lddq % 8 == 0 && lddk % 8 == 0 && lddv % 8 == 0,
                  "attn_bwd: ld must be multiples of 8");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t rows = (int64_t)a->B * a->L * a->Hq;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, a->B, a->L, a->Hq, a->D,
-                     (const bf16_t*)out, ldo, (const bf16_t*)dout, lddo, workspace);
-  if (int rc = svla::check_launch("attn_delta")) return rc;
   const bool pair = (a->Hq / a->Hkv) % 2 == 0;
   const bool cap = a->softcap > 0.f;
-  const bf16_t* d_o = (const bf16_t*)dout;
+  const bf16_t *o = (const bf16_t*)out, *d_o = (const bf16_t*)dout;
   if (a->D == 256)
-    return pair ? bwd_dispatch<256, 2>(*a, rope, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s)
-                : bwd_dispatch<256, 1>(*a, rope, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
+    return pair ? bwd_dispatch<256, 2>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s)
+                : bwd_dispatch<256, 1>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
   SVLA_CHECK_ARG(!rope, "attn_bwd: RoPE only with D=256");
-  return bwd_dispatch<72, 1>(*a, false, cap, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
+  return bwd_dispatch<72, 1>(*a, false, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
 }

@@ -216,6 +216,148 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
   }
 }
 
+// ------------------------------------------------------------------ RMSNorm pair backward
+// The backward of h = res + rms(y; w1), x = rms(h; w2) (decoder-layer post-attention norm + residual and the
+// pre-feedforward norm, modeling_gemma2.py:487-490) in one pass over the rows:
+//   dh = bf16(bf16(rms_bwd(h; dx)) + dres)    (stored: the residual-stream gradient of res)
+//   dy = bf16(rms_bwd(y; dh))
+// with the weight-gradient partials of both norms as two planes [2][blocks][N] (w2 first).  The per-row arithmetic and
+// reduction order are rms_bwd_kernel's, so dh / dy / the partials are bitwise those of two svla_rmsnorm_bwd calls;
+// one launch and one read of dh fewer.
+template <int MC>
+__global__ __launch_bounds__(NTH) void rms_bwd2_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ h,
+                                                       const bf16_t* __restrict__ w2, const float* __restrict__ rstd2,
+                                                       const bf16_t* __restrict__ dx, const bf16_t* __restrict__ dres,
+                                                       const bf16_t* __restrict__ y, const bf16_t* __restrict__ w1,
+                                                       const float* __restrict__ rstd1, bf16_t* __restrict__ dh_out,
+                                                       bf16_t* __restrict__ dy_out, float* __restrict__ partial) {
+  __shared__ float red[16];
+  const int nch = (int)(N >> 3);
+  float wf2[MC][8], wf1[MC][8], acc2[MC][8], acc1[MC][8];
+#pragma unroll
+  for (int c = 0; c < MC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc2[c][j] = acc1[c][j] = 0.f;
+    if (ch < nch) {
+      ld8(w2 + ch * 8, wf2[c]);
+      ld8(w1 + ch * 8, wf1[c]);
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * RPB;
+  const int nr = (int)min<int64_t>(RPB, rows - r0);
+  u32x4 ph[MC], pd[MC], pr[MC], py[MC];
+  float prs2 = 0.f, prs1 = 0.f;
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      const int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        ph[c] = *reinterpret_cast<const u32x4*>(h + row * N + ch * 8);
+        pd[c] = *reinterpret_cast<const u32x4*>(dx + row * N + ch * 8);
+        if (dres) pr[c] = *reinterpret_cast<const u32x4*>(dres + row * N + ch * 8);
+        py[c] = *reinterpret_cast<const u32x4*>(y + row * N + ch * 8);
+      }
+    }
+    prs2 = rstd2[row];
+    prs1 = rstd1[row];
+  };
+  fetch(r0);
+  for (int rr = 0; rr < nr; ++rr) {
+    const int64_t row = r0 + rr;
+    const float rs2 = prs2, rs1 = prs1;
+    u32x4 ch_[MC], cd[MC], cr[MC], cy[MC];
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      ch_[c] = ph[c];
+      cd[c] = pd[c];
+      cr[c] = pr[c];
+      cy[c] = py[c];
+    }
+    if (rr + 1 < nr) fetch(row + 1);
+    // norm 2 (x = rms(h; w2)): dh
+    float xv[MC][8], gv[MC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float d[8];
+        unpack8(ch_[c], xv[c]);
+        unpack8(cd[c], d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float xh = xv[c][j] * rs2;
+          xv[c][j] = xh;
+          gv[c][j] = d[j] * (1.0f + wf2[c][j]);
+          dot += gv[c][j] * xh;
+          acc2[c][j] += d[j] * xh;
+        }
+      }
+    }
+    dot = block_sum(dot, red) / (float)N;
+    float dh[MC][8];
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dh[c][j] = rs2 * (gv[c][j] - xv[c][j] * dot);
+        if (dres) {
+          float r[8];
+          unpack8(cr[c], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dh[c][j] = round_bf(dh[c][j]) + r[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dh[c][j] = round_bf(dh[c][j]);  // the bf16 dh both consumers read
+        st8(dh_out + row * N + ch * 8, dh[c]);
+      }
+    }
+    // norm 1 (h = res + rms(y; w1)): dy from the bf16 dh
+    float dot1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        unpack8(cy[c], xv[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float xh = xv[c][j] * rs1;
+          xv[c][j] = xh;
+          gv[c][j] = dh[c][j] * (1.0f + wf1[c][j]);
+          dot1 += gv[c][j] * xh;
+          acc1[c][j] += dh[c][j] * xh;
+        }
+      }
+    }
+    __syncthreads();  // red[] is reused by the second reduction
+    dot1 = block_sum(dot1, red) / (float)N;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      int ch = threadIdx.x + c * NTH;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs1 * (gv[c][j] - xv[c][j] * dot1);
+        st8(dy_out + row * N + ch * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MC; ++c) {
+    int ch = threadIdx.x + c * NTH;
+    if (ch < nch) {
+      float* p2 = partial + (int64_t)blockIdx.x * N + ch * 8;
+      float* p1 = p2 + (int64_t)gridDim.x * N;
+      *reinterpret_cast<f32x4*>(p2) = f32x4{acc2[c][0], acc2[c][1], acc2[c][2], acc2[c][3]};
+      *reinterpret_cast<f32x4*>(p2 + 4) = f32x4{acc2[c][4], acc2[c][5], acc2[c][6], acc2[c][7]};
+      *reinterpret_cast<f32x4*>(p1) = f32x4{acc1[c][0], acc1[c][1], acc1[c][2], acc1[c][3]};
+      *reinterpret_cast<f32x4*>(p1 + 4) = f32x4{acc1[c][4], acc1[c][5], acc1[c][6], acc1[c][7]};
+    }
+  }
+}
+
 // ------------------------------------------------------------------ wave-per-row backward (N <= 1536 / 2048)
 // One wave per row (lane l owns 16-B chunks l, l+64, ..): the row reductions are wave shuffles, so the four waves
 // of a block work on four rows at once with no barrier; each block still covers RPB rows and writes one weight-
@@ -611,6 +753,27 @@ extern "C" int svla_rmsnorm_bwd(int64_t rows, int64_t N, const void* x, const vo
                          dw_partial);
   }
   return svla::check_launch("rmsnorm_bwd");
+}
+
+extern "C" int svla_rmsnorm2_bwd(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2,
+                                 const void* dx, const void* dres, const void* y, const void* w1, const float* rstd1,
+                                 void* dh_out, void* dy_out, float* dw_partial, int64_t* n_partial, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 8 == 0 && N <= NTH * 8 * 4, "rmsnorm2_bwd: bad N");
+  SVLA_CHECK_ARG(h && w2 && rstd2 && dx && y && w1 && rstd1 && dh_out && dy_out && dw_partial,
+                 "rmsnorm2_bwd: null pointer");
+  SVLA_CHECK_ARG(al16(h) && al16(w2) && al16(dx) && (!dres || al16(dres)) && al16(y) && al16(w1) && al16(dh_out) &&
+                     al16(dy_out) && al16(dw_partial), "rmsnorm2_bwd: misaligned pointer");
+  const int64_t nb = (rows + RPB - 1) / RPB;
+  if (n_partial) *n_partial = nb;
+  if (N <= NTH * 8 * 2)
+    hipLaunchKernelGGL(rms_bwd2_kernel<2>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)h, (const bf16_t*)w2, rstd2, (const bf16_t*)dx, (const bf16_t*)dres,
+                       (const bf16_t*)y, (const bf16_t*)w1, rstd1, (bf16_t*)dh_out, (bf16_t*)dy_out, dw_partial);
+  else
+    hipLaunchKernelGGL(rms_bwd2_kernel<4>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)h, (const bf16_t*)w2, rstd2, (const bf16_t*)dx, (const bf16_t*)dres,
+                       (const bf16_t*)y, (const bf16_t*)w1, rstd1, (bf16_t*)dh_out, (bf16_t*)dy_out, dw_partial);
+  return svla::check_launch("rmsnorm2_bwd");
 }
 
 extern "C" int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,

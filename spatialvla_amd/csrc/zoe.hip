@@ -312,7 +312,88 @@ __global__ __launch_bounds__(256) void upsample_bilinear_nhwc_kernel(UpsArgs a) 
   *reinterpret_cast<u32x4*>(a.out + (((int64_t)n * a.H2 + h2) * a.W2 + w2) * a.C + 8 * c8) = pack8(o);
 }
 
+// ---------------------------------------------------------------------------------------------
+// ZoeDepthAttractorLayerUnnormed's bin update (transformers zoedepth [3p], the nyu-kitti head's four attractor
+// layers, memory_efficient, "mean"/"sum"): for every (b, bin k, y, x) with c = bin_centers[b, k, y, x]
+//   delta = 0;  for i < n_att: delta = bf16(delta + inv_attractor(bf16(A[b, i, y, x] - c)))
+//   delta = bf16(delta / n_att) (mean);  out = bf16(c + delta)
+// inv_attractor(dx) = dx / (1 + alpha dx^gamma) (the TorchScript-fused kernel: fp32 from the bf16 dx, one rounding),
+// the bf16 rounding of each eager op between -- the 3 n_att + 2 launches and the bf16 traffic of the stock loop in
+// one pass.  One thread = 8 consecutive bins of one pixel (channels-last maps: one 16-B load / store).
+struct AttrArgs {
+  int B, H, W, NA, NB, mean;
+  float alpha;
+  int gamma;
+  const bf16_t* A; int64_t as[4];     // attractors [B, NA, H, W], element strides (b, c, y, x)
+  const bf16_t* C; int64_t cs[4];     // bin centres [B, NB, H, W]
+  bf16_t* out; int64_t os[4];         // new bin centres [B, NB, H, W]
+};
+
+__global__ __launch_bounds__(256) void zoe_attractor_kernel(AttrArgs a) {
+  const int ng = a.NB / 8;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.H * a.W * ng;
+  if (idx >= total) return;
+  const int kg = (int)(idx % ng);
+  int64_t r = idx / ng;
+  const int x = (int)(r % a.W);
+  r /= a.W;
+  const int y = (int)(r % a.H);
+  const int b = (int)(r / a.H);
+  const int k0 = 8 * kg;
+  float c[8], d[8];
+  const bf16_t* cp = a.C + (int64_t)b * a.cs[0] + y * a.cs[2] + x * a.cs[3] + k0 * a.cs[1];
+  if (a.cs[1] == 1) {
+    unpack8(*reinterpret_cast<const u32x4*>(cp), c);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = bf2f(cp[j * a.cs[1]]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  const bf16_t* ap = a.A + (int64_t)b * a.as[0] + y * a.as[2] + x * a.as[3];
+  for (int i = 0; i < a.NA; ++i) {
+    const float ai = bf2f(ap[i * a.as[1]]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dx = round_bf(ai - c[j]);
+      float p = dx;
+      for (int q = 1; q < a.gamma; ++q) p = p * dx;
+      d[j] = round_bf(d[j] + round_bf(dx / (a.alpha * p + 1.0f)));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (a.mean) d[j] = round_bf(d[j] * (1.0f / (float)a.NA));
+    d[j] = c[j] + d[j];
+  }
+  bf16_t* op = a.out + (int64_t)b * a.os[0] + y * a.os[2] + x * a.os[3] + k0 * a.os[1];
+  if (a.os[1] == 1) {
+    *reinterpret_cast<u32x4*>(op) = pack8(d);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) op[j * a.os[1]] = f2bf(d[j]);
+  }
+}
+
 }  // namespace
+
+extern "C" int svla_zoe_attractor(int B, int H, int W, int n_att, int n_bins, const void* attractors,
+                                  const int64_t* a_strides, const void* centres, const int64_t* c_strides, float alpha,
+                                  int gamma, int mean, void* out, const int64_t* out_strides, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && H > 0 && W > 0 && n_att > 0 && n_bins > 0 && n_bins % 8 == 0 && gamma >= 1,
+                 "zoe_attractor: bad sizes (bins a multiple of 8, gamma >= 1)");
+  SVLA_CHECK_ARG(attractors && centres && out && a_strides && c_strides && out_strides, "zoe_attractor: NULL");
+  SVLA_CHECK_ARG((c_strides[1] != 1 || ((uintptr_t)centres & 15) == 0) && (out_strides[1] != 1 || ((uintptr_t)out & 15) == 0),
+                 "zoe_attractor: channels-last maps must be 16-B aligned");
+  AttrArgs a;
+  a.B = B; a.H = H; a.W = W; a.NA = n_att; a.NB = n_bins; a.mean = mean ? 1 : 0; a.alpha = alpha; a.gamma = gamma;
+  a.A = (const bf16_t*)attractors; a.C = (const bf16_t*)centres; a.out = (bf16_t*)out;
+  for (int i = 0; i < 4; ++i) { a.as[i] = a_strides[i]; a.cs[i] = c_strides[i]; a.os[i] = out_strides[i]; }
+  const int64_t total = (int64_t)B * H * W * (n_bins / 8);
+  hipLaunchKernelGGL(zoe_attractor_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+  return svla::check_launch("zoe_attractor");
+}
 
 extern "C" int svla_zoe_metric_tail(int B, int H, int W, int h, int w, int CF, int CE, int NBins, int Hid,
                                     const void* feat, const int64_t* feat_strides, const void* rel,

@@ -112,9 +112,9 @@ class AddRMSNormFn(torch.autograd.Function):
 class AddRMSNorm2Fn(torch.autograd.Function):
     """(h, x) = (res + Gemma2RMSNorm_1(y), Gemma2RMSNorm_2(h)): the decoder layer's post-attention norm + residual
     and its pre-feedforward norm (modeling_gemma2.py:487-490) in one forward launch (svla_add_rmsnorm2_fwd_train,
-    bitwise AddRMSNormFn then RMSNormFn).  Backward: dh_total = rms_bwd_2(dx) + dh (dh: h's residual-branch
-    gradient, from slot_h when its consumer parks it there), then dy = rms_bwd_1(dh_total); dh_total is the gradient
-    of res (parked in slot_res for the pre-norm that also reads res, as AddRMSNormFn does)."""
+    bitwise AddRMSNormFn then RMSNormFn).  Backward (one launch, svla_rmsnorm2_bwd): dh_total = rms_bwd_2(dx) + dh
+    (dh: h's residual-branch gradient, from slot_h when its consumer parks it there), then dy = rms_bwd_1(dh_total);
+    dh_total is the gradient of res (parked in slot_res for the pre-norm that also reads res, as AddRMSNormFn does)."""
 
     @staticmethod
     def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None):
@@ -137,13 +137,13 @@ class AddRMSNorm2Fn(torch.autograd.Function):
             if parked is not None:
                 dh = parked if dh is None else dh + parked
         dw2, acc2, ret2 = _grad_dest(w2, ctx.needs_input_grad[3])
+        dw1, acc1, ret1 = _grad_dest(w1, ctx.needs_input_grad[2])
         dht = torch.empty_like(h)
+        dy = torch.empty_like(y)
         if dx is None:
             dx = torch.zeros_like(h)
-        K.rmsnorm_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), dht, dw2, dw_accumulate=acc2)
-        dw1, acc1, ret1 = _grad_dest(w1, ctx.needs_input_grad[2])
-        dy = torch.empty_like(y)
-        K.rmsnorm_bwd(y, w1, r1, dht, None, dy, dw1, dw_accumulate=acc1)
+        # both norms' backward in one pass (bitwise the two svla_rmsnorm_bwd calls)
+        K.rmsnorm2_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), y, w1, r1, dht, dy, dw2, dw1, acc2, acc1)
         if slot_res is not None:
             slot_res.put(dht)
             return None, dy, ret1, ret2, None, None, None, None
@@ -278,6 +278,8 @@ class LinearFn(torch.autograd.Function):
 WEIGHT_EPOCH = [0]
 # fp8 projections: the input-gradient (dgrad) GEMMs run in e4m3 too (the weight-gradient GEMMs stay bf16)
 FP8_DGRAD = [True]
+# Gemma2 MLP backward: the GeGLU derivative in the down-projection dgrad's epilogue (False: plain dgrad + svla_geglu_bwd)
+FUSED_GEGLU_BWD = [os.environ.get("SVLA_FUSED_GEGLU_BWD", "1") != "0"]
 
 
 class FP8Weights:
@@ -563,14 +565,18 @@ class GemmaMLPFn(torch.autograd.Function):
         if dwd is not None:
             K.linear_wgrad(dout, h, [dwd], accumulate=acc)
         dgu = _empty(M, 2 * I, like=x)
-        # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (measured in the training
-        # step: the GEGLU_BWD GEMM epilogue cost +60% over the plain dgrad, the separate pass ~0.17 ms)
         f8 = ctx.f8 if FP8_DGRAD[0] else None
         if f8 is not None:
             _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
+            K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+        elif FUSED_GEGLU_BWD[0]:
+            # dH never reaches HBM: the 4-wave GEMM's direct epilogue turns each accumulator row chunk into dG, dU
+            # (svla_geglu_bwd's arithmetic, bitwise), its g / u loads one row block ahead
+            K.linear_dgrad(dout, [wd], dgu[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=dgu[:, :I],
+                           out2=dgu[:, I:])
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
-        K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+            K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)

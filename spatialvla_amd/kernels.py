@@ -403,6 +403,29 @@ def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False):
         colsum_f32(part[:npart.value], dw_out, dw_accumulate)
 
 
+def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1, acc2=False, acc1=False):
+    """Backward of add_rmsnorm2_fwd_train in one pass (svla_rmsnorm2_bwd); weight gradients dw2 / dw1 (or None) by
+    one column-sum launch over both partial planes (two when only one is wanted or the accumulate modes differ)."""
+    rows, N = h.shape
+    for t, n in ((h, "h"), (dx, "dx"), (y, "y"), (dh_out, "dh_out"), (dy_out, "dy_out")):
+        _req(t.shape == (rows, N) and t.is_contiguous(), f"rmsnorm2_bwd: {n} must be contiguous [{rows}, {N}]")
+    _req(dres is None or (dres.shape == (rows, N) and dres.is_contiguous()), "rmsnorm2_bwd: dres")
+    nb = (rows + RPB - 1) // RPB
+    part = torch.empty(2, nb, N, dtype=torch.float32, device=h.device)
+    npart = ctypes.c_int64(0)
+    L.check(L.lib().svla_rmsnorm2_bwd(rows, N, h.data_ptr(), w2.data_ptr(), rstd2.data_ptr(), dx.data_ptr(), _ptr(dres),
+                                      y.data_ptr(), w1.data_ptr(), rstd1.data_ptr(), dh_out.data_ptr(), dy_out.data_ptr(),
+                                      part.data_ptr(), ctypes.byref(npart), _stream()), "rmsnorm2_bwd")
+    if dw2 is not None and dw1 is not None and acc2 == acc1:
+        L.check(L.lib().svla_colsum2_f32(npart.value, N, part.data_ptr(), dw2.data_ptr(), dw1.data_ptr(), int(acc2),
+                                         _stream()), "colsum2_f32")
+    else:
+        if dw2 is not None:
+            colsum_f32(part[0], dw2, acc2)
+        if dw1 is not None:
+            colsum_f32(part[1], dw1, acc1)
+
+
 def layernorm_fwd(x, w, b, eps, y, mean, rstd):
     rows, N = x.shape
     L.check(L.lib().svla_layernorm_fwd(rows, N, x.data_ptr(), w.data_ptr(), b.data_ptr(), eps, y.data_ptr(),
@@ -733,6 +756,23 @@ def zoe_metric_tail(clb, feat, rel, emb, ctr):
                                          rel.data_ptr(), i64(rel), emb.data_ptr(), i64(emb), ctr.data_ptr(), i64(ctr),
                                          prm.data_ptr(), float(clb.p_eps), float(clb.max_temp), float(clb.min_temp),
                                          1e-4, out.data_ptr(), _stream()), "zoe_metric_tail")
+    return out
+
+
+def zoe_attractor(attractors: torch.Tensor, centres: torch.Tensor, alpha: float, gamma: int, mean: bool):
+    """ZoeDepthAttractorLayerUnnormed's bin update on the fused kernel (svla_zoe_attractor): attractors [B, NA, H, W],
+    centres [B, NB, H, W] (bf16, any strides; channels-last for the 16-B path) -> new centres, channels-last."""
+    B, NA, H, W = attractors.shape
+    _, NB, h2, w2 = centres.shape
+    _req(centres.shape[0] == B and (h2, w2) == (H, W), "zoe_attractor: attractors and centres must share B, H, W")
+    _chk_bf16(attractors, "zoe_attractor attractors")
+    _chk_bf16(centres, "zoe_attractor centres")
+    _req(NB % 8 == 0, "zoe_attractor: bin count must be a multiple of 8")
+    out = torch.empty(B, NB, H, W, dtype=BF16, device=centres.device, memory_format=torch.channels_last)
+    i64 = lambda t: (ctypes.c_int64 * 4)(*t.stride())  # noqa: E731
+    L.check(L.lib().svla_zoe_attractor(B, H, W, NA, NB, attractors.data_ptr(), i64(attractors), centres.data_ptr(),
+                                       i64(centres), float(alpha), int(gamma), int(bool(mean)), out.data_ptr(),
+                                       i64(out), _stream()), "zoe_attractor")
     return out
 
 

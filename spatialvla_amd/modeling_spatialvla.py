@@ -19,7 +19,7 @@ from typing import List, Optional, Tuple, Union
 import torch
 import torch.nn.functional as F
 from torch import nn
-from transformers import PreTrainedModel
+from transformers import GenerationMixin, PreTrainedModel
 from transformers.utils import ModelOutput
 
 from . import functional as Fn
@@ -126,7 +126,7 @@ class SpatialVLAPreTrainedModel(PreTrainedModel):
                 module.weight.data[module.padding_idx].zero_()
 
 
-class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel):
+class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMixin):
     def __init__(self, config: SpatialVLAConfig, vision_model=None, vision_zoe_model=None, projector_model=None,
                  language_model=None):
         super().__init__(config)

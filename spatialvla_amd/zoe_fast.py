@@ -28,7 +28,10 @@ another order (tolerances in tests/test_model_gpu.py):
 * Metric head tail (ZoeDepthMetricDepthEstimationHead.forward after the last attractor): on the GPU the
   relative-depth concat, both bilinear upsamplings, the 1x1-conv MLP, the log-binomial softmax over the bins
   and the bin-centre expectation run as one HIP kernel (svla_zoe_metric_tail, csrc/zoe.hip) with the eager
-  path's bf16 rounding points; the seed regressor, projectors and attractors stay stock modules.
+  path's bf16 rounding points.
+* Attractor layers (ZoeDepthAttractorLayerUnnormed.forward): the two align_corners resizes on the NHWC resize
+  kernel and the memory-efficient attractor loop as one kernel (svla_zoe_attractor) with the eager bf16 rounding
+  of each op; the 1x1 convs are the libsvla convs above, the ReLU / softplus and one add stay stock ops.
 """
 import types
 
@@ -76,11 +79,36 @@ def _metric_head_forward(self, outconv_activation, bottleneck, feature_blocks, r
     for projector, attractor, feature in zip(self.projectors, self.attractors, feature_blocks):
         bin_embedding = projector(feature)
         bin, bin_centers = attractor(bin_embedding, prev_bin, prev_bin_embedding, interpolate=True)
-        prev_bin = bin.clone()
-        prev_bin_embedding = bin_embedding.clone()
+        # the stock loop clones both (fresh tensors here, nothing writes them in place afterwards)
+        prev_bin = bin
+        prev_bin_embedding = bin_embedding
     from . import kernels as K
     return K.zoe_metric_tail(self.conditional_log_binomial, outconv_activation, relative_depth, bin_embedding,
                              bin_centers), None
+
+
+def _attractor_unnormed_forward(self, x, prev_bin, prev_bin_embedding=None, interpolate=True):
+    """ZoeDepthAttractorLayerUnnormed.forward (transformers zoedepth [3p]; the nyu-kitti head's four attractor layers)
+    with both align_corners resizes on the HIP NHWC kernel and the memory-efficient attractor loop (n_att x (sub,
+    inv_attractor, add) + zeros + mean + add, ~3 n_att + 3 launches) as one kernel (svla_zoe_attractor) with the same
+    bf16 rounding points; anything else keeps the stock module."""
+    if (not (_fast_ok(x) and prev_bin.dtype == torch.bfloat16 and prev_bin.dim() == 4 and prev_bin.shape[1] % 8 == 0)
+            or not self.memory_efficient or self.kind not in ("mean", "sum")):
+        return type(self).forward(self, x, prev_bin, prev_bin_embedding, interpolate)
+    from . import kernels as K
+    if prev_bin_embedding is not None:
+        if interpolate:
+            prev_bin_embedding = _interp(_cl(prev_bin_embedding), x.shape[-2:], mode="bilinear", align_corners=True)
+        x = x + prev_bin_embedding
+    x = self.conv1(x)
+    x = self.act1(x)
+    x = self.conv2(x)
+    attractors = self.act2(x)
+    height, width = attractors.shape[-2:]
+    bin_centers = _interp(_cl(prev_bin), (height, width), mode="bilinear", align_corners=True)
+    # inv_attractor's defaults (alpha 300, gamma 2): the module calls it without its own alpha / gamma
+    new = K.zoe_attractor(attractors, bin_centers, 300.0, 2, self.kind == "mean")
+    return new, new
 
 
 def _interp(x, size=None, scale_factor=None, mode="bilinear", align_corners=None):
@@ -346,6 +374,9 @@ def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout:
             m._svla_fast = True
         elif name == "ZoeDepthMetricDepthEstimationHead" and tail and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_metric_head_forward, m)
+            m._svla_fast = True
+        elif name == "ZoeDepthAttractorLayerUnnormed" and tail and not getattr(m, "_svla_fast", False):
+            m.forward = types.MethodType(_attractor_unnormed_forward, m)
             m._svla_fast = True
         elif name == "ZoeDepthPreActResidualLayer" and convs and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_preact_forward, m)

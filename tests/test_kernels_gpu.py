@@ -497,6 +497,30 @@ def test_rmsnorm(cuda):
     assert rel_l2(dx, xf.grad + res.float()) < 1e-2
 
 
+@pytest.mark.parametrize("R,N,with_dres,acc", [(624, 2304, True, (False, False)), (77, 2304, False, (True, False)),
+                                                (9, 4096, True, (False, False))])
+def test_rmsnorm2_bwd_bitwise_two_calls(cuda, R, N, with_dres, acc):
+    """svla_rmsnorm2_bwd (the norm pair's backward in one pass) gives dh, dy and both weight gradients of two
+    svla_rmsnorm_bwd calls bit for bit, with and without the residual gradient, accumulate modes equal or not."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(8)
+    y, h, dx = _r(R, N), _r(R, N), _r(R, N)
+    dres = _r(R, N) if with_dres else None
+    w1, w2 = _r(N, scale=0.1), _r(N, scale=0.1)
+    r1, r2 = torch.rand(R, device=cuda) + 0.5, torch.rand(R, device=cuda) + 0.5
+    base1, base2 = _r(N), _r(N)
+    dh0, dy0 = torch.empty_like(h), torch.empty_like(y)
+    dw2_0, dw1_0 = base2.clone(), base1.clone()
+    Kn.rmsnorm_bwd(h, w2, r2, dx, dres, dh0, dw2_0, dw_accumulate=acc[0])
+    Kn.rmsnorm_bwd(y, w1, r1, dh0, None, dy0, dw1_0, dw_accumulate=acc[1])
+    dh1, dy1 = torch.empty_like(h), torch.empty_like(y)
+    dw2_1, dw1_1 = base2.clone(), base1.clone()
+    Kn.rmsnorm2_bwd(h, w2, r2, dx, dres, y, w1, r1, dh1, dy1, dw2_1, dw1_1, acc[0], acc[1])
+    torch.cuda.synchronize()
+    for a, b, n in ((dh1, dh0, "dh"), (dy1, dy0, "dy"), (dw2_1, dw2_0, "dw2"), (dw1_1, dw1_0, "dw1")):
+        assert torch.equal(a, b), n
+
+
 def test_layernorm_colsum(cuda):
     from spatialvla_amd import kernels as Kn
     torch.manual_seed(5)
@@ -829,6 +853,24 @@ def test_geglu_bwd_kernel_matches_epilogue(cuda):
     F.gelu(gl, approximate="tanh").backward(torch.ones_like(gl))
     assert rel_l2(new[:, I:], dh * act) < 1e-2
     assert rel_l2(new[:, :I], (dh * uf) * gl.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,I", [(9984, 2304, 9216), (1024, 2304, 4608), (1000, 512, 4608)])
+def test_geglu_bwd_direct_epilogue_bitwise(cuda, M, K, I):
+    """The GEGLU_BWD epilogue on the 4-wave kernel (direct from the accumulators on interior tiles, the LDS image on
+    ragged ones; stream-K tiles included) equals the plain dH GEMM + svla_geglu_bwd bit for bit, at the 4B shape."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(15)
+    g, u = _r(M, I), _r(M, I)
+    wd, dout = _r(K, I, scale=0.05), _r(M, K)
+    fused = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+    Kn.linear_dgrad(dout, [wd], fused[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=fused[:, :I],
+                    out2=fused[:, I:])
+    ref = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+    Kn.linear_dgrad(dout, [wd], ref[:, :I])
+    Kn.geglu_bwd(ref[:, :I], g, u, ref[:, :I], ref[:, I:])
+    torch.cuda.synchronize()
+    assert torch.equal(fused, ref)
 
 
 def test_inv3x3_closed_form(cuda):

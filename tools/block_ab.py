@@ -1,5 +1,6 @@
 """A/B one Gemma2DecoderLayer fwd+bwd (bench.py's gemma2_block workload) with and without ResidualSlot fusion,
-interleaved on one box.  usage: python tools/block_ab.py [reps]"""
+interleaved on one box.  usage: python tools/block_ab.py [reps]
+  python tools/block_ab.py flag <geglu_bwd|norm_pair> [reps]: the same A/B toggling one fusion switch instead."""
 import os, sys, time
 import numpy as np
 import torch
@@ -61,6 +62,18 @@ def run(use_slot, iters=10):
     return np.mean(out, 0), x.grad.clone()
 
 
+if len(sys.argv) > 2 and sys.argv[1] == "flag":
+    from spatialvla_amd import modeling_gemma2 as MG
+    sw = Fn.FUSED_GEGLU_BWD if sys.argv[2] == "geglu_bwd" else MG.FUSED_NORM_PAIR
+    gs = {}
+    for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
+        for mode in (0, 1):
+            sw[0] = bool(mode)
+            (f, t), gx = run(True)
+            gs[mode] = gx
+            print(f"{sys.argv[2]}={mode} fwd {f:.3f} ms  fwd+bwd {t:.3f} ms", flush=True)
+    print("x.grad bitwise equal:", torch.equal(gs[0], gs[1]))
+    sys.exit(0)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 if len(sys.argv) > 2:  # profile mode: one configuration only (for rocprofv3 --kernel-trace)
     (f, t), _ = run(sys.argv[2] == "1", iters=int(sys.argv[3]) if len(sys.argv) > 3 else 10)

@@ -15,7 +15,8 @@ SHAPES = [  # name, M, N, K, layouts
     ("siglip qkv fwd", 8192, 3456, 1152, "nt"), ("siglip o fwd", 8192, 1152, 1152, "nt"),
     ("siglip fc2 fwd", 8192, 1152, 4304, "nt"), ("siglip fc2 dgrad", 8192, 4304, 1152, "nn"),
     ("siglip fc1 wgrad", 4304, 1152, 8192, "tn"), ("siglip o wgrad", 1152, 1152, 8192, "tn"),
-    ("qkv wgrad", 4096, 2304, M, "tn"), ("o dgrad", M, 2048, 2304, "nn"),
+    ("qkv wgrad", 4096, 2304, M, "tn"), ("o dgrad", M, 2048, 2304, "nn"), ("o wgrad", 2304, 2048, M, "tn"),
+    ("qkv dgrad", M, 2304, 4096, "nn"),
     ("square 4k", 4096, 4096, 4096, "nt"), ("square 8k", 8192, 8192, 8192, "nt"),
 ]
 
