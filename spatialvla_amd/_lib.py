@@ -99,7 +99,7 @@ SIGNATURES = {
     "svla_layernorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    ctypes.POINTER(c_i64), c_vp]),
     "svla_colsum_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
-    "svla_rmsnorm2_bwd": (c_i32, [c_i64, c_i64] + [c_vp] * 12 + [ctypes.POINTER(c_i64), c_vp]),
+    "svla_rmsnorm2_bwd": (c_i32, [c_i64, c_i64] + [c_vp] * 11 + [ctypes.POINTER(c_i64), c_vp]),
     "svla_colsum2_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "svla_colsum_bf16": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "svla_embed_merge": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),

@@ -1535,7 +1535,7 @@ static_assert(F8_RB1 >= 8 && F8_DA0 > F8_RB1 && F8_DB0 >= F8_DA0 + 4 && F8_RB2 >
 // The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
 // template are also instantiated for the host, where the device-only helpers they call fail to substitute and
 // the kernel stub silently disappears.
-template <int LA, int LB, bool F8 = false, bool GG = false, bool GB = false>
+template <int LA, int LB, bool F8 = false, bool GG = false>
 __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
                                            const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
                                            const SKArgs& sk, const F8Scales& fs) {
@@ -1814,11 +1814,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   };
   auto direct_epilogue = [&](int64_t m0, int64_t n0, int lane) -> bool {
     const int kind = E.kind;
-    if constexpr (GB) {  // the GeGLU-backward instance runs that epilogue only
-      if (kind != SVLA_EPI_GEGLU_BWD) return false;
-    } else if (!(kind == SVLA_EPI_STORE || (GG && (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE)))) {
-      return false;
-    }
+    if (!(kind == SVLA_EPI_STORE || (GG && (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE)))) return false;
     if (GG && kind == SVLA_EPI_STORE) return false;  // the paired kernel runs GEGLU and head-256 ROPE only
     if (m0 + BM > M || n0 + BN > N) return false;
     int cs = 0;
@@ -1907,52 +1903,6 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         });
       });
      }
-    } else if constexpr (GB) {
-      // dH = dY W_down (the accumulators) -> dG (out1), dU (out2) with svla_geglu_bwd's rounding points.  Rolling
-      // prefetch: chunk p's g / u registers are refilled with row block i + 1's chunk p as soon as row block i has
-      // consumed them, so 8 loads stay in flight.  Buffer descriptors based at the wave's 128 x 128 block keep the
-      // addressing at one VGPR per operand (row block in the SGPR offset, chunk in the immediate): with 64-bit
-      // pointers per row the kernel reached 504 VGPRs and spilled SGPRs to scratch
-      const int64_t rb = m0 + 128 * wr, cb = n0 + 128 * wc;
-      const __amdgpu_buffer_rsrc_t rg = make_rsrc((const bf16_t*)E.in0 + rb * E.ld_in0 + cb);
-      const __amdgpu_buffer_rsrc_t ru = make_rsrc((const bf16_t*)E.in1 + rb * E.ld_in1 + cb);
-      const __amdgpu_buffer_rsrc_t rdg = make_rsrc((const bf16_t*)E.out1 + rb * E.ld_out1 + cb);
-      const __amdgpu_buffer_rsrc_t rdu = make_rsrc((const bf16_t*)E.out2 + rb * E.ld_out2 + cb);
-      const uint32_t vg = (uint32_t)(r * E.ld_in0 + cofs) * 2, vu = (uint32_t)(r * E.ld_in1 + cofs) * 2;
-      const uint32_t vdg = (uint32_t)(r * E.ld_out1 + cofs) * 2, vdu = (uint32_t)(r * E.ld_out2 + cofs) * 2;
-      u32x4 gq[4], uq[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        gq[p] = __builtin_amdgcn_raw_buffer_load_b128(rg, vg + 64 * p, 0, 0);
-        uq[p] = __builtin_amdgcn_raw_buffer_load_b128(ru, vu + 64 * p, 0, 0);
-      }
-      static_for<0, 8>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        static_for<0, 4>([&](auto P) {
-          constexpr int p = decltype(P)::value;
-          f32x4 a = agpr_get<i * 8 + 2 * p>(), b = agpr_get<i * 8 + 2 * p + 1>();
-          swap4(a, b);
-          const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-          float gv[8], uv[8], dg[8], du[8];
-          unpack8(gq[p], gv);
-          unpack8(uq[p], uv);
-          if constexpr (i + 1 < 8) {
-            gq[p] = __builtin_amdgcn_raw_buffer_load_b128(rg, vg + 64 * p, (uint32_t)(32 * (i + 1) * E.ld_in0), 0);
-            uq[p] = __builtin_amdgcn_raw_buffer_load_b128(ru, vu + 64 * p, (uint32_t)(32 * (i + 1) * E.ld_in1), 0);
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float dh = round_bf(v[q]);
-            const float act = round_bf(gelu_tanh(gv[q]));
-            const float dact = round_bf(dh * uv[q]);
-            du[q] = dh * act;
-            dg[q] = dact * gelu_tanh_grad(gv[q]);
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(pack8(dg), rdg, vdg + 64 * p, (uint32_t)(32 * i * E.ld_out1), 0);
-          __builtin_amdgcn_raw_buffer_store_b128(pack8(du), rdu, vdu + 64 * p, (uint32_t)(32 * i * E.ld_out2), 0);
-          __builtin_amdgcn_sched_barrier(0);  // one chunk at a time: unbounded interleaving raised the VGPR peak
-        });
-      });
     } else {
       // one row chunk: v = 8 consecutive fp32 columns n .. n+7 of row m (reference rounding points of epi_pass_fast)
       const float alpha = E.alpha;
@@ -2176,8 +2126,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   auto direct_ok = [&](int64_t m0, int64_t n0) {
     if constexpr (F8) return false;
     const int kind = E.kind;
-    const bool k_ok = GG ? (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE)
-                         : (GB ? kind == SVLA_EPI_GEGLU_BWD : kind == SVLA_EPI_STORE);
+    const bool k_ok = GG ? (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE) : kind == SVLA_EPI_STORE;
     return k_ok && m0 + BM <= M && n0 + BN <= N;
   };
   int tile, kb, ke, st;
@@ -2293,12 +2242,6 @@ SVLA_GEMM4_KERNEL(1, 1)
 __global__ __launch_bounds__(256, 1) void gemm4_kernel_00g(int64_t M, int64_t N, int64_t K, svla_operand A,
                                                            svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
   gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, false, true>(M, N, K, A, B, Cd, E, sk, F8Scales{});
-}
-// Gemma2 down-projection dgrad (dY KC x W_down RC) with the GeGLU derivative in the direct epilogue: its own
-// instance, so the larger epilogue does not raise the register budget of the generic kernels
-__global__ __launch_bounds__(256, 1) void gemm4_kernel_01b(int64_t M, int64_t N, int64_t K, svla_operand A,
-                                                           svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
-  gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_RC, false, false, true>(M, N, K, A, B, Cd, E, sk, F8Scales{});
 }
 __global__ __launch_bounds__(256, 1) void gemm4f8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B,
                                                          CDesc Cd, svla_epilogue E, SKArgs sk, F8Scales fs) {
@@ -2919,7 +2862,10 @@ struct GemmCtx {
 using svla::num_cus;
 
 #ifndef G4_SKMIN
-#define G4_SKMIN 8  // fewest k-tiles per block of the 4-wave kernel's stream-K share
+// fewest k-tiles per block of the 4-wave kernel's stream-K share before a full wave of tiles is folded in as well:
+// 4, not 8 -- the o-projection dgrad (312 tiles, K = 2304) ran all-stream-K at 8 (every tile split, a 256 KB slab
+// per block) and 256 whole tiles + 56 split ones at 4: 132 -> 109 us (tools/gemm_ab.py, profiles/r4f_gemm_ab.txt)
+#define G4_SKMIN 4
 #endif
 
 // 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
@@ -3006,15 +2952,6 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     return svla::check_launch("gemm4 fp8");
   }
   const int la = A.layout, lb = B.layout;
-  if (E.kind == SVLA_EPI_GEGLU_BWD) {  // dispatcher: A KC, B RC only
-    static bool lds_set = false;
-    if (!lds_set) {
-      (void)hipFuncSetAttribute((const void*)gemm4_kernel_01b, hipFuncAttributeMaxDynamicSharedMemorySize, p4::LDS);
-      lds_set = true;
-    }
-    hipLaunchKernelGGL(gemm4_kernel_01b, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);
-    return svla::check_launch("gemm4 geglu_bwd");
-  }
   // GeGLU (B: two KC GEGLU segments, checked by the dispatcher) and head_dim-256 RoPE (q|k|v): the paired kernel
   if (E.kind == SVLA_EPI_GEGLU ||
       (E.kind == SVLA_EPI_ROPE && E.rope_D == 256 && la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC)) {
@@ -3272,8 +3209,9 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   // The k-loop floor is 384: the lm_head weight gradient (265344 x 2304 x 416) runs 0.70 ms here vs 0.85 ms on the
   // 8-phase kernel (tools/gemm_probe.py); head_dim-256 RoPE stores from the paired accumulators (qkv 0.23 -> 0.19 ms).
   const int ek = epi->kind;
-  const bool light_epi = ek == SVLA_EPI_STORE || ek == SVLA_EPI_BIAS || ek == SVLA_EPI_GEGLU || ek == SVLA_EPI_ROPE ||
-                         (ek == SVLA_EPI_GEGLU_BWD && A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_RC);
+  // (GEGLU_BWD measured in the direct epilogue of its own 4-wave instance, loads one row block ahead, r4: block
+  // fwd+bwd 5.00 -> 5.11 ms against plain dgrad + svla_geglu_bwd; the pass stays separate)
+  const bool light_epi = ek == SVLA_EPI_STORE || ek == SVLA_EPI_BIAS || ek == SVLA_EPI_GEGLU || ek == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
                     (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 384 && 4 * t256 >= num_cus()));
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile

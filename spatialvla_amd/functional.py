@@ -278,8 +278,6 @@ class LinearFn(torch.autograd.Function):
 WEIGHT_EPOCH = [0]
 # fp8 projections: the input-gradient (dgrad) GEMMs run in e4m3 too (the weight-gradient GEMMs stay bf16)
 FP8_DGRAD = [True]
-# Gemma2 MLP backward: the GeGLU derivative in the down-projection dgrad's epilogue (False: plain dgrad + svla_geglu_bwd)
-FUSED_GEGLU_BWD = [os.environ.get("SVLA_FUSED_GEGLU_BWD", "1") != "0"]
 
 
 class FP8Weights:
@@ -566,17 +564,14 @@ class GemmaMLPFn(torch.autograd.Function):
             K.linear_wgrad(dout, h, [dwd], accumulate=acc)
         dgu = _empty(M, 2 * I, like=x)
         f8 = ctx.f8 if FP8_DGRAD[0] else None
+        # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (in the down dgrad's epilogue
+        # it cost more than the pass: +60 % on the 8-phase kernel's LDS image, +0.11 ms per layer from the 4-wave
+        # kernel's accumulators with the g / u loads one row block ahead, r4)
         if f8 is not None:
             _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
-            K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
-        elif FUSED_GEGLU_BWD[0]:
-            # dH never reaches HBM: the 4-wave GEMM's direct epilogue turns each accumulator row chunk into dG, dU
-            # (svla_geglu_bwd's arithmetic, bitwise), its g / u loads one row block ahead
-            K.linear_dgrad(dout, [wd], dgu[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=dgu[:, :I],
-                           out2=dgu[:, I:])
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
-            K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+        K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)

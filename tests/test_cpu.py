@@ -144,6 +144,11 @@ def test_header_symbols_exported_by_library():
     for n in names:
         assert hasattr(lib, n), n
     assert names == set(_lib.SIGNATURES), "python binding must cover exactly the header"
+    # the binding's argument count equals the prototype's (a wrong count only fails at the first GPU call)
+    body = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    for m in re.finditer(r"(?:const char\*|int|size_t)\s+(svla_\w+)\s*\(([^)]*)\)\s*;", body):
+        params = [p for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(_lib.SIGNATURES[m.group(1)][1]), (m.group(1), len(params))
     _lib.load()
     assert b"gfx950" in _lib.lib().svla_version()
 

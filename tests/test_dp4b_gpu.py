@@ -11,8 +11,8 @@ Compared on sampled tensors (whole parameters, lm_head a row block), gathered fr
   * step 1 (identical weights on every process), the exchange: each rank's owned chunks after the bf16 AVG
     reduce-scatter equal the fp32 mean of the two ranks' local gradients (captured as each bucket enters the
     reduce-scatter) within one bf16 rounding of the addends' magnitude, elementwise;
-  * step 1, the model: that mean vs the single process's gradient, rel-L2 <= GRAD_TOL (q/k projections: the 8e-2
-    exception of test_full4b_gpu.py) on the scale of the addends, max(||g_single||, ||(|g_0| + |g_1|) / 2||) -- a
+  * step 1, the model: that mean vs the single process's gradient, rel-L2 <= GRAD_TOL (3e-2, every tensor) on the
+    scale of the addends, max(||g_single||, ||(|g_0| + |g_1|) / 2||) -- a
     gradient summed over two halves that cancel (the last SigLIP q bias) carries the halves' bf16 rounding.  The
     per-rank GEMMs see M = 312 instead of 624 rows (other tile / stream-K schedules, other fp32 partial-sum orders);
   * step 2's gradients are reported, not bounded: AdamW's first update is lr * g / |g| elementwise, so every element
@@ -58,10 +58,9 @@ SAMPLES = [
 
 
 def _grad_tol(name):
-    """GRAD_TOL, or the q/k-projection exception of tests/test_full4b_gpu.py (8e-2): their gradient passes through the
-    centred softmax gradient P o (dP - rowsum) of bf16 P, which amplifies any difference in the forward (here the
-    M = 312 vs 624 GEMM schedules) most in the deepest layers of the backward (measured r4: layer 0 q_proj 5.1e-2)."""
-    return 8e-2 if name.endswith(("self_attn.q_proj.weight", "self_attn.k_proj.weight")) else H.GRAD_TOL
+    """GRAD_TOL for every sampled tensor at step 1 (measured r4: max 2.5e-2, spatial_embed_tokens; the q/k-projection
+    exception of test_full4b_gpu.py is not needed here: layer 0 q_proj 1.8e-2)."""
+    return H.GRAD_TOL
 
 
 def _port():

@@ -855,24 +855,6 @@ def test_geglu_bwd_kernel_matches_epilogue(cuda):
     assert rel_l2(new[:, :I], (dh * uf) * gl.grad) < 1e-2
 
 
-@pytest.mark.parametrize("M,K,I", [(9984, 2304, 9216), (1024, 2304, 4608), (1000, 512, 4608)])
-def test_geglu_bwd_direct_epilogue_bitwise(cuda, M, K, I):
-    """The GEGLU_BWD epilogue on the 4-wave kernel (direct from the accumulators on interior tiles, the LDS image on
-    ragged ones; stream-K tiles included) equals the plain dH GEMM + svla_geglu_bwd bit for bit, at the 4B shape."""
-    from spatialvla_amd import kernels as Kn, _lib as L
-    torch.manual_seed(15)
-    g, u = _r(M, I), _r(M, I)
-    wd, dout = _r(K, I, scale=0.05), _r(M, K)
-    fused = torch.empty(M, 2 * I, dtype=BF, device=cuda)
-    Kn.linear_dgrad(dout, [wd], fused[:, :I], kind=L.EPI_GEGLU_BWD, in0=g, in1=u, out1=fused[:, :I],
-                    out2=fused[:, I:])
-    ref = torch.empty(M, 2 * I, dtype=BF, device=cuda)
-    Kn.linear_dgrad(dout, [wd], ref[:, :I])
-    Kn.geglu_bwd(ref[:, :I], g, u, ref[:, :I], ref[:, I:])
-    torch.cuda.synchronize()
-    assert torch.equal(fused, ref)
-
-
 def test_inv3x3_closed_form(cuda):
     """svla_inv3x3_f32 vs torch.linalg.inv on scaled camera intrinsics (the backproject_patch inverse, reference
     modeling_spatialvla.py:221) and on random well-conditioned matrices: fp32 rounding only."""

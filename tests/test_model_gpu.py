@@ -170,16 +170,14 @@ def test_tiny_vs_oracle_random_batch(cuda):
     assert res["argmax_agree_confident"] == 1.0
 
 
-@pytest.mark.parametrize("flag", ["norm_pair", "geglu_bwd"])
-def test_fused_norm_pair_bitwise(cuda, flag):
-    """The training step's fusions give the loss, logits and every gradient of the unfused path bit for bit:
-    norm_pair -- the post-attention + pre-feedforward norm pair in one launch forward and backward (AddRMSNorm2Fn);
-    geglu_bwd -- the GeGLU derivative in the down-projection dgrad's epilogue (functional.FUSED_GEGLU_BWD)."""
-    from spatialvla_amd import functional as Fn, modeling_gemma2 as MG, presets
+def test_fused_norm_pair_bitwise(cuda):
+    """The post-attention + pre-feedforward norm pair in one launch forward and backward (AddRMSNorm2Fn) gives the
+    loss, logits and every gradient of the two separate Functions bit for bit."""
+    from spatialvla_amd import modeling_gemma2 as MG, presets
     cfgd = H.cfg_dict("tiny")
     b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=2, seed=5), cuda)
     depth = torch.rand(2, 1, 224, 224, generator=torch.Generator().manual_seed(3)).mul(3).add(0.5).to(cuda)
-    sw = MG.FUSED_NORM_PAIR if flag == "norm_pair" else Fn.FUSED_GEGLU_BWD
+    sw = MG.FUSED_NORM_PAIR
     out = {}
     for fused in (True, False):
         sw[0] = fused

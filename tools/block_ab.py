@@ -1,6 +1,6 @@
 """A/B one Gemma2DecoderLayer fwd+bwd (bench.py's gemma2_block workload) with and without ResidualSlot fusion,
 interleaved on one box.  usage: python tools/block_ab.py [reps]
-  python tools/block_ab.py flag <geglu_bwd|norm_pair> [reps]: the same A/B toggling one fusion switch instead."""
+  python tools/block_ab.py flag norm_pair [reps]: the same A/B toggling the norm-pair fusion switch instead."""
 import os, sys, time
 import numpy as np
 import torch
@@ -64,7 +64,7 @@ def run(use_slot, iters=10):
 
 if len(sys.argv) > 2 and sys.argv[1] == "flag":
     from spatialvla_amd import modeling_gemma2 as MG
-    sw = Fn.FUSED_GEGLU_BWD if sys.argv[2] == "geglu_bwd" else MG.FUSED_NORM_PAIR
+    sw = MG.FUSED_NORM_PAIR
     gs = {}
     for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
         for mode in (0, 1):

@@ -1,5 +1,5 @@
 """A/B two libsvla builds in ONE process (interleaved rounds, best of N per arm): python tools/gemm_ab.py libA.so
-libB.so [shape-name filters].  Shapes from tools/gemm_bench.py; each build gets its own stream-K workspace."""
+libB.so [shape-name filters].  Shapes from tools/gemm_bench.py; both builds share kernels.gemm's stream-K workspace."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -9,11 +9,7 @@ from tools.gemm_bench import SHAPES, BF
 libs = []
 for path in sys.argv[1:3]:
     cd = L.load(os.path.abspath(path))
-    n = int(cd.svla_gemm_workspace_bytes())
-    ws = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    L.check(cd.svla_gemm_set_workspace(ws.data_ptr(), n), "ws")
-    libs.append((os.path.basename(path), cd, ws))
-K._gemm_ws[torch.cuda.current_device()] = libs[0][2]  # keep kernels.gemm from registering another
+    libs.append((os.path.basename(path), cd, None))  # kernels.gemm passes its (zero-kept) workspace per call
 sel = sys.argv[3:]
 for name, m, n, k, lay in SHAPES:
     if sel and not any(x in name for x in sel):
