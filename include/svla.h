@@ -378,6 +378,11 @@ int svla_clip_scale(const float* sumsq, float max_norm, float* clip_scale, float
 int svla_zoe_attractor(int B, int H, int W, int n_att, int n_bins, const void* attractors, const int64_t* a_strides,
                        const void* centres, const int64_t* c_strides, float alpha, int gamma, int mean, void* out,
                        const int64_t* out_strides, void* stream);
+/* DPT readout "project" input of the frozen Zoe estimator (transformers ZoeDepthReassembleStage.forward [3p], called
+ * from model/modeling_spatialvla.py:314-323): hidden [B, T + 1, C] bf16 (CLS first) -> out [B * T, 2C] with row
+ * (b, t) = [hidden(b, 1 + t), hidden(b, 0)] -- the values torch.cat(hidden_states) + permute + torch.cat((tokens,
+ * readout), -1) produce, in one pass; C % 8 == 0, 16-B aligned. */
+int svla_zoe_readout_cat(int64_t B, int64_t T, int64_t C, const void* hidden, void* out, void* stream);
 /* Bilinear resize of a channels-last bf16 map [B, H1, W1, C] -> [B, H2, W2, C] with torch's
  * upsample_bilinear2d semantics (transformers ZoeDepthFeatureFusionLayer.forward interpolate(scale_factor=2,
  * align_corners=True) and the relative head's nn.Upsample, called from modeling_spatialvla.py:317-323's Zoe

@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #define G4_STAMPS 0  // diagnostic build: per-wave cycles spent in each wait of the k-loop (tools/gemm_stamps.py)
 #endif
 #if G4_STAMPS
-__device__ unsigned long long g4_stamps[16384][4][11];  // [block][wave][top lgkm, RB1, RB2, k-loop, prologue, epilogue, tiles, total]
+__device__ unsigned long long g4_stamps[16384][4][14];  // [block][wave][top lgkm, RB1, RB2, k-loop, prologue, epilogue, tiles, total]
 #endif
 #ifndef G4_GROUP_M
 #define G4_GROUP_M GROUP_M
@@ -1562,7 +1562,8 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 
   const int64_t ksa = LA == SVLA_LAYOUT_KC ? 2 : A.ld * 2, ksb = LB == SVLA_LAYOUT_KC ? 2 : B.ld * 2;
 #if G4_STAMPS
-  unsigned long long stmp[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // [11..13]: stream-K mainloop ticks and k-tiles, data-parallel k-tiles (this block); [8..10] LDS-epilogue parts
+  unsigned long long stmp[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -2137,7 +2138,18 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t_in));
     int64_t m0, n0;
     coords(tile, m0, n0);
+#if G4_STAMPS
+    const unsigned long long tml = __builtin_amdgcn_s_memtime();
+#endif
     mainloop(m0, n0, kb, ke, t & 63, pre);
+#if G4_STAMPS
+    if (kb != 0 || ke != nk) {
+      stmp[11] += __builtin_amdgcn_s_memtime() - tml;
+      stmp[12] += ke - kb;
+    } else {
+      stmp[13] += ke - kb;
+    }
+#endif
     pre = false;
     if (kb != 0 || ke != nk) {
       // partial tile: the stream-K hand-off of gemm8_kernel (slab per segment, last arriver reduces in k order)
@@ -2224,7 +2236,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #if G4_STAMPS
   stmp[7] = __builtin_amdgcn_s_memtime() - tk0;
   if ((t_in & 63) == 0)
-    for (int i = 0; i < 11; ++i) g4_stamps[blockIdx.x % 16384][w][i] = stmp[i];
+    for (int i = 0; i < 14; ++i) g4_stamps[blockIdx.x % 16384][w][i] = stmp[i];
 #endif
 }
 

@@ -376,7 +376,30 @@ __global__ __launch_bounds__(256) void zoe_attractor_kernel(AttrArgs a) {
   }
 }
 
+// DPT readout "project" input (transformers ZoeDepthReassembleStage.forward [3p]): row r = (b, t) of the
+// [B*T, 2C] output is [hidden(b, 1 + t, :), hidden(b, 0, :)] -- the stacking cat, the NCHW round trip and the
+// readout cat of the stock module as one 16-B copy per chunk.
+__global__ __launch_bounds__(256) void zoe_readout_cat_kernel(int64_t B, int64_t T, int64_t C,
+                                                              const bf16_t* __restrict__ hs, bf16_t* __restrict__ out) {
+  const int64_t cpr = C >> 3;  // 16-B chunks per half row
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * T * 2 * cpr) return;
+  const int64_t r = idx / (2 * cpr), j = idx - r * 2 * cpr;
+  const int64_t b = r / T, t = r - b * T;
+  const bf16_t* src = j < cpr ? hs + (b * (T + 1) + 1 + t) * C + 8 * j : hs + b * (T + 1) * C + 8 * (j - cpr);
+  *reinterpret_cast<u32x4*>(out + r * 2 * C + 8 * j) = *reinterpret_cast<const u32x4*>(src);
+}
+
 }  // namespace
+
+extern "C" int svla_zoe_readout_cat(int64_t B, int64_t T, int64_t C, const void* hidden, void* out, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && T > 0 && C > 0 && C % 8 == 0 && hidden && out, "zoe_readout_cat: bad args");
+  SVLA_CHECK_ARG(((uintptr_t)hidden & 15) == 0 && ((uintptr_t)out & 15) == 0, "zoe_readout_cat: 16-B alignment");
+  const int64_t total = B * T * (C / 4);
+  hipLaunchKernelGGL(zoe_readout_cat_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     B, T, C, (const bf16_t*)hidden, (bf16_t*)out);
+  return svla::check_launch("zoe_readout_cat");
+}
 
 extern "C" int svla_zoe_attractor(int B, int H, int W, int n_att, int n_bins, const void* attractors,
                                   const int64_t* a_strides, const void* centres, const int64_t* c_strides, float alpha,

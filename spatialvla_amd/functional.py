@@ -842,6 +842,9 @@ class LMHeadCEFn(torch.autograd.Function):
         ctx.cap, ctx.V = cap, V
         ctx.row_plan = stash.pop("row_plan", None) if stash is not None else None
         ctx.mark_non_differentiable(logits_buf)
+        # the logits output never receives a gradient: without this autograd hands backward a materialised zero
+        # [M, V] bf16 tensor (5.3 GB at B=32, ~0.9 ms of fills per step, r4 ATen attribution)
+        ctx.set_materialize_grads(False)
         return logits_buf[:, :V], loss2[0]
 
     @staticmethod
@@ -852,6 +855,8 @@ class LMHeadCEFn(torch.autograd.Function):
         therefore run over the labelled rows only: dh is zero elsewhere and dW = sum over labelled rows, the same
         values as the dense products (whose other terms are exact zeros), at 1/24 of their cost."""
         h, w, logits_buf, lse, target, loss2 = ctx.saved_tensors
+        if dloss is None:  # the loss did not reach the graph's output
+            return None, None, None, None, None
         M, ldv = logits_buf.shape
         V = ctx.V
         gscale = (dloss.float() / torch.clamp(loss2[1], min=1.0)).reshape(1).contiguous()

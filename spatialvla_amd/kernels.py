@@ -759,6 +759,15 @@ def zoe_metric_tail(clb, feat, rel, emb, ctr):
     return out
 
 
+def zoe_readout_cat(hidden: torch.Tensor, out: torch.Tensor):
+    """svla_zoe_readout_cat: hidden [B, T + 1, C] (CLS first) -> out [B * T, 2C] rows [token, CLS]."""
+    B, T1, C = hidden.shape
+    _req(hidden.is_contiguous() and hidden.dtype == torch.bfloat16, "zoe_readout_cat: contiguous bf16 hidden")
+    _req(out.shape == (B * (T1 - 1), 2 * C) and out.is_contiguous(), "zoe_readout_cat: out [B*T, 2C]")
+    L.check(L.lib().svla_zoe_readout_cat(B, T1 - 1, C, hidden.data_ptr(), out.data_ptr(), _stream()),
+            "zoe_readout_cat")
+
+
 def zoe_attractor(attractors: torch.Tensor, centres: torch.Tensor, alpha: float, gamma: int, mean: bool):
     """ZoeDepthAttractorLayerUnnormed's bin update on the fused kernel (svla_zoe_attractor): attractors [B, NA, H, W],
     centres [B, NB, H, W] (bf16, any strides; channels-last for the 16-B path) -> new centres, channels-last."""

@@ -18,7 +18,8 @@ another order (tolerances in tests/test_model_gpu.py):
   bias, all on libsvla (functional.beit_layer); the bias is copied once per layer into [heads, L, round8(L)] rows.
 * DPT readout projections (ZoeDepthReassembleStage.readout_projects[i] = Linear(2H, H) + exact GELU): one libsvla
   GEMM with the BIAS_GELU_ERF epilogue (bf16(gelu_erf(bf16(acc + b))), the eager module's rounding points) instead
-  of the stock Linear (hipBLASLt) + elementwise GELU.
+  of the stock Linear (hipBLASLt) + elementwise GELU; its [token, CLS] input rows straight from the backbone's
+  hidden states (svla_zoe_readout_cat) and its output to the reassemble convs as a channels-last view.
 * Every convolution (nn.Conv2d / nn.ConvTranspose2d instances: the BEiT patch projection, the DPT reassemble
   projections and resizes, the neck's 3x3 convs, the fusion and relative-head convs, the metric head's 1x1 convs) on
   libsvla: svla_conv2d_nhwc implicit-GEMM on channels-last maps (csrc/conv.hip), the patchify conv as im2col + GEMM;
@@ -310,6 +311,30 @@ def _readout_forward(self, x):
     return out.view(*shp[:-1], lin.out_features)
 
 
+def _reassemble_forward(self, hidden_states, patch_height, patch_width):
+    """ZoeDepthReassembleStage.forward (transformers zoedepth [3p]) with readout "project": per stage the readout
+    GEMM's input rows [token, CLS] come from svla_zoe_readout_cat (the stock path's stacking cat, NCHW round trip
+    and readout cat: ~0.6 ms of ATen copies per step at B=32), and its [B*T, C] output goes to the reassemble
+    layer as a channels-last NCHW view (no permute copy; the convolutions read channels-last).  Same values."""
+    from . import kernels as K
+    hs0 = hidden_states[0]
+    if (self.readout_type != "project" or torch.is_grad_enabled() or not hs0.is_cuda
+            or hs0.dtype != torch.bfloat16 or hs0.shape[-1] % 8
+            or not all(getattr(p, "_svla_fast", False) for p in self.readout_projects)):
+        return type(self).forward(self, hidden_states, patch_height, patch_width)
+    B, T1, C = hs0.shape
+    if T1 - 1 != patch_height * patch_width:
+        return type(self).forward(self, hidden_states, patch_height, patch_width)
+    out = []
+    for s, hs in enumerate(hidden_states):
+        x = torch.empty(B * (T1 - 1), 2 * C, dtype=hs.dtype, device=hs.device)
+        K.zoe_readout_cat(hs.contiguous(), x)
+        y = self.readout_projects[s](x)
+        y = y.view(B, patch_height, patch_width, y.shape[-1]).permute(0, 3, 1, 2)
+        out.append(self.layers[s](y))
+    return out
+
+
 def _is_exact_gelu(m) -> bool:
     if isinstance(m, torch.nn.GELU):
         return m.approximate == "none"
@@ -343,7 +368,7 @@ def _patch_beit_mask():
 
 
 def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout: bool = True,
-            convs: bool = True) -> torch.nn.Module:
+            convs: bool = True, reassemble: bool = True) -> torch.nn.Module:
     """Patch the instances inside `zoe` (idempotent).  tail=False / beit=False / readout=False / convs=False keep
     the stock metric-head tail / BEiT layers / readout projections / convolutions (the other paths are bitwise
     identical to the stock modules)."""
@@ -357,6 +382,9 @@ def install(zoe: torch.nn.Module, tail: bool = True, beit: bool = True, readout:
                         and _is_exact_gelu(seq[1])):
                     seq.forward = types.MethodType(_readout_forward, seq)
                     seq._svla_fast = True
+            if reassemble and not getattr(m, "_svla_fast", False):
+                m.forward = types.MethodType(_reassemble_forward, m)
+                m._svla_fast = True
         if name == "BeitRelativePositionBias" and not getattr(m, "_svla_fast", False):
             m.forward = types.MethodType(_cached_rel_pos_bias(m.forward), m)
             m._svla_fast = True

@@ -74,6 +74,26 @@ def test_zoe_fast_paths_bitwise(cuda):
             assert torch.equal(fast(pixel_values=x).predicted_depth, d0)
 
 
+def test_zoe_reassemble_readout_cat_bitwise(cuda):
+    """ZoeDepthReassembleStage with the readout input built by svla_zoe_readout_cat and the readout output handed to
+    the reassemble convs as a channels-last view gives the depth of the stock stage (cat / permute / cat) bit for
+    bit, with every other fast path the same in both models."""
+    from transformers import ZoeDepthForDepthEstimation
+    from spatialvla_amd import zoe_fast
+    cfg = H.build_hip_model(H.cfg_dict("tiny"), "cuda:0").config.vision_zoe_config
+    torch.manual_seed(5)
+    ref = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
+    fast = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
+    fast.load_state_dict(ref.state_dict())
+    zoe_fast.install(ref, reassemble=False)
+    zoe_fast.install(fast)
+    x = torch.randn(2, 3, 384, 384, device=cuda).to(torch.bfloat16)
+    with torch.no_grad():
+        d0 = ref(pixel_values=x).predicted_depth
+        d1 = fast(pixel_values=x).predicted_depth
+    assert torch.equal(d1, d0)
+
+
 def test_zoe_fused_metric_tail(cuda):
     """The fused metric-head tail (csrc/zoe.hip) on the nyu-kitti head shapes (64 bins, 161->80->4 MLP) at
     384x384 vs the stock transformers tail on the same features; random-init weights, B=2.  The stock path
