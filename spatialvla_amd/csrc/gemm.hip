@@ -922,7 +922,7 @@ struct SKArgs {
   int dp_tiles;
   int nk;
   int grid;
-  int _pad;
+  int sk_first;      // 4-wave kernel: stream-K pieces before the data-parallel tiles, last piece first (gemm4_body)
   int64_t sk_iters;  // (tiles - dp_tiles) * nk, >= grid when nonzero
   float* slabs;      // [2 * grid][32 f32x4 x 512 threads]
   int* counters;     // [tiles - dp_tiles] (< 2 * grid), zero between launches
@@ -1260,6 +1260,9 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(int64_t M, int64_t N, int
 #endif
 #ifndef G4_RS
 #define G4_RS 1  // fragment reads: one per G4_RS MFMAs
+#endif
+#ifndef G4_SKFIRST_MIN
+#define G4_SKFIRST_MIN 40  // stream-K k-tiles per block from which launch4 orders the stream-K pieces first
 #endif
 #ifndef G4_STAMPS
 #define G4_STAMPS 0  // diagnostic build: per-wave cycles spent in each wait of the k-loop (tools/gemm_stamps.py)
@@ -2105,16 +2108,22 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   int* sflag = reinterpret_cast<int*>(smem);
   int dp_tile = L;
   int64_t it = (int64_t)L * I / G;
-  // the block's work items in order: its data-parallel tiles, then its stream-K k-range
-  auto next_item = [&](int& tile, int& kb, int& ke, int& st) -> bool {
-    st = 0;
-    if (dp_tile < sk.dp_tiles) {
-      tile = dp_tile;
-      dp_tile += sk.grid;
-      kb = 0;
-      ke = nk;
-      return true;
-    }
+  int64_t ithi = it1;
+  // The block's work items.  sk.sk_first 0: its data-parallel tiles, then its stream-K k-range from the low end (the
+  // tail of one tile, then the head of the next).  1: the stream-K pieces first, last piece first -- every block
+  // opens with the head (k = 0) of a tile at the same moment, so the blocks of an XCD that share an operand panel
+  // stream the same k-slices together (the low-end order left every block at its own k offset: 2x the L2->fabric
+  // fetch of hipBLASLt's stream-K on the q|k|v weight gradient, r4j), and the data-parallel tiles that follow start
+  // together too.  Pieces, slabs and the reduction order are the same, so the results are bitwise those of order 0.
+  auto next_dp = [&](int& tile, int& kb, int& ke) -> bool {
+    if (dp_tile >= sk.dp_tiles) return false;
+    tile = dp_tile;
+    dp_tile += sk.grid;
+    kb = 0;
+    ke = nk;
+    return true;
+  };
+  auto next_sk_low = [&](int& tile, int& kb, int& ke, int& st) -> bool {
     if (it >= it1) return false;
     st = (int)(it / nk);
     kb = (int)(it - (int64_t)st * nk);
@@ -2122,6 +2131,27 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     it += ke - kb;
     tile = sk.dp_tiles + st;
     return true;
+  };
+  auto next_sk_high = [&](int& tile, int& kb, int& ke, int& st) -> bool {
+    if (ithi <= it) return false;
+    st = (int)((ithi - 1) / nk);
+    const int64_t t0 = (int64_t)st * nk, pb = max(it, t0);
+    kb = (int)(pb - t0);
+    ke = (int)(ithi - t0);
+    ithi = pb;
+    tile = sk.dp_tiles + st;
+    return true;
+  };
+  auto next_item = [&](int& tile, int& kb, int& ke, int& st) -> bool {
+    st = 0;
+    if (sk.sk_first) {
+      if (next_sk_high(tile, kb, ke, st)) return true;
+      st = 0;
+      return next_dp(tile, kb, ke);
+    } else {
+      if (next_dp(tile, kb, ke)) return true;
+      return next_sk_low(tile, kb, ke, st);
+    }
   };
   // the direct epilogue (below) stores from the accumulators and leaves LDS untouched
   auto direct_ok = [&](int64_t m0, int64_t n0) {
@@ -2940,6 +2970,10 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
+    // long stream-K shares run first (tools/gemm_ab.py, profiles/r4k_skorder.txt: q|k|v wgrad 237 -> 175 us, gate/up
+    // dgrad 705 -> 666, wgrad 697 -> 659, down fwd 366 -> 347); short ones (the o projection, SigLIP at K = 1152) were
+    // 5-12 % slower that way
+    sk.sk_first = sk.sk_iters >= (int64_t)G4_SKFIRST_MIN * G ? 1 : 0;
     sk.slabs = reinterpret_cast<float*>(ctx.ws);
     sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * G * 32 * p8::NTH * 16);
   }
