@@ -176,24 +176,29 @@ def gemma2_block_roofline(model, B, L, device, iters=20):
     mac_tok = H * (hq + 2 * hkv) * D + hq * D * H + 3 * H * I + 2 * hq * L * D
     flops = 3 * 2.0 * mac_tok * B * L
     stream = torch.cuda.current_stream()
-    fwd_ms, tot_ms = [], []
-    # the layer's ~28 launches (and autograd's backward dispatch) are queued behind a GPU-side spin, so the events
-    # bracket the kernels' back-to-back execution rather than the Python dispatch of the first launches; the training
-    # step this layer sits in is GPU-bound (its ~2000 launches queue ahead of the GPU)
-    spin = getattr(torch.cuda, "_sleep", None)
-    for it in range(iters + 2):
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    # iterations run back to back (the host queues them ahead of the GPU, as in the training step this layer sits
+    # in) between two events; fwd from events around each forward.  A GPU-side spin ahead of each iteration (tried in
+    # round 4) lowered the clock the layer then ran at: 5.5 ms against 5.0-5.1 ms back to back on the same box.
+    def one(ev=None):
         x.grad = None
-        if spin is not None:
-            spin(int(20e6))  # ~10 ms of GPU cycles
-        e0.record(stream)
+        if ev is not None:
+            ev[0].record(stream)
         y = layer(x, mask, rope)
-        e1.record(stream)
+        if ev is not None:
+            ev[1].record(stream)
         y.backward(gy)
-        e2.record(stream)
-        e2.synchronize()
-        if it >= 2:
-            fwd_ms.append(e0.elapsed_time(e1)); tot_ms.append(e0.elapsed_time(e2))
+    for _ in range(3):
+        one()
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(iters)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for it in range(iters):
+        one(evs[it])
+    e1.record(stream)
+    e1.synchronize()
+    fwd_ms = [a.elapsed_time(b) for a, b in evs]
+    tot_ms = [e0.elapsed_time(e1) / iters]
     ms = float(np.median(tot_ms))
     ach = flops / (ms * 1e-3) / 1e12
     return {"what": f"Gemma2DecoderLayer fwd+bwd, B={B} x L={L} (M={B * L} token rows)", "bound": "mfma",

@@ -872,8 +872,18 @@ def test_inv3x3_closed_form(cuda):
 @pytest.mark.parametrize("M,N,K", [(300, 4304, 1152), (1024, 4096, 1024)])
 def test_gelu_rows_matches_epilogues(cuda, M, N, K):
     """Bias GEMM + svla_gelu_rows == the fused BIAS_GELU / BIAS_GELU_ERF epilogues, and plain dgrad + the backward
-    pass == the GELU_BWD epilogue, bit for bit."""
+    pass == the GELU_BWD epilogue, bit for bit.  Every GEMM here runs variant 2 (the 8-phase kernel, no stream-K):
+    the dispatcher puts the plain and the fused epilogues on different kernels whose stream-K splits (and so fp32
+    summation orders) differ, and the point is the epilogue arithmetic."""
     from spatialvla_amd import kernels as Kn, _lib as L
+    Kn.gemm_variant = 2
+    try:
+        _gelu_rows_vs_epilogues(cuda, Kn, L, M, N, K)
+    finally:
+        Kn.gemm_variant = 0
+
+
+def _gelu_rows_vs_epilogues(cuda, Kn, L, M, N, K):
     torch.manual_seed(41)
     x, w, b = _r(M, K), _r(N, K, scale=0.05), _r(N, scale=0.5)
     act_f, pre_f = torch.empty(M, N, dtype=BF, device=cuda), torch.empty(M, N, dtype=BF, device=cuda)
