@@ -242,8 +242,8 @@ int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* y
                          void* h, float* rstd, void* stream);
 /* Backward of the training pair svla_add_rmsnorm2_fwd_train (h = res + rms(y; w1), x = rms(h; w2)) in one pass:
  * dh_out = bf16(bf16(rms_bwd(h; dx)) + dres) (dres may be NULL), dy_out = bf16(rms_bwd(y; dh_out)); dw_partial: two
- * planes [2][ceil(rows/rows_per_block)][N] fp32 (w2's partials, then w1's) for svla_colsum2_f32.  Bitwise two
- * svla_rmsnorm_bwd calls. */
+ * planes [2][ceil(rows/8)][N] fp32 (w2's partials, then w1's) for svla_colsum2_f32.  dh_out / dy_out are bitwise
+ * two svla_rmsnorm_bwd calls; dw is the same sum over 8-row instead of 16-row partials. */
 int svla_rmsnorm2_bwd(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2, const void* dx,
                       const void* dres, const void* y, const void* w1, const float* rstd1, void* dh_out, void* dy_out,
                       float* dw_partial, int64_t* n_partial, void* stream);

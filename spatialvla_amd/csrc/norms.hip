@@ -10,7 +10,12 @@
 namespace {
 constexpr int NTH = 256;
 constexpr int MAXC = 4;  // rows up to 256*4*8 = 8192 elements
-constexpr int RPB = 16;  // rows per block in the backward kernels
+// Rows per block in the backward kernels (kernels.py mirrors both to size the weight-gradient partial planes).  The
+// norm-pair backward walks each row through two dependent block reductions: at 16 rows a block the 4B shape gave 624
+// blocks for 256 CUs (2.4 each) and 80.6 us, at 8 rows 70.5 us; the single-norm kernel is faster at 16 (35.1 vs
+// 38.5 us: half the partial rows) -- tools/norm_ab.py, profiles/r4o_norm_ab.txt.
+constexpr int RPB = 16;
+constexpr int RPB2 = 8;
 
 __device__ __forceinline__ void ld8(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const u32x4*>(p), f); }
 __device__ __forceinline__ void st8(bf16_t* p, const float* f) { *reinterpret_cast<u32x4*>(p) = pack8(f); }
@@ -222,8 +227,9 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
 //   dh = bf16(bf16(rms_bwd(h; dx)) + dres)    (stored: the residual-stream gradient of res)
 //   dy = bf16(rms_bwd(y; dh))
 // with the weight-gradient partials of both norms as two planes [2][blocks][N] (w2 first).  The per-row arithmetic and
-// reduction order are rms_bwd_kernel's, so dh / dy / the partials are bitwise those of two svla_rmsnorm_bwd calls;
-// one launch and one read of dh fewer.
+// reduction order are rms_bwd_kernel's, so dh / dy are bitwise those of two svla_rmsnorm_bwd calls; the weight
+// partials cover RPB2 = 8 rows a block (RPB = 16 there), the same sums reassociated.  One launch and one read of dh
+// fewer.
 template <int MC>
 __global__ __launch_bounds__(NTH) void rms_bwd2_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ h,
                                                        const bf16_t* __restrict__ w2, const float* __restrict__ rstd2,
@@ -244,8 +250,8 @@ __global__ __launch_bounds__(NTH) void rms_bwd2_kernel(int64_t rows, int64_t N, 
       ld8(w1 + ch * 8, wf1[c]);
     }
   }
-  const int64_t r0 = (int64_t)blockIdx.x * RPB;
-  const int nr = (int)min<int64_t>(RPB, rows - r0);
+  const int64_t r0 = (int64_t)blockIdx.x * RPB2;
+  const int nr = (int)min<int64_t>(RPB2, rows - r0);
   u32x4 ph[MC], pd[MC], pr[MC], py[MC];
   float prs2 = 0.f, prs1 = 0.f;
   auto fetch = [&](int64_t row) {
@@ -763,7 +769,7 @@ extern "C" int svla_rmsnorm2_bwd(int64_t rows, int64_t N, const void* h, const v
                  "rmsnorm2_bwd: null pointer");
   SVLA_CHECK_ARG(al16(h) && al16(w2) && al16(dx) && (!dres || al16(dres)) && al16(y) && al16(w1) && al16(dh_out) &&
                      al16(dy_out) && al16(dw_partial), "rmsnorm2_bwd: misaligned pointer");
-  const int64_t nb = (rows + RPB - 1) / RPB;
+  const int64_t nb = (rows + RPB2 - 1) / RPB2;
   if (n_partial) *n_partial = nb;
   if (N <= NTH * 8 * 2)
     hipLaunchKernelGGL(rms_bwd2_kernel<2>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,

@@ -377,7 +377,8 @@ def add_rmsnorm2_fwd_train(res, yin, w1, w2, eps1, eps2, h, x, rstd1, rstd2):
                                                 rstd1.data_ptr(), rstd2.data_ptr(), _stream()), "add_rmsnorm2_fwd_train")
 
 
-RPB = 16  # rows per block of the norm backward kernels (norms.hip)
+RPB = 16  # rows per block of the norm backward kernels (norms.hip RPB): sizes the weight-gradient partial planes
+RPB2 = 8  # the norm-pair backward's (norms.hip RPB2)
 
 
 def add_rmsnorm2_fwd(res, yin, w1, w2, eps1, eps2, h, x):
@@ -410,7 +411,7 @@ def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1,
     for t, n in ((h, "h"), (dx, "dx"), (y, "y"), (dh_out, "dh_out"), (dy_out, "dy_out")):
         _req(t.shape == (rows, N) and t.is_contiguous(), f"rmsnorm2_bwd: {n} must be contiguous [{rows}, {N}]")
     _req(dres is None or (dres.shape == (rows, N) and dres.is_contiguous()), "rmsnorm2_bwd: dres")
-    nb = (rows + RPB - 1) // RPB
+    nb = (rows + RPB2 - 1) // RPB2
     part = torch.empty(2, nb, N, dtype=torch.float32, device=h.device)
     npart = ctypes.c_int64(0)
     L.check(L.lib().svla_rmsnorm2_bwd(rows, N, h.data_ptr(), w2.data_ptr(), rstd2.data_ptr(), dx.data_ptr(), _ptr(dres),

@@ -497,11 +497,18 @@ def test_rmsnorm(cuda):
     assert rel_l2(dx, xf.grad + res.float()) < 1e-2
 
 
+def _within_bf16_step(a, b):
+    """|a - b| <= one bf16 step at b, elementwise (fp32 sums reassociated before the bf16 rounding)."""
+    step = torch.finfo(torch.bfloat16).eps * b.float().abs().clamp_min(1e-30)
+    return bool(((a.float() - b.float()).abs() <= step * 1.01).all())
+
+
 @pytest.mark.parametrize("R,N,with_dres,acc", [(624, 2304, True, (False, False)), (77, 2304, False, (True, False)),
                                                 (9, 4096, True, (False, False))])
 def test_rmsnorm2_bwd_bitwise_two_calls(cuda, R, N, with_dres, acc):
-    """svla_rmsnorm2_bwd (the norm pair's backward in one pass) gives dh, dy and both weight gradients of two
-    svla_rmsnorm_bwd calls bit for bit, with and without the residual gradient, accumulate modes equal or not."""
+    """svla_rmsnorm2_bwd (the norm pair's backward in one pass) gives dh and dy of two svla_rmsnorm_bwd calls bit
+    for bit, with and without the residual gradient, accumulate modes equal or not; its weight-gradient partials
+    cover 8 rows a block (16 in svla_rmsnorm_bwd), so dw agrees to fp32 reassociation: within one bf16 step."""
     from spatialvla_amd import kernels as Kn
     torch.manual_seed(8)
     y, h, dx = _r(R, N), _r(R, N), _r(R, N)
@@ -517,8 +524,10 @@ def test_rmsnorm2_bwd_bitwise_two_calls(cuda, R, N, with_dres, acc):
     dw2_1, dw1_1 = base2.clone(), base1.clone()
     Kn.rmsnorm2_bwd(h, w2, r2, dx, dres, y, w1, r1, dh1, dy1, dw2_1, dw1_1, acc[0], acc[1])
     torch.cuda.synchronize()
-    for a, b, n in ((dh1, dh0, "dh"), (dy1, dy0, "dy"), (dw2_1, dw2_0, "dw2"), (dw1_1, dw1_0, "dw1")):
+    for a, b, n in ((dh1, dh0, "dh"), (dy1, dy0, "dy")):
         assert torch.equal(a, b), n
+    for a, b, n in ((dw2_1, dw2_0, "dw2"), (dw1_1, dw1_0, "dw1")):
+        assert _within_bf16_step(a, b), n
 
 
 def test_layernorm_colsum(cuda):

@@ -192,7 +192,8 @@ def test_tiny_vs_oracle_random_batch(cuda):
 
 def test_fused_norm_pair_bitwise(cuda):
     """The post-attention + pre-feedforward norm pair in one launch forward and backward (AddRMSNorm2Fn) gives the
-    loss, logits and every gradient of the two separate Functions bit for bit."""
+    loss, logits and every gradient of the two separate Functions bit for bit, the pair's two norm weights to within
+    one bf16 step (their partial sums are grouped by 8 rows instead of 16)."""
     from spatialvla_amd import modeling_gemma2 as MG, presets
     cfgd = H.cfg_dict("tiny")
     b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=2, seed=5), cuda)
@@ -209,8 +210,13 @@ def test_fused_norm_pair_bitwise(cuda):
     (l1, lg1, g1, _), (l0, lg0, g0, _) = out[True], out[False]
     assert torch.equal(l1, l0) and torch.equal(lg1, lg0)
     assert g1.keys() == g0.keys()
+    step = torch.finfo(torch.bfloat16).eps
     for n in g1:
-        assert torch.equal(g1[n], g0[n]), n
+        if n.endswith(("post_attention_layernorm.weight", "pre_feedforward_layernorm.weight")):
+            # the pair's weight-gradient partials cover 8 rows (16 in the single-norm kernel): same sums reassociated
+            assert ((g1[n].float() - g0[n].float()).abs() <= 1.01 * step * g0[n].float().abs()).all(), n
+        else:
+            assert torch.equal(g1[n], g0[n]), n
 
 
 def _layer4b_model(li, cuda):
