@@ -225,6 +225,13 @@ int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t
 int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
                   const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
                   float* workspace, void* stream);
+/* The same backward for head_dim 256 (Gemma2, modeling_gemma2.py:169-195) with dS stored instead of recomputed:
+ * delta = rowsum(dO * O) -> dK/dV (which also writes dS^T, bf16 [B][Hq][round64(L)][round64(L)]) -> dQ = dS K.
+ * workspace: >= svla_attn_bwd_ds_workspace_bytes(B, L, Hq) bytes, 256-B aligned (delta, then dS^T). */
+size_t svla_attn_bwd_ds_workspace_bytes(int32_t B, int32_t L, int32_t Hq);
+int svla_attn_bwd_ds(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                     const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                     void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Norms.  Gemma2RMSNorm (modeling_gemma2.py:60-77): y = bf16(x*rsqrt(mean(x^2)+eps)*(1+w)) in fp32.

@@ -82,6 +82,9 @@ SIGNATURES = {
     "svla_attn_fwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_vp]),
     "svla_attn_bwd": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_i64, c_vp, c_vp]),
+    "svla_attn_bwd_ds_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32]),
+    "svla_attn_bwd_ds": (c_i32, [ctypes.POINTER(AttnArgs), c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                 c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
     "svla_attn_decode_workspace_bytes": (ctypes.c_size_t, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "svla_attn_decode": (c_i32, [ctypes.POINTER(AttnDecodeArgs), c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
     "svla_attn_decode_rope_workspace_bytes": (ctypes.c_size_t, [c_i32] * 6),

@@ -554,11 +554,12 @@ __device__ __forceinline__ float score_grad(float s, float dp, float lse2, float
 // heads of the group and their 32-row Q / dO tiles stream through one LDS stage by LDS-DMA (a co-resident block
 // covers the load); lse / delta of the group's heads and the key classes are preloaded to LDS.  ~70 KiB of LDS: two blocks per CU where registers allow
 // (D=72; at D=256 the K-row registers plus both accumulators need more than 256 VGPRs).
-template <int D, bool ROPE, bool CAP>
+template <int D, bool ROPE, bool CAP, bool DS = false>
 __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svla_attn_args a, const bf16_t* __restrict__ dout,
                                                               int64_t lddo, const float* __restrict__ lse,
                                                               const float* __restrict__ delta, bf16_t* __restrict__ dk,
-                                                              int64_t lddk, bf16_t* __restrict__ dv, int64_t lddv) {
+                                                              int64_t lddk, bf16_t* __restrict__ dv, int64_t lddv,
+                                                              bf16_t* __restrict__ dsT = nullptr) {
   constexpr int DP = Cfg<D>::DP, DV = Cfg<D>::DV, RS = Cfg<D>::RS;
   constexpr int NKS = DP / 32, NDT = DV / 16;
   constexpr int TB = tile_bytes<D>(64), QB = tile_bytes<D>(32);
@@ -682,6 +683,13 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
     if (plain) scores(std::true_type{});
     else scores(std::false_type{});
     const bf16x8 pa = pack_frag(pv), za = pack_frag(zv);
+    if constexpr (DS) {  // dS^T[b][h][key][q]: this lane's key, queries q0 + 16mt + 4g .. +3 (8 B each)
+      const int LPK = (L + 63) / 64 * 64;
+      const u32x4 zw = __builtin_bit_cast(u32x4, za);
+      bf16_t* dst = dsT + (((int64_t)b * a.Hq + hk * grp + hh) * LPK + kj) * LPK + q0 + 4 * g;
+      *reinterpret_cast<uint64_t*>(dst) = (uint64_t)zw[0] | ((uint64_t)zw[1] << 32);
+      *reinterpret_cast<uint64_t*>(dst + 16) = (uint64_t)zw[2] | ((uint64_t)zw[3] << 32);
+    }
     mfma_tr_sweep<RS, NDT, false>(adv, ldsO, 0, pa, lane);
     mfma_tr_sweep<RS, NDT, false>(adk, ldsQ, 0, za, lane);
   }
@@ -710,6 +718,101 @@ __global__ __launch_bounds__(256, D == 256 ? 1 : 2) void attn_bwd_dkv_kernel(svl
       *reinterpret_cast<u32x4*>(dv + ((int64_t)b * L + key) * lddv + (int64_t)hk * D + ch * 8) =
           *reinterpret_cast<const u32x4*>(imgV + r * DV + ch * 8);
     }
+  }
+}
+
+// ================================================================== backward with stored dS (head_dim 256)
+// delta = rowsum(dO * O) per (b, h, q) row, one wave a row (the dS path runs it before dK/dV, which needs it).
+// head_dim 256: 32 lanes x 16 B a row, two rows a wave, eight a block.
+__global__ __launch_bounds__(256) void attn_delta_kernel(int B, int L, int H, const bf16_t* __restrict__ o,
+                                                         int64_t ldo, const bf16_t* __restrict__ dout, int64_t lddo,
+                                                         float* __restrict__ delta) {
+  constexpr int D = 256;
+  const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);  // (b, q, h) rows
+  const int l32 = threadIdx.x & 31;
+  const bool ok = row < (int64_t)B * L * H;
+  const int64_t rw = ok ? row : 0;
+  const int h = (int)(rw % H);
+  const int64_t bq = rw / H;
+  const int q = (int)(bq % L), b = (int)(bq / L);
+  float x[8], y[8];
+  unpack8(*reinterpret_cast<const u32x4*>(o + bq * ldo + (int64_t)h * D + 8 * l32), x);
+  unpack8(*reinterpret_cast<const u32x4*>(dout + bq * lddo + (int64_t)h * D + 8 * l32), y);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += x[j] * y[j];
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);  // within the 32-lane half
+  if (l32 == 0 && ok) delta[((int64_t)b * H + h) * L + q] = s;
+}
+
+// dQ = dS K from the dS^T tiles the dK/dV kernel stored ([b][h][key][query], bf16, rows and columns padded to 64):
+// no second recompute of S, P and dP.  Block = (query tile of 64, query head, batch), 4 waves x 16 queries; per
+// 64-key tile the K rows (LDS-DMA) and the dS^T tile go to LDS, and each wave multiplies its 16 queries' dS (the A
+// operand, in the dQ kernel's key order) into the K rows by mfma_tr_sweep, as attn_bwd_dq_kernel does with dS it
+// recomputes.  Epilogue: RoPE transpose, bf16 rows.
+template <bool ROPE>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(svla_attn_args a, const bf16_t* __restrict__ dsT,
+                                                                bf16_t* __restrict__ dq, int64_t lddq) {
+  constexpr int D = 256, RS = Cfg<256>::RS, DV = Cfg<256>::DV, NDT = DV / 16;
+  constexpr int TB = tile_bytes<D>(64), SB = 64 * 64 * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int L = a.L, LPK = (L + 63) / 64 * 64;
+  int qt, h, b;
+  block_coords(LPK / 64, a.Hq, qt, h, b);
+  const int t = threadIdx.x, lane = t & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int hk = h / (a.Hq / a.Hkv);
+  const bf16_t* kbase = (const bf16_t*)a.k + (int64_t)b * L * a.ldk + (int64_t)hk * D;
+  const bf16_t* sbase = dsT + ((int64_t)b * a.Hq + h) * LPK * LPK + qt * 64;
+  // one stage (40 KB, several blocks a CU): a double-buffered version (80 KB) ran 52 vs 46 us per layer
+  const bf16_t* ls = (const bf16_t*)(smem + TB);
+  f32x4 acc[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < LPK / 64; ++kt) {
+    __syncthreads();  // the previous tile is consumed
+    glds_tile<RS, 64, 4>(smem, kbase + (int64_t)kt * 64 * a.ldk, a.ldk, L - kt * 64, D, w, lane);
+    u32x4 sv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + 256 * u, r = i >> 3, ch = i & 7;
+      sv[u] = *reinterpret_cast<const u32x4*>(sbase + (int64_t)(kt * 64 + r) * LPK + ch * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = t + 256 * u, r = i >> 3, ch = i & 7;
+      *reinterpret_cast<u32x4*>(smem + TB + (r * 64 + ch * 8) * 2) = sv[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float zv[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // keys 32ks + 4g + j and 32ks + 16 + 4g + j of the wave's query 16w + c
+        zv[j] = bf2f(ls[(32 * ks + 4 * g + j) * 64 + 16 * w + c]);
+        zv[4 + j] = bf2f(ls[(32 * ks + 16 + 4 * g + j) * 64 + 16 * w + c]);
+      }
+      mfma_tr_sweep<RS, NDT, false>(acc, smem, 32 * ks, pack_frag(zv), lane);
+    }
+  }
+  // acc: C[q = 16w + 4g + j][d = 16dt + c]
+  if constexpr (ROPE) rope_t_acc<NDT>(acc, a, qt * 64 + 16 * w, L, g, c);
+  __syncthreads();
+  bf16_t* img = (bf16_t*)smem + w * 16 * DV;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) img[(4 * g + j) * DV + 16 * dt + c] = f2bf(acc[dt][j]);
+  __syncthreads();
+  constexpr int CPR = D / 8;
+  for (int idx = lane; idx < 16 * CPR; idx += 64) {
+    const int r = idx / CPR, ch = idx % CPR;
+    const int q = qt * 64 + 16 * w + r;
+    if (q < L)
+      *reinterpret_cast<u32x4*>(dq + ((int64_t)b * L + q) * lddq + (int64_t)h * D + ch * 8) =
+          *reinterpret_cast<const u32x4*>(img + r * DV + ch * 8);
   }
 }
 
@@ -883,10 +986,29 @@ int fwd_launch(const svla_attn_args& a, bf16_t* out, int64_t ldo, float* lse, hi
 template <int D, int NH, bool ROPE, bool CAP>
 int bwd_launch(const svla_attn_args& a, const bf16_t* out, int64_t ldo, const bf16_t* dout, int64_t lddo,
                const float* lse, float* delta, bf16_t* dq, int64_t lddq, bf16_t* dk, int64_t lddk, bf16_t* dv,
-               int64_t lddv, hipStream_t s) {
+               int64_t lddv, hipStream_t s, bf16_t* dsT = nullptr) {
   const int grp = a.Hq / a.Hkv;
   const int LP = (a.L + 35) / 32 * 32;
   const int nt = (a.L + 63) / 64;
+  if constexpr (D == 256) {
+    if (dsT) {  // delta -> dK/dV (storing dS^T) -> dQ = dS K
+      const int64_t rows = (int64_t)a.B * a.L * a.Hq;
+      hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, s, a.B, a.L, a.Hq, out,
+                         ldo, dout, lddo, delta);
+      if (int rc = svla::check_launch("attn_delta")) return rc;
+      const int lds_kv = tile_bytes<D>(64) + 4 * tile_bytes<D>(32) + 8 * grp * LP + round16(a.L);
+      SVLA_CHECK_ARG(lds_kv <= 160 * 1024, "attn_bwd: L*group too large for the LDS-resident lse/delta");
+      set_lds_once<attn_bwd_dkv_kernel<D, ROPE, CAP, true>>(lds_kv);
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE, CAP, true>), dim3((unsigned)(nt * a.Hkv * a.B)), dim3(256),
+                         lds_kv, s, a, dout, lddo, lse, delta, dk, lddk, dv, lddv, dsT);
+      if (int rc = svla::check_launch("attn_bwd_dkv")) return rc;
+      const int lds_q = tile_bytes<D>(64) + 64 * 64 * 2;
+      set_lds_once<attn_bwd_dq_ds_kernel<ROPE>>(lds_q);
+      hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<ROPE>), dim3((unsigned)(nt * a.Hq * a.B)), dim3(256), lds_q, s, a,
+                         dsT, dq, lddq);
+      return svla::check_launch("attn_bwd_dq_ds");
+    }
+  }
   // dQ first: it forms delta = rowsum(dO * O) for its queries (no separate pass) and leaves it for dK/dV
   const int lds_q = 4 * tile_bytes<D>(64) + round16(a.L);
   set_lds_once<attn_bwd_dq_kernel<D, NH, ROPE, CAP>>(lds_q);
@@ -936,17 +1058,17 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
 template <int D, int NH>
 static int bwd_dispatch(const svla_attn_args& a, bool rope, bool cap, const bf16_t* o, int64_t ldo, const bf16_t* d_o,
                         int64_t lddo, const float* lse, float* delta, void* dq, int64_t lddq, void* dk, int64_t lddk,
-                        void* dv, int64_t lddv, hipStream_t s) {
+                        void* dv, int64_t lddv, hipStream_t s, bf16_t* ds = nullptr) {
   bf16_t *q = (bf16_t*)dq, *k = (bf16_t*)dk, *v = (bf16_t*)dv;
-  if (rope) return cap ? bwd_launch<D, NH, true, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
-                       : bwd_launch<D, NH, true, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
-  return cap ? bwd_launch<D, NH, false, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s)
-             : bwd_launch<D, NH, false, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s);
+  if (rope) return cap ? bwd_launch<D, NH, true, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s, ds)
+                       : bwd_launch<D, NH, true, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s, ds);
+  return cap ? bwd_launch<D, NH, false, true>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s, ds)
+             : bwd_launch<D, NH, false, false>(a, o, ldo, d_o, lddo, lse, delta, q, lddq, k, lddk, v, lddv, s, ds);
 }
 
-extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
-                             const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
-                             float* workspace, void* stream) {
+static int attn_bwd_impl(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                         const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                         float* workspace, bf16_t* ds, void* stream) {
   if (int rc = check_args(a)) return rc;
   SVLA_CHECK_ARG(a->D != 64 && !a->bias, "attn_bwd: head_dim 64 / additive bias are forward-only (frozen BEiT)");
   const bool rope = a->rope_cos != nullptr;
@@ -959,8 +1081,33 @@ extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t l
   const bool cap = a->softcap > 0.f;
   const bf16_t *o = (const bf16_t*)out, *d_o = (const bf16_t*)dout;
   if (a->D == 256)
-    return pair ? bwd_dispatch<256, 2>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s)
-                : bwd_dispatch<256, 1>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
-  SVLA_CHECK_ARG(!rope, "attn_bwd: RoPE only with D=256");
+    return pair ? bwd_dispatch<256, 2>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s, ds)
+                : bwd_dispatch<256, 1>(*a, rope, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s, ds);
+  SVLA_CHECK_ARG(!rope && !ds, "attn_bwd: RoPE and the stored-dS path only with D=256");
   return bwd_dispatch<72, 1>(*a, false, cap, o, ldo, d_o, lddo, lse, workspace, dq, lddq, dk, lddk, dv, lddv, s);
+}
+
+extern "C" int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,
+                             const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                             float* workspace, void* stream) {
+  return attn_bwd_impl(a, out, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, workspace, nullptr, stream);
+}
+
+static size_t delta_bytes(int32_t B, int32_t L, int32_t Hq) { return ((size_t)B * Hq * L * 4 + 255) / 256 * 256; }
+
+extern "C" size_t svla_attn_bwd_ds_workspace_bytes(int32_t B, int32_t L, int32_t Hq) {
+  const size_t lpk = ((size_t)L + 63) / 64 * 64;
+  return delta_bytes(B, L, Hq) + (size_t)B * Hq * lpk * lpk * 2;
+}
+
+extern "C" int svla_attn_bwd_ds(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout,
+                                int64_t lddo, const float* lse, void* dq, int64_t lddq, void* dk, int64_t lddk,
+                                void* dv, int64_t lddv, void* workspace, size_t ws_bytes, void* stream) {
+  if (int rc = check_args(a)) return rc;
+  SVLA_CHECK_ARG(a->D == 256, "attn_bwd_ds: head_dim 256 only");
+  SVLA_CHECK_ARG(workspace && ((uintptr_t)workspace & 255) == 0 &&
+                     ws_bytes >= svla_attn_bwd_ds_workspace_bytes(a->B, a->L, a->Hq),
+                 "attn_bwd_ds: workspace must be 256-B aligned and svla_attn_bwd_ds_workspace_bytes long");
+  bf16_t* ds = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(workspace) + delta_bytes(a->B, a->L, a->Hq));
+  return attn_bwd_impl(a, out, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, (float*)workspace, ds, stream);
 }

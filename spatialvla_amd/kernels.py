@@ -578,7 +578,20 @@ def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
                                          int(p0), _stream()), "qkv_rope_append")
 
 
+# head_dim-256 backward with dS stored by the dK/dV kernel and dQ = dS K (svla_attn_bwd_ds) instead of the dQ kernel
+# that recomputes S, P and dP (svla_attn_bwd); SVLA_ATTN_DS=0 selects the latter
+ATTN_DS = [os.environ.get("SVLA_ATTN_DS", "1") != "0"]
+
+
 def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):
+    if a.D == 256 and ATTN_DS[0]:
+        n = int(L.lib().svla_attn_bwd_ds_workspace_bytes(a.B, a.L, a.Hq))
+        buf = torch.empty(n + 256, dtype=torch.uint8, device=out.device)
+        off = (-buf.data_ptr()) % 256
+        L.check(L.lib().svla_attn_bwd_ds(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),
+                                         lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv,
+                                         buf.data_ptr() + off, n, _stream()), "attn_bwd_ds")
+        return
     ws = torch.empty(a.B * a.Hq * a.L, dtype=torch.float32, device=out.device)
     L.check(L.lib().svla_attn_bwd(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),
                                   lse.data_ptr(), dq.data_ptr(), lddq, dk.data_ptr(), lddk, dv.data_ptr(), lddv,

@@ -609,12 +609,26 @@ def _ref_attn(q, k, v, scale, cap, kv_class, window, cos=None, sin=None):
     return (p @ v).transpose(1, 2)
 
 
+@pytest.mark.parametrize("ds", [True, False])
 @pytest.mark.parametrize("D,Hq,Hkv,L,rope,cap", [(256, 2, 1, 140, True, 50.0), (256, 8, 4, 312, True, 50.0),
                                                  (256, 4, 1, 200, True, 50.0), (256, 3, 3, 100, True, 50.0),
                                                  (256, 2, 2, 65, False, 0.0),
                                                  (72, 2, 2, 256, False, 0.0), (72, 3, 3, 70, False, 0.0)])
-def test_attention(cuda, D, Hq, Hkv, L, rope, cap):
+def test_attention(cuda, D, Hq, Hkv, L, rope, cap, ds):
+    """Forward and backward against the fp32 eager reference; head_dim 256 through both backward paths: dS stored
+    by the dK/dV kernel and dQ = dS K (svla_attn_bwd_ds, ds=True, the product's) and the dQ kernel that recomputes
+    S, P and dP (svla_attn_bwd)."""
     from spatialvla_amd import kernels as Kn
+    if D != 256 and ds:
+        pytest.skip("the stored-dS backward is the head_dim-256 path")
+    Kn.ATTN_DS[0] = ds
+    try:
+        _attention_case(cuda, Kn, D, Hq, Hkv, L, rope, cap)
+    finally:
+        Kn.ATTN_DS[0] = True
+
+
+def _attention_case(cuda, Kn, D, Hq, Hkv, L, rope, cap):
     torch.manual_seed(6)
     B = 2
     qkv = _r(B * L, (Hq + 2 * Hkv) * D)

@@ -1,6 +1,7 @@
 """A/B one Gemma2DecoderLayer fwd+bwd (bench.py's gemma2_block workload) with and without ResidualSlot fusion,
 interleaved on one box.  usage: python tools/block_ab.py [reps]
-  python tools/block_ab.py flag norm_pair [reps]: the same A/B toggling the norm-pair fusion switch instead."""
+  python tools/block_ab.py flag norm_pair|attn_ds [reps]: the same A/B toggling one switch instead (the norm-pair
+  fusion, or the stored-dS attention backward)."""
 import os, sys, time
 import numpy as np
 import torch
@@ -64,7 +65,8 @@ def run(use_slot, iters=10):
 
 if len(sys.argv) > 2 and sys.argv[1] == "flag":
     from spatialvla_amd import modeling_gemma2 as MG
-    sw = MG.FUSED_NORM_PAIR
+    from spatialvla_amd import kernels as Kn
+    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS}[sys.argv[2]]
     gs = {}
     for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
         for mode in (0, 1):
