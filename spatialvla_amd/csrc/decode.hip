@@ -274,6 +274,49 @@ __global__ __launch_bounds__(NT) void attn_decode_split_kernel(svla_attn_decode_
     // combine (attn_decode_combine_kernel's arithmetic and order), chunks in batches of CB whose sc1 loads are all
     // issued before the first use
     constexpr int CB = 8;
+    constexpr int PER = (G * D + NT - 1) / NT;  // outputs per thread
+    if (nch <= CB) {
+      // up to 8 chunks (Lk <= 512, the decode of every SpatialVLA prompt): every partial this thread needs -- both
+      // of its outputs, max, sum and O of every chunk -- is loaded in one batch, so the combine is one memory round
+      // trip instead of 2 * PER dependent ones; the same arithmetic in the same order as the loop below
+      float mv[PER][CB], lv[PER][CB], ov[PER][CB];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * NT;
+        const int g = i / D, d = i % D;
+        const float* o0 = ws + ws_index(bq, hk * G + (i < G * D ? g : 0), 0, a.Hq, nch, D);
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+          mv[k][u] = -INFINITY;
+          if (u < nch && i < G * D) {
+            const float* o = o0 + (int64_t)u * (D + 2);
+            mv[k][u] = ws_load_sc1(o + D);
+            lv[k][u] = ws_load_sc1(o + D + 1);
+            ov[k][u] = ws_load_sc1(o + d);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * NT;
+        if (i >= G * D) continue;
+        const int g = i / D, d = i % D, h = hk * G + g;
+        float M = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < CB; ++u) M = fmaxf(M, mv[k][u]);
+        float l = 0.f, acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+          if (u < nch) {
+            const float fc = __expf(mv[k][u] - M);
+            l = fmaf(lv[k][u], fc, l);
+            acc = fmaf(ov[k][u], fc, acc);
+          }
+        }
+        f.out[(int64_t)bq * f.ldo + (int64_t)h * D + d] = f2bf(acc / l);
+      }
+      return;
+    }
     for (int i = tid; i < G * D; i += NT) {
       const int g = i / D, d = i % D, h = hk * G + g;
       const float* o0 = ws + ws_index(bq, h, 0, a.Hq, nch, D);
