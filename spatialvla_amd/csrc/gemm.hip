@@ -3295,11 +3295,33 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
 // statistics are bitwise the fused epilogue's.  Persistent blocks, the bf16 tanh table staged in LDS once per block.
 // ------------------------------------------------------------------------------------------------------------
 namespace {
+// softcap_bf16_tab on a packed bf16 pair, returning the packed bf16 results: the two roundings are one
+// v_cvt_pk_bf16_f32 each, and the range tests fold into one unsigned offset d = |a| - lo: d < NTAB indexes the table,
+// NTAB <= d <= 0x7f80 - lo (|a| >= 4, inf included) reads the sentinel entry tab[NTAB] = 1.0, and d beyond that (|a|
+// below the table: tanh(a) = a in bf16; NaN) keeps |a|.  Bitwise softcap_bf16_tab<_, true> of each element.
+constexpr uint32_t TAB_LO = (uint32_t)SVLA_TANH_TAB_E0 << 7, TAB_N = ((uint32_t)SVLA_TANH_TAB_E1 << 7) - TAB_LO;
+static_assert(TAB_N * 2 == TANH_TAB_BYTES, "table covers [E0, E1) exactly");
+template <typename Tab>
+__device__ __forceinline__ uint32_t softcap_pair_tab(uint32_t w, float cap, float icap, const Tab& tab) {
+  const uint32_t a = pack2(__uint_as_float(w << 16) * icap, __uint_as_float(w & 0xffff0000u) * icap);
+  uint32_t t[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t ab = (a >> (16 * h)) & 0x7fffu;
+    const uint32_t d = ab - TAB_LO;
+    const uint32_t tb = tab[min(d, TAB_N)];
+    const uint32_t rb = d > 0x7f80u - TAB_LO ? ab : tb;
+    t[h] = (((a >> (16 * h)) & 0x8000u) | rb) << 16;
+  }
+  return pack2(__uint_as_float(t[0]) * cap, __uint_as_float(t[1]) * cap);
+}
+
 __global__ __launch_bounds__(256) void softcap_rows_kernel(int64_t M, int64_t N, bf16_t* __restrict__ lg, int64_t ld,
                                                            float cap, float* __restrict__ row_stats) {
-  __shared__ __attribute__((aligned(16))) unsigned short tab[TANH_TAB_BYTES / 2];
+  __shared__ __attribute__((aligned(16))) unsigned short tab[TANH_TAB_BYTES / 2 + 8];  // + the 1.0 sentinel
   if ((int)threadIdx.x < TANH_TAB_BYTES / 16)
     reinterpret_cast<u32x4*>(tab)[threadIdx.x] = reinterpret_cast<const u32x4*>(svla_tanh_bf16_tab)[threadIdx.x];
+  if (threadIdx.x == 0) tab[TAB_N] = 0x3f80;
   __syncthreads();
   const float icap = 1.0f / cap;
   const int lane = threadIdx.x & 63;
@@ -3315,7 +3337,20 @@ __global__ __launch_bounds__(256) void softcap_rows_kernel(int64_t M, int64_t N,
     float v[8];
     float mx = -INFINITY, se = 0.f;
     int am = 0x7fffffff;
-    if (nv > 0) {
+    if (nv >= 8) {  // whole 16-B chunk: packed pairs, the result words stored as they come
+      const u32x4 w = *reinterpret_cast<const u32x4*>(p);
+      u32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = softcap_pair_tab(w[i], cap, icap, tab);
+      *reinterpret_cast<u32x4*>(p) = o;
+      unpack8(o, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[j] > mx) { mx = v[j]; am = (int)(n + j); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) se += __expf(v[j] - mx);
+      if (mx == -INFINITY) se = 0.f;
+    } else if (nv > 0) {
       load8f(p, v, nv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {

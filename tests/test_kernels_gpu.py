@@ -445,6 +445,27 @@ def test_softcap_every_bf16_logit(cuda, M):
                               f"{got[0][~same[0]][:5].tolist()} vs {ref[~same[0]][:5].tolist()}")
 
 
+def test_softcap_rows_every_bf16_logit(cuda):
+    """Every bf16 logit value (finite and +-inf) through svla_softcap_ce_rows in place -- the packed-pair table path of
+    whole 16-B chunks and the scalar path of a ragged row end -- against the reference's op-by-op bf16 softcap
+    (modeling_gemma2.py:994-997) in float64: bit-exact."""
+    from spatialvla_amd import kernels as Kn
+    vals = torch.arange(-32768, 32768, dtype=torch.int32).to(torch.int16).view(torch.bfloat16)
+    vals = vals[~torch.isnan(vals.float())]
+    for V in (vals.numel(), vals.numel() - 3):  # ragged row ends: 2 and 7 values in the last 8-column chunk
+        ldv = Kn.round_up(V, 64)
+        buf = torch.zeros(2, ldv, dtype=BF, device=cuda)
+        buf[:, :V] = vals[:V].to(cuda)
+        stats = torch.empty(2, Kn.ceil_div(V, 128), 3, dtype=torch.float32, device=cuda)
+        Kn.softcap_ce_rows(buf, V, stats, 30.0)
+        x = vals[:V].double()
+        ref = ((x / 30.0).to(torch.bfloat16).double().tanh().to(torch.bfloat16).double() * 30.0).to(torch.bfloat16)
+        got = buf[:, :V].cpu()
+        same = got.view(torch.int16) == ref.view(torch.int16)[None, :]
+        assert bool(same.all()), (f"{int((~same).sum())} mismatches, e.g. {vals[:V][~same[0]][:5].tolist()} -> "
+                                  f"{got[0][~same[0]][:5].tolist()} vs {ref[~same[0]][:5].tolist()}")
+
+
 @pytest.mark.parametrize("M,H,V,every", [(300, 256, 1000, 7), (9984 // 8, 2304, 4099, 24), (64, 128, 300, 0)])
 def test_lm_head_ce_fn_label_rows(cuda, M, H, V, every):
     """LMHeadCEFn's backward runs the softmax gradient and both lm_head GEMMs over the labelled rows only;
