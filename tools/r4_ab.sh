@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 A/B of the in-tree build against ab/lib_prev.so (the previous commit's library): norm passes, attention
-# (plus optional variant libs), greedy decode (prev / new / prev), then the affected GPU tests.
+# (plus optional variant libs), greedy decode (prev / new / prev), then the affected GPU tests (AB_TESTS).
 # usage: bash tools/r4_ab.sh [variant.so ...]
 set -o pipefail
 O=gpurun_out/r4ab
@@ -11,5 +11,5 @@ for arm in prev new prev2; do
   lib=ab/lib_prev.so; [ $arm = new ] && lib=spatialvla_amd/libsvla.so
   SVLA_LIB=$lib timeout -k 10 300 python -u tools/decode_bench.py --reps 3 --no-uncached > $O/decode_$arm.json 2> $O/decode_$arm.err || exit $?
 done
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_kernels_gpu.py \
-  -k "rms or norm or attention or decode" tests/test_full4b_gpu.py -s > $O/tests.txt 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread ${AB_TESTS:-tests/test_decode_gpu.py} \
+  -s > $O/tests.txt 2>&1
