@@ -27,6 +27,9 @@ logits = torch.empty(R, LDV, dtype=BF, device=dev)
 logits.view(-1)[:].copy_((torch.randn(R * LDV // 64, device=dev) * 8).repeat_interleave(64).to(BF))  # 5.3 GB
 stats = torch.empty(R, (V + 127) // 128, 3, device=dev)
 small = (torch.randn(512, LDV, device=dev) * 8).to(BF)
+gsig = r(8192, 4304)
+part = torch.randn(624, 2304, device=dev)
+cs1, cs2, cs3 = (torch.empty(n, dtype=BF, device=dev) for n in (4304, 1152, 2304))
 
 
 def softcap_small():
@@ -48,6 +51,9 @@ def cases():
         "rms_bwd": (lambda: K.rmsnorm_bwd(x, w1, rs1, dy, dres, o1, dw1), (o1, dw1)),
         "rms_bwd2": (lambda: K.rmsnorm2_bwd(x, w2, rs2, dy, dres, y, w1, rs1, o1, o2, dw2, dw1), (o1, o2, dw1, dw2)),
         "softcap_rows": (lambda: K.softcap_ce_rows(logits, V, stats, 30.0), None),
+        "colsum_bf16_4304": (lambda: K.colsum_bf16(gsig, cs1), (cs1,)),  # SigLIP fc1 bias gradient
+        "colsum_bf16_1152": (lambda: K.colsum_bf16(gsig[:, :1152], cs2), (cs2,)),
+        "colsum_f32_2304": (lambda: K.colsum_f32(part, cs3), (cs3,)),  # norm-weight partial planes
     }
 
 
