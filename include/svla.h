@@ -279,8 +279,11 @@ int svla_colsum_f32(int64_t P, int64_t N, const float* in, void* out_bf16, int32
 /* The two planes [2][P][N] of svla_layernorm_bwd in one launch: out0 = bf16(sum_p in[0][p]), out1 = plane 1. */
 int svla_colsum2_f32(int64_t P, int64_t N, const float* in, void* out0_bf16, void* out1_bf16, int32_t accumulate,
                      void* stream);
-/* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients of nn.Linear), one launch, fixed order.
- * N % 8 == 0, ldx % 8 == 0; workspace unused (may be NULL). */
+/* out[n] = bf16(sum_m x[m, n]) over a bf16 matrix (bias gradients of nn.Linear), fixed order, run-to-run bitwise.
+ * N % 8 == 0, ldx % 8 == 0.  workspace: NULL = one launch (one block per 32 columns), or
+ * svla_colsum_bf16_workspace_bytes(M, N) bytes (16-B aligned; 0 = the split does not pay) = row slices summed into
+ * fp32 partial rows, then reduced in slice order (two launches, the chip filled for narrow N). */
+size_t svla_colsum_bf16_workspace_bytes(int64_t M, int64_t N);
 int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16, int32_t accumulate,
                      float* workspace, void* stream);
 

@@ -105,6 +105,7 @@ SIGNATURES = {
     "svla_rmsnorm2_bwd": (c_i32, [c_i64, c_i64] + [c_vp] * 11 + [ctypes.POINTER(c_i64), c_vp]),
     "svla_colsum2_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "svla_colsum_bf16": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "svla_colsum_bf16_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "svla_embed_merge": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     "svla_embed_merge_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp]),
     "svla_ego3d_encode": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp,

@@ -7,6 +7,8 @@
 // (one launch) — no atomics, bitwise reproducible.
 #include "svla_common.h"
 
+#include <algorithm>
+
 namespace {
 constexpr int NTH = 256;
 constexpr int MAXC = 4;  // rows up to 256*4*8 = 8192 elements
@@ -715,8 +717,70 @@ int launch_colsum1(int64_t P, int64_t N, const T* in, int64_t ld, int64_t plane_
   return svla::check_launch("colsum");
 }
 
+// Row-split bf16 column sums (bias gradients of SigLIP's nn.Linear layers): a single pass gives one block per 32
+// columns -- 36 to 135 blocks for N = 1152 .. 4304, most CUs idle.  Slice s of S sums rows [s*RS, (s+1)*RS) per
+// column exactly as colsum1_kernel does over its rows (row groups, fixed order) into fp32 partial row s of the
+// workspace; a second colsum1 launch reduces the S partial rows in slice order.
+template <int CB>
+__global__ __launch_bounds__(256) void colsum_slice_kernel(int64_t M, int64_t N, const bf16_t* __restrict__ in,
+                                                           int64_t ld, int64_t rows_per_slice,
+                                                           float* __restrict__ part) {
+  constexpr int CL = CB / 8, RG = 256 / CL;
+  __shared__ float red[RG][CB + 1];
+  const int cl = threadIdx.x % CL, rg = threadIdx.x / CL;
+  const int64_t n0 = (int64_t)blockIdx.x * CB + cl * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slice, r1 = min(M, r0 + rows_per_slice);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (n0 < N) {
+    const bf16_t* src = in + n0;
+    int64_t p = r0 + rg;
+    auto add_row = [&](int64_t q) {
+      float v[8];
+      unpack8(*reinterpret_cast<const u32x4*>(src + q * ld), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    };
+    for (; p + 3 * RG < r1; p += 4 * RG) {
+      add_row(p);
+      add_row(p + RG);
+      add_row(p + 2 * RG);
+      add_row(p + 3 * RG);
+    }
+    for (; p < r1; p += RG) add_row(p);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][cl * 8 + j] = s[j];
+  __syncthreads();
+  if (threadIdx.x < CB) {
+    const int64_t n = (int64_t)blockIdx.x * CB + threadIdx.x;
+    if (n < N) {
+      float t = 0.f;
+      for (int q = 0; q < RG; ++q) t += red[q][threadIdx.x];
+      part[(int64_t)blockIdx.y * N + n] = t;
+    }
+  }
+}
+
+// slices for an M x N bf16 column sum: about 1024 blocks of 32 columns, slices of at least 512 rows -- only below 64
+// column blocks (tools/colsum_ab.py, profiles/r4t_colsum_split_ab.txt: 8192 x 1152 14.8 -> 9.6 us; at 3456 / 4304
+// columns the split ran 18.2 -> 20.5 / 25.1 -> 28.6 us, the single pass is not short of blocks there)
+int64_t colsum_slices(int64_t M, int64_t N) {
+  const int64_t cb = (N + 31) / 32;
+  if (cb >= 64) return 1;
+  int64_t S = (1024 + cb - 1) / cb;
+  S = std::min<int64_t>(S, M / 512);
+  return S < 2 ? 1 : S;
+}
+
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
+
+extern "C" size_t svla_colsum_bf16_workspace_bytes(int64_t M, int64_t N) {
+  const int64_t S = colsum_slices(M, N);
+  return S > 1 ? (size_t)S * (size_t)N * sizeof(float) : 0;
+}
 
 extern "C" int svla_rmsnorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, float eps, void* y,
                                 float* rstd, void* stream) {
@@ -831,9 +895,17 @@ extern "C" int svla_colsum2_f32(int64_t P, int64_t N, const float* in, void* out
 
 extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx, void* out_bf16,
                                 int32_t accumulate, float* workspace, void* stream) {
-  (void)workspace;  // single pass since round 4; kept in the ABI
   SVLA_CHECK_ARG(M > 0 && N > 0 && N % 8 == 0 && x && out_bf16 && ldx >= N && ldx % 8 == 0 && al16(x),
                  "colsum_bf16: bad args");
+  const int64_t S = colsum_slices(M, N);
+  if (workspace && S > 1) {  // sized by svla_colsum_bf16_workspace_bytes(M, N)
+    const int64_t rps = (M + S - 1) / S;
+    hipLaunchKernelGGL(colsum_slice_kernel<32>, dim3((unsigned)((N + 31) / 32), (unsigned)S), dim3(256), 0,
+                       (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, rps, workspace);
+    if (int rc = svla::check_launch("colsum_bf16 slices")) return rc;
+    return launch_colsum1<float>(S, N, workspace, N, 0, 1, (bf16_t*)out_bf16, nullptr, accumulate,
+                                 (hipStream_t)stream);
+  }
   return launch_colsum1<bf16_t>(M, N, (const bf16_t*)x, ldx, 0, 1, (bf16_t*)out_bf16, nullptr, accumulate,
                                 (hipStream_t)stream);
 }

@@ -460,11 +460,14 @@ def colsum_f32(part, out, accumulate=False):
 
 
 def colsum_bf16(x, out, accumulate=False):
-    """out[n] = bf16(sum_m x[m, n]) (+ out) over a row-strided bf16 matrix (bias gradients), one launch."""
+    """out[n] = bf16(sum_m x[m, n]) (+ out) over a row-strided bf16 matrix (bias gradients): row slices into an fp32
+    workspace and their reduction where one block per 32 columns would leave the chip idle, else one launch."""
     M, N = x.shape
     _req(out.numel() == N and out.is_contiguous(), "colsum_bf16: [N] contiguous output")
-    L.check(L.lib().svla_colsum_bf16(M, N, x.data_ptr(), _ld(x), out.data_ptr(), int(accumulate), None, _stream()),
-            "colsum_bf16")
+    nb = int(L.lib().svla_colsum_bf16_workspace_bytes(M, N))
+    ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=x.device) if nb else None
+    L.check(L.lib().svla_colsum_bf16(M, N, x.data_ptr(), _ld(x), out.data_ptr(), int(accumulate),
+                                     ws.data_ptr() if ws is not None else None, _stream()), "colsum_bf16")
 
 
 # ---------------------------------------------------------------------------------------- attention
