@@ -763,12 +763,13 @@ __global__ __launch_bounds__(256) void colsum_slice_kernel(int64_t M, int64_t N,
   }
 }
 
-// slices for an M x N bf16 column sum: about 1024 blocks of 32 columns, slices of at least 512 rows -- only below 64
-// column blocks (tools/colsum_ab.py, profiles/r4t_colsum_split_ab.txt: 8192 x 1152 14.8 -> 9.6 us; at 3456 / 4304
-// columns the split ran 18.2 -> 20.5 / 25.1 -> 28.6 us, the single pass is not short of blocks there)
+// slices for an M x N bf16 column sum: about 1024 blocks of CS_CB = 64 columns (a whole 128-B line of every row per
+// block: at 32 columns two blocks on different XCDs each fetched half of every line), slices of at least 512 rows.
+// tools/colsum_ab.py, profiles/r4u_colsum_cb64_ab.txt: 8192 x 4304 25.1 -> 21.8 us, x 3456 17.9 -> 12.5, x 1152
+// 14.8 -> 6.5 (32-column slices: 28.6 / 20.2 / 9.5, so they were kept to N < 2048 before)
+constexpr int CS_CB = 64;
 int64_t colsum_slices(int64_t M, int64_t N) {
-  const int64_t cb = (N + 31) / 32;
-  if (cb >= 64) return 1;
+  const int64_t cb = (N + CS_CB - 1) / CS_CB;
   int64_t S = (1024 + cb - 1) / cb;
   S = std::min<int64_t>(S, M / 512);
   return S < 2 ? 1 : S;
@@ -900,7 +901,7 @@ extern "C" int svla_colsum_bf16(int64_t M, int64_t N, const void* x, int64_t ldx
   const int64_t S = colsum_slices(M, N);
   if (workspace && S > 1) {  // sized by svla_colsum_bf16_workspace_bytes(M, N)
     const int64_t rps = (M + S - 1) / S;
-    hipLaunchKernelGGL(colsum_slice_kernel<32>, dim3((unsigned)((N + 31) / 32), (unsigned)S), dim3(256), 0,
+    hipLaunchKernelGGL(colsum_slice_kernel<CS_CB>, dim3((unsigned)((N + CS_CB - 1) / CS_CB), (unsigned)S), dim3(256), 0,
                        (hipStream_t)stream, M, N, (const bf16_t*)x, ldx, rps, workspace);
     if (int rc = svla::check_launch("colsum_bf16 slices")) return rc;
     return launch_colsum1<float>(S, N, workspace, N, 0, 1, (bf16_t*)out_bf16, nullptr, accumulate,
