@@ -341,7 +341,7 @@ def main():
     n_train = sum(p.numel() for p in model.parameters() if p.requires_grad)
     total = args.warmup + args.steps
     engine = TrainEngine(model, lr=2e-5, weight_decay=0.0, max_grad_norm=1.0, warmup_ratio=0.005,
-                         total_steps=max(total, 10))
+                         total_steps=max(total, 10), defer_host_checks=True)
     log(f"[bench] rank {rank}/{world}: model built in {time.perf_counter() - t0:.1f}s, trainable {n_train / 1e9:.3f}B, "
         f"flat buffers {engine.numel / 1e9:.3f}B elems, buckets {len(engine.buckets)}")
     batches = [make_batch(cfgd, B, args.seed + 1000 * rank + s, device) for s in range(total)]

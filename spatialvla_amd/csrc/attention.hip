@@ -751,6 +751,10 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(int B, int L, int H, co
 // 64-key tile the K rows (LDS-DMA) and the dS^T tile go to LDS, and each wave multiplies its 16 queries' dS (the A
 // operand, in the dQ kernel's key order) into the K rows by mfma_tr_sweep, as attn_bwd_dq_kernel does with dS it
 // recomputes.  Epilogue: RoPE transpose, bf16 rows.
+// Padded query columns: when L % 64 is 1..32 the dK/dV kernel writes dS^T only up to query round32(L), so columns
+// round32(L)..round64(L)-1 of the workspace hold whatever the allocator left there (possibly NaN patterns).  Query
+// column q of dS^T feeds only output row q of dQ (it is the A operand's row), and rows q >= L are never stored (the
+// q < L test of the epilogue), so those columns cannot reach a result; no zero-fill is needed.
 template <bool ROPE>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(svla_attn_args a, const bf16_t* __restrict__ dsT,
                                                                 bf16_t* __restrict__ dq, int64_t lddq) {

@@ -177,10 +177,15 @@ class TrainEngine:
 
     def __init__(self, model, lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  max_grad_norm: float = 1.0, warmup_ratio: float = 0.005, total_steps: int = 1000,
-                 process_group=None, bucket_bytes: int = 256 << 20, overlap: bool = True, kernels=None):
+                 process_group=None, bucket_bytes: int = 256 << 20, overlap: bool = True, kernels=None,
+                 defer_host_checks: bool = False):
         """kernels: the optimizer kernel module (sumsq / clip_scale / adamw); the libsvla wrappers unless a test
-        injects a stand-in to exercise the exchange logic without a GPU."""
+        injects a stand-in to exercise the exchange logic without a GPU.
+        defer_host_checks: opt-in; the model's image-token count check (reference modeling_spatialvla.py:379-385)
+        is then raised from the next forward instead of the current one, so no step waits on a host read."""
         self.model = model
+        if defer_host_checks and hasattr(model, "defer_checks"):
+            model.defer_checks = True
         self.K = kernels if kernels is not None else K
         if hasattr(model, "clear_decode_cache"):  # captured decode graphs point at the storage rebound below
             model.clear_decode_cache()

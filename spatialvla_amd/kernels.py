@@ -584,11 +584,14 @@ def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
 # head_dim-256 backward with dS stored by the dK/dV kernel and dQ = dS K (svla_attn_bwd_ds) instead of the dQ kernel
 # that recomputes S, P and dP (svla_attn_bwd); SVLA_ATTN_DS=0 selects the latter
 ATTN_DS = [os.environ.get("SVLA_ATTN_DS", "1") != "0"]
+# The stored-dS workspace is bf16 B*Hq*round64(L)^2 (52 MB at the 4B training shape, B=32, L=312) and grows with L^2
+# (2 GiB per call at B=8, L=4096); above this cap the recomputing path (B*Hq*L fp32 of workspace) runs instead.
+ATTN_DS_MAX_BYTES = int(os.environ.get("SVLA_ATTN_DS_MAX_MB", "512")) << 20
 
 
 def attn_bwd(a: L.AttnArgs, out, dout, lse, dq, lddq, dk, lddk, dv, lddv):
-    if a.D == 256 and ATTN_DS[0]:
-        n = int(L.lib().svla_attn_bwd_ds_workspace_bytes(a.B, a.L, a.Hq))
+    n = int(L.lib().svla_attn_bwd_ds_workspace_bytes(a.B, a.L, a.Hq)) if a.D == 256 and ATTN_DS[0] else 0
+    if 0 < n <= ATTN_DS_MAX_BYTES:
         buf = torch.empty(n + 256, dtype=torch.uint8, device=out.device)
         off = (-buf.data_ptr()) % 256
         L.check(L.lib().svla_attn_bwd_ds(ctypes.byref(a), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout),

@@ -13,6 +13,7 @@ hand in already-rotated q/k/v as the reference does.
 """
 import math
 import os
+import warnings
 from dataclasses import dataclass
 from typing import Optional
 
@@ -202,7 +203,8 @@ class Gemma2Attention(nn.Module):
                                             cache.value_cache[i], cache.kv_class, cache.seen_tokens, cfg)
             return out.view(B, Lq, H)
         if cos.shape[0] != Lq and torch.is_grad_enabled() and (
-                hidden_states.requires_grad or any(w.requires_grad for w in (self.q_proj.weight, self.k_proj.weight))):
+                hidden_states.requires_grad or any(w.requires_grad for w in (self.q_proj.weight, self.k_proj.weight,
+                                                                             self.v_proj.weight, self.o_proj.weight))):
             # autograd.Function.forward runs with grad mode off, so this is checked here, where the caller's grad
             # mode is visible: the attention backward applies the RoPE transpose with table row = position in the
             # sequence, which per-sequence tables ([B*L] rows, padded prompts) would not match
@@ -426,7 +428,13 @@ class Gemma2ForCausalLM(nn.Module):
         _set_gradient_checkpointing, which flips `gradient_checkpointing` on the modules that have it; the reference
         decoder then re-runs each layer in backward, modeling_gemma2.py:752-762).  Accepted as a recorded no-op: the
         whole B=32 working set (~120 GB) stays resident in the 288 GB of HBM, so recompute would only
-        add a forward pass.  Numerically the two are the same computation."""
+        add a forward pass.  Numerically the two are the same computation.  Enabling it warns once: a caller who
+        relies on it to fit a larger batch or a smaller device gets no memory saving."""
+        if enable and not getattr(Gemma2ForCausalLM, "_svla_ckpt_warned", False):
+            Gemma2ForCausalLM._svla_ckpt_warned = True
+            warnings.warn("spatialvla_amd: gradient checkpointing is accepted but never recomputes; activations stay "
+                          "resident in HBM (about 120 GB at B=32, L=312 for SpatialVLA-4B), so it saves no memory",
+                          stacklevel=2)
         for m in self.modules():
             if hasattr(m, "gradient_checkpointing"):
                 m.gradient_checkpointing = bool(enable)

@@ -155,9 +155,12 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         self.pad_token_id = config.pad_token_id if config.pad_token_id is not None else -1
         # predict_action replays each decode step from a captured HIP graph (SVLA_DECODE_GRAPHS=0: eager launches)
         self.decode_graphs = os.environ.get("SVLA_DECODE_GRAPHS", "1") != "0"
-        # reference raises on an image-token count mismatch (:379-385); here the count is copied to pinned host
-        # memory behind an event and checked at the next forward (check_deferred), so no step waits on the GPU
+        # reference raises on an image-token count mismatch inside the same forward (:379-385), and so does this
+        # forward by default (one host read of the count).  defer_checks = True (opt-in: TrainEngine(...,
+        # defer_host_checks=True), bench.py) copies the count to pinned host memory behind an event instead and
+        # raises at the next forward / check_deferred(), so a training step never waits on the GPU.
         self.strict_checks = True
+        self.defer_checks = False
         self._deferred = []
         self.last_stash = {}
         self.post_init()
@@ -168,9 +171,10 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         return torch.zeros(1, dtype=torch.int64, pin_memory=dev.type == "cuda")  # torch's caching host allocator
 
     def _defer(self, value, check):
-        """Copy the device scalar `value` to pinned host memory behind an event; check(v) runs at the next
-        check_deferred().  CPU tensors are checked at once."""
-        if value.device.type != "cuda":
+        """check(v) on the device scalar `value`: at once (the reference's synchronous raise, default), or, with
+        defer_checks, after copying it to pinned host memory behind an event at the next check_deferred().
+        CPU tensors are always checked at once."""
+        if value.device.type != "cuda" or not self.defer_checks:
             check(int(value))
             return
         buf = self._pinned_i64(value.device)
@@ -307,7 +311,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
                             "Number of images does not match number of special image tokens in the input text. "
                             f"Got {n_tok} image tokens in the text but {n_img} tokens from image embeddings.")
                 self._defer(img_mask.sum(), check)
-            # image rows beyond the features (a mismatch, reported by the deferred check) read the text embedding
+            # image rows beyond the features (a mismatch, reported by a deferred check) read the text embedding
             # instead of past the end of the feature rows
             idx = torch.cumsum(img_mask.to(torch.int32), 0) - 1
             img_index = torch.where(img_mask & (idx < n_img), idx, -1).to(torch.int32)
@@ -794,17 +798,22 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
 
     @torch.no_grad()
     def generate(self, input_ids=None, pixel_values=None, intrinsic=None, attention_mask=None,
-                 max_new_tokens: int = 256, do_sample: bool = False, eos_token_id=None, pad_token_id=None,
-                 generation_config=None, **kwargs):
+                 max_new_tokens: Optional[int] = None, do_sample: Optional[bool] = None, eos_token_id=None,
+                 pad_token_id=None, generation_config=None, **kwargs):
         """Greedy `generate` as the reference's predict_action calls it (:491, HF generate with do_sample=False over a
         HybridCache): the loop runs prepare_inputs_for_generation -> forward(past_key_values=Gemma2KVCache) per step
         and returns prompt + new tokens; finished sequences get pad_token_id, the loop stops once every sequence
         emitted eos.  Every step is eager here; predict_action is the graph-replayed fast path with the same tokens."""
+        # HF precedence: explicit arguments override the generation_config, which overrides the defaults
         if generation_config is not None:
-            max_new_tokens = getattr(generation_config, "max_new_tokens", None) or max_new_tokens
-            do_sample = bool(getattr(generation_config, "do_sample", do_sample))
+            if max_new_tokens is None:
+                max_new_tokens = getattr(generation_config, "max_new_tokens", None)
+            if do_sample is None:
+                do_sample = getattr(generation_config, "do_sample", None)
             eos_token_id = getattr(generation_config, "eos_token_id", None) if eos_token_id is None else eos_token_id
             pad_token_id = getattr(generation_config, "pad_token_id", None) if pad_token_id is None else pad_token_id
+        max_new_tokens = 256 if max_new_tokens is None else int(max_new_tokens)
+        do_sample = bool(do_sample)
         if do_sample or int(kwargs.pop("num_beams", 1)) != 1:
             raise NotImplementedError("generate: greedy decoding only (the reference calls do_sample=False)")
         kwargs.pop("token_type_ids", None)

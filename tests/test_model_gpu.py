@@ -126,16 +126,24 @@ def test_zoe_fused_metric_tail(cuda):
 
 def test_zoe_attractor_fused(cuda):
     """ZoeDepthAttractorLayerUnnormed on the fused kernel (resizes on the NHWC kernel, svla_zoe_attractor for the
-    attractor loop) vs the stock module, nyu-kitti shapes (16 / 8 / 4 / 1 attractors, 64 bins, 128-channel embedding),
-    channels-last inputs as the estimator produces them.  The stock loop is TorchScript's fused inv_attractor between
-    eager bf16 ops; the kernel keeps every rounding point, so the outputs agree to the last bf16 bit on nearly every
-    element (asserted: rel-L2 <= 1e-3, measured value printed)."""
+    attractor loop), nyu-kitti shapes (16 / 8 / 4 / 1 attractors, 64 bins, 128-channel embedding), channels-last
+    inputs as the estimator produces them.
+
+    The kernel's intended semantics are those of the reference's pinned transformers 4.47, where inv_attractor is
+    a TorchScript function that the fuser runs as one kernel: fp32 from the bf16 dx, ONE rounding to bf16 per
+    attractor term, then the bf16 running sum.  That is pinned here against an fp32 single-rounding restatement of
+    the loop computed in the test from the module's own attractor maps and bin centres (bound: rel-L2 1e-3 and at most
+    0.5 % of the elements differing, from fp32 operation-order differences that move a bf16 rounding; measured
+    numbers printed).  The installed transformers' stock module is compared too, but only loosely (rel-L2 1e-2):
+    its TorchScript function may run unfused (profiling runs), rounding pow, mul, add and div to bf16 one by one,
+    so parity with the pinned 4.47 fused path is NOT pinned by the stock module."""
     from transformers import ZoeDepthForDepthEstimation, CONFIG_MAPPING
     from spatialvla_amd import zoe_fast, presets
     cfg = CONFIG_MAPPING["zoedepth"](**{k: v for k, v in presets._zoe_large().items() if k != "model_type"})
     torch.manual_seed(5)
     zoe = ZoeDepthForDepthEstimation(cfg).to(cuda).to(torch.bfloat16).eval()
     cl = torch.channels_last
+    interp = torch.nn.functional.interpolate
     for li, att in enumerate(zoe.metric_head.attractors):
         h = 12 * 2 ** li
         x = torch.randn(2, 128, 2 * h, 2 * h, device=cuda).to(torch.bfloat16).contiguous(memory_format=cl)
@@ -144,9 +152,26 @@ def test_zoe_attractor_fused(cuda):
         with torch.no_grad():
             ref, _ = type(att).forward(att, x, prev, emb, interpolate=True)
             got, _ = zoe_fast._attractor_unnormed_forward(att, x, prev, emb, interpolate=True)
+            # fp32 single-rounding restatement (inv_attractor defaults alpha 300, gamma 2; kind "mean")
+            a_ = att.act2(att.conv2(att.act1(att.conv1(x + interp(emb, x.shape[-2:], mode="bilinear",
+                                                                      align_corners=True)))))
+            c = interp(prev, a_.shape[-2:], mode="bilinear", align_corners=True).float()
+            d = torch.zeros_like(c)
+            for i in range(a_.shape[1]):
+                dx = (a_[:, i:i + 1].float() - c).to(torch.bfloat16).float()
+                t = (dx / (300.0 * (dx * dx) + 1.0)).to(torch.bfloat16).float()
+                d = (d + t).to(torch.bfloat16).float()
+            if att.kind == "mean":
+                d = (d * (1.0 / a_.shape[1])).to(torch.bfloat16).float()
+            ref32 = (c + d).to(torch.bfloat16)
+        diff32 = (got.float() != ref32.float()).float().mean().item()
         diff = (got.float() != ref.float()).float().mean().item()
-        print(f"attractor {li} ({att.n_attractors} attractors): rel-L2 {H.rel_l2(got, ref):.2e}, elements differing {diff:.2e}")
-        assert got.shape == ref.shape and H.rel_l2(got, ref) <= 1e-3
+        print(f"attractor {li} ({att.n_attractors} attractors): vs fp32 single rounding rel-L2 "
+              f"{H.rel_l2(got, ref32):.2e}, differing {diff32:.2e}; vs installed stock module rel-L2 "
+              f"{H.rel_l2(got, ref):.2e}, differing {diff:.2e}")
+        assert got.shape == ref.shape == ref32.shape
+        assert H.rel_l2(got, ref32) <= 1e-3 and diff32 <= 5e-3
+        assert H.rel_l2(got, ref) <= 1e-2
 
 
 def H_rel(a, b):
@@ -362,29 +387,49 @@ def test_decode_states_bounded_and_invalidated(cuda):
     assert torch.equal(again, ref)
 
 
-def test_image_token_mismatch_raises_deferred(cuda):
-    """The reference raises when the image-token count differs from the image feature rows (:379-385).  The HIP
-    forward copies the count to pinned memory behind an event and raises at check_deferred() (run at the start of
-    the next forward), so a training step never waits on it; meanwhile the surplus image positions read the text
-    embedding instead of running past the feature rows."""
+@pytest.mark.parametrize("deferred", [False, True], ids=["sync", "deferred"])
+def test_image_token_mismatch_raises(cuda, deferred):
+    """The reference raises when the image-token count differs from the image feature rows, inside the same forward
+    (:379-385); so does the HIP forward by default.  With the opt-in deferral (model.defer_checks, set by
+    TrainEngine(defer_host_checks=True)) the count is copied to pinned memory behind an event and raised at
+    check_deferred() (run at the start of the next forward), so a training step never waits on it; meanwhile the
+    surplus image positions read the text embedding instead of running past the feature rows."""
     g = _load("tiny_train.safetensors")
     cfgd = H.cfg_dict("tiny")
     model = H.build_hip_model(cfgd, "cuda:0")
+    assert model.defer_checks is False
+    model.defer_checks = deferred
     batch = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}
     model.predict_depth = lambda pv: g["out.depth"].to(cuda)
     ids = batch["input_ids"].clone()
     img_pos = (ids[0] == model.config.image_token_index).nonzero().view(-1)
     ids[0, img_pos[0]] = model.config.image_token_index + 1  # one image token fewer than feature rows
     batch["input_ids"] = ids
-    with torch.no_grad():
-        out = model(**batch)
-    assert torch.isfinite(out.logits.float()).all()
-    with pytest.raises(ValueError, match="Number of images does not match"):
-        model.check_deferred()
+    if not deferred:
+        with torch.no_grad(), pytest.raises(ValueError, match="Number of images does not match"):
+            model(**batch)
+        assert not model._deferred
+    else:
+        with torch.no_grad():
+            out = model(**batch)
+        assert torch.isfinite(out.logits.float()).all()
+        with pytest.raises(ValueError, match="Number of images does not match"):
+            model.check_deferred()
     with torch.no_grad():  # a well-formed batch afterwards runs clean
         batch["input_ids"] = {k[3:]: v.to(cuda) for k, v in g.items() if k.startswith("in.")}["input_ids"]
         model(**batch)
         model.check_deferred()
+
+
+def test_train_engine_defer_opt_in(cuda):
+    """TrainEngine leaves the synchronous check alone unless defer_host_checks=True is passed."""
+    from spatialvla_amd.engine import TrainEngine
+    cfgd = H.cfg_dict("tiny")
+    model = H.build_hip_model(cfgd, "cuda:0")
+    TrainEngine(model, total_steps=10)
+    assert model.defer_checks is False
+    TrainEngine(model, total_steps=10, defer_host_checks=True)
+    assert model.defer_checks is True
 
 
 def test_zoe_readout_projection_fused(cuda):

@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-5 probe call: gemm4 k-loop stamps with ablations, MFMA-busy PMC of the isolated Gemma2 block (every kernel in
+# situ), attention PMC, the bench line and the block trace.  Each GPU step has its own time limit; a crash or timeout
+# stops the script.
+set -o pipefail
+export TMPDIR=/tmp
+R=$(pwd)
+TAG=${TAG:-r5a}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+step() {
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 $secs "$@"
+  local rc=$?
+  echo "[$name] rc=$rc"
+  if [ $rc -gt 1 ]; then echo "[$name] stopping: crash or timeout"; exit $rc; fi
+  return 0
+}
+if [ -n "$LIST" ]; then timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1; fi
+if [ -n "$STAMPS" ]; then
+  step stamps 300 python -u tools/stamps_multi.py $STAMPS -- $STAMP_SHAPES > $O/stamps.txt 2>&1
+  cat $O/stamps.txt
+fi
+if [ -n "$AB_LIB" ]; then
+  step gemm_ab 300 python -u tools/gemm_ab.py spatialvla_amd/libsvla.so $AB_LIB $AB_SHAPES > $O/gemm_ab.txt 2>&1
+  cat $O/gemm_ab.txt
+fi
+if [ -n "$BLOCK_PMC" ]; then
+  step blk_pmc1 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d /tmp/bp1 -o p1 --output-format csv -- python3 tools/block_ab.py 1 1 3 > $O/blk_pmc1.log 2>&1
+  step blk_pmc2 180 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d /tmp/bp2 -o p2 --output-format csv -- python3 tools/block_ab.py 1 1 3 > $O/blk_pmc2.log 2>&1
+  step blk_trace 180 rocprofv3 --kernel-trace --stats -d /tmp/bt -o bt --output-format csv -- python3 tools/block_ab.py 1 1 5 > $O/blk_trace.log 2>&1
+  python tools/block_trace.py /tmp/bt > $O/block_breakdown.txt 2>&1
+  cp /tmp/bt/*/*kernel_stats.csv $O/blk_kernel_stats.csv 2>/dev/null
+  python tools/pmc_dispatch.py /tmp/bp1 /tmp/bp2 > $O/block_pmc.txt 2>&1
+  mkdir -p $O/bp1 $O/bp2 && cp $(find /tmp/bp1 -name "*counter_collection.csv") $O/bp1/ && cp $(find /tmp/bp2 -name "*counter_collection.csv") $O/bp2/
+  cat $O/block_breakdown.txt
+fi
+if [ -n "$GEMM_PMC" ]; then
+  for shp in $GEMM_PMC; do
+    step gemm_pmc 400 tools/gemm_pmc2.sh $TAG ${shp//,/ } > $O/gemm_pmc_$shp.log 2>&1
+  done
+  for f in $O/*_svla.txt $O/*_torch.txt; do echo "== $f"; cat $f; done
+fi
+if [ -n "$BENCH" ]; then
+  step bench 600 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err
+  head -c 2500 $O/bench.json; echo
+fi
+ls $O
