@@ -115,8 +115,11 @@ def dominant_kernel_roofline(records, fp8=False):
     ach = flops / (avg * 1e-3) / 1e12
     ob = 1 if fp8 else 2                             # operand bytes per element
     bytes_alg = ob * (M * K + N * K) + 2.0 * 3 * M * (N // 2)   # x, Wg, Wu read; h, g, u written (bf16)
+    if fp8:
+        bytes_alg += (M * K + N * K) / 32                # one E8M0 block scale per 32 operand elements
     peak = PEAK_FP8_TFLOPS if fp8 else PEAK_BF16_TFLOPS
-    kern = ("svla gemm4f8_kernel (256x256 tile, 4 waves x 128x128, v_mfma_scale_f32_32x32x64_f8f6f4 e4m3, row scales)"
+    kern = ("svla gemm4mx_kernel (256x256 tile, 4 waves x 128x128, v_mfma_scale_f32_32x32x64_f8f6f4 e4m3, OCP MX "
+            "E8M0 block scales per 32 k)"
             if fp8 else "svla gemm4_kernel_00g (256x256 tile, 4 waves x 128x128, AGPR C^T accumulators, gate/up B "
                         "fragments paired per output block, GeGLU stored straight from the accumulators)")
     return {"kernel": kern + " EPI_GEGLU (Gemma2 gate/up, M=%d N=%d K=%d)" % (M, N, K),
@@ -128,7 +131,7 @@ def dominant_kernel_roofline(records, fp8=False):
 
 def fp8_leg(model, engine, batches, args):
     """BASELINE configs[4] beside the bf16 line (N=1, after the timed region, same model and batches): the training
-    step with the Gemma2 q|k|v, o, gate|up and down projections on the fp8 (e4m3, row-scaled) MFMA GEMM, forward and
+    step with the Gemma2 q|k|v, o, gate|up and down projections on the fp8 (e4m3, OCP MX block-scaled) MFMA GEMM, forward and
     dgrad, weight copies re-quantised after every optimizer step; timed like the main line (barrier-free: one rank).
     roofline: the fp8 gate/up GeGLU launches inside the timed steps vs the dense fp8 peak (5 PFLOP/s)."""
     from spatialvla_amd import kernels as K

@@ -118,10 +118,28 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
                       const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * fp8 projections (BASELINE configs[4]; OCP e4m3, MX-scaled MFMA v_mfma_scale_f32_32x32x64_f8f6f4 at unit block
- * scales, fp32 accumulate).  Replaces the bf16 forward nn.Linear of Gemma2 q/k/v/o and gate/up/down
- * (model/modeling_gemma2.py:86-92, 351-354, 376-408) when fp8 projections are enabled; the backward stays bf16.
+ * fp8 projections (BASELINE configs[4]; OCP e4m3 on v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulate).
+ * Replaces the bf16 nn.Linear of Gemma2 q/k/v/o and gate/up/down (model/modeling_gemma2.py:86-92, 351-354,
+ * 376-408) in the forward and the input-gradient (dgrad) GEMMs when fp8 projections are enabled.  Two scalings:
+ * OCP MX block scales (svla_quant_mx_rows + svla_gemm_mxfp8: one E8M0 scale per 32 consecutive k of a row, fed to
+ * the MFMA; the product path) and per-row fp32 scales (svla_quant_fp8_rows + svla_gemm_fp8: unit MFMA block
+ * scales, row scales applied in the epilogue).
  * ---------------------------------------------------------------------------------------- */
+/* OCP MX (Microscaling spec v1.0) e4m3 quantisation of rows: for each block of 32 consecutive k of row r,
+ * X = clamp(floor(log2(amax)) - 8, -127, 127), q[r,k] = e4m3(clamp(x[r,k] * 2^-X, +-448)) (RNE), scale byte
+ * E8M0 = 127 + X.  Scales are tile-major: the 4 bytes of row r in 128-k tile t at scales[t * sld + 4 r]
+ * (sld >= 4 rows, a multiple of 4), so a k-tile's scales of 256 consecutive rows are contiguous.  x bf16
+ * [rows][ldx], q bytes [rows][ldq]; K % 128 == 0. */
+int svla_quant_mx_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq, void* scales,
+                       int64_t sld, void* stream);
+/* C[M,N] = epilogue( sum_k 2^(Xa(m,k/32) + Xb(n,k/32)) A(m,k) B(n,k) ): A, B e4m3 KC operands as svla_gemm_fp8
+ * with their MX block scales in svla_quant_mx_rows' layout (a_mx: M rows, b_mx: N rows -- GEGLU: the gate rows then
+ * the up rows of one [N] scale matrix; *_ld the per-k-tile stride, *_bytes the buffer size); K and k_valid
+ * multiples of 128.  Epilogues and workspace as svla_gemm_fp8. */
+int svla_gemm_mxfp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const void* a_mx, int64_t a_mx_ld,
+                    int64_t a_mx_bytes, const svla_operand* B, const void* b_mx, int64_t b_mx_ld, int64_t b_mx_bytes,
+                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                    const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream);
 /* Row-wise quantisation: x'[r,k] = x[r,k] * colscale[k] (colscale fp32 [K], 16-B aligned, or NULL = 1);
  * scale[r] = amax_r(x')/448, q[r,k] = e4m3(clamp(x'[r,k]*448/amax_r, +-448)) (RNE; a zero row gives q = 0,
  * scale 0).  x bf16 [rows][ldx], q bytes [rows][ldq]; K % 8 == 0 (the dgrad GEMMs quantise dY with

@@ -76,6 +76,11 @@ SIGNATURES = {
                                   ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t, c_i32, c_vp]),
     "svla_quant_fp8_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "svla_transpose_u8": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "svla_quant_mx_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "svla_gemm_mxfp8": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), c_vp, c_i64, c_i64,
+                                ctypes.POINTER(Operand), c_vp, c_i64, c_i64, ctypes.POINTER(c_vp),
+                                ctypes.POINTER(c_i64), c_i32, c_i64, ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t,
+                                c_vp]),
     "svla_gemm_fp8": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), c_vp, ctypes.POINTER(Operand), c_vp,
                               ctypes.POINTER(c_vp), ctypes.POINTER(c_i64), c_i32, c_i64, ctypes.POINTER(Epilogue), c_vp,
                               ctypes.c_size_t, c_vp]),
@@ -146,13 +151,16 @@ class SvlaError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """dlopen libsvla.so and bind every symbol; raises if anything is missing."""
+def load(path: str = LIB_PATH, strict: bool = True) -> ctypes.CDLL:
+    """dlopen libsvla.so and bind every symbol; raises if anything is missing (strict=False: diagnostic builds of
+    an older tree, for A/B tools, skip the symbols they lack)."""
     if not os.path.exists(path):
         raise SvlaError(f"libsvla.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; "
                         f"g.build()'` (make -C spatialvla_amd/csrc). There is no fallback path.")
     cdll = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(cdll, name):
+            continue
         fn = getattr(cdll, name)  # AttributeError if an export is missing
         fn.restype = res
         fn.argtypes = args

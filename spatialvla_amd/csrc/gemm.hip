@@ -1294,8 +1294,9 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 
 template <int LAYOUT>
 struct Op4 {
-  uint32_t v0, v1;  // per-lane byte offsets of piece 0 (RC: pieces with n & 2 use v1); piece n adds n * rs via soffset
-  int kq;           // KC: k offset (elements) of this lane's chunk; RC: k-row of this lane in piece 0
+  uint32_t v0, v1;  // per-lane byte offsets of piece 0 (RC: pieces with n & 2 use v1, KC fp8: odd pieces use v1);
+                    // piece n adds n * rs via soffset
+  int kq, kq1;      // KC: k offset (elements) of this lane's chunk (kq1: odd pieces); RC: k-row of this lane in piece 0
   int nvalid;       // KC: pieces whose row of this lane is inside the valid extent
   bool ok0, ok1;    // RC: this lane's outer chunk (v0 / v1 variant) starts inside the valid extent
   uint32_t rs;      // wave-uniform byte step per piece: KC 8 rows, RC 4 k-rows
@@ -1307,23 +1308,31 @@ struct Op4 {
 //      64w + 8n .. +7.  GEGLU: rows 0..127 are gate rows r0/2.., 128..255 the up rows of the second tensor.
 //  RC: two half images [64 k][128 outer] (256-B rows, chunk p of k-row k = global chunk p ^ rc_swz(k)); piece n
 //      of wave w = k-rows 4j .. 4j+3 of its half, j = 8 (w & 1) + n.  rc_swz depends on n only through n & 2.
-template <int LAYOUT>
+//  KC, fp8 (FSW): chunk p of row r holds global chunk p ^ ((r >> 1) & 7).  The 32x32x64 fp8 fragment puts rows
+//      r = 0..31 on lanes 0..31 (and again on 32..63); a ds_read_b128 lane group ({0-3, 12-15, 20-27}, ...) then
+//      holds rows r and r + 8, which the r & 7 swizzle puts on one 16-B slot of the bank row (2-way: 45 % of the
+//      fp8 kernel's LDS cycles were conflict cycles, r5d PMC); (r >> 1) & 7 spreads the group over all 16 slots.
+//      (r >> 1) & 7 of piece n's rows is (4 n + (lane >> 4)) & 7: two voffset variants, even and odd pieces.
+template <int LAYOUT, bool FSW = false>
 __device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane,
                                           Op4<LAYOUT>& st) {
   const int64_t ldb = op.ld * 2;
   if (LAYOUT == SVLA_LAYOUT_KC) {
-    const int gc = (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
+    const int gc = FSW ? (lane & 7) ^ (lane >> 4) : (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
+    const int gc1 = FSW ? (lane & 7) ^ (4 + (lane >> 4)) : gc;
     st.kq = gc * 8;
+    st.kq1 = gc1 * 8;
     const int row = 64 * w + (lane >> 3);
     const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + (row & 127) : r0 + row;
     const int64_t nv = (rv - grow + 7) / 8;
     st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, 8);
-    st.v0 = st.v1 = (uint32_t)((row & 127) * ldb + gc * 16);
+    st.v0 = (uint32_t)((row & 127) * ldb + gc * 16);
+    st.v1 = (uint32_t)((row & 127) * ldb + gc1 * 16);
     st.ok0 = st.ok1 = true;
     st.rs = __builtin_amdgcn_readfirstlane((uint32_t)(8 * ldb));
   } else {
     const int kr = 32 * (w & 1) + (lane >> 4);  // k-row of piece 0 (piece n: + 4n)
-    st.kq = kr;
+    st.kq = st.kq1 = kr;
     st.nvalid = 8;
     const int64_t o = r0 + 128 * (w >> 1);
     const int gc0 = (lane & 15) ^ rc_swz(kr), gc1 = (lane & 15) ^ rc_swz(kr + 8);
@@ -1339,7 +1348,7 @@ __device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, in
 // not templates: the lambdas of gemm4_body are also analysed for the host, where a device-only function template
 // called from them fails to substitute.
 __device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_KC>& st, int n, int64_t krem) {
-  return (st.kq < krem && n < st.nvalid) ? st.v0 : OOB;
+  return (n & 1) ? ((st.kq1 < krem && n < st.nvalid) ? st.v1 : OOB) : ((st.kq < krem && n < st.nvalid) ? st.v0 : OOB);
 }
 __device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_RC>& st, int n, int64_t krem) {
   return (st.kq + 4 * n < krem && ((n & 2) ? st.ok1 : st.ok0)) ? ((n & 2) ? st.v1 : st.v0) : OOB;
@@ -1482,25 +1491,37 @@ __device__ __forceinline__ void agpr_set(const f32x4& v) {
 //  * v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate), unit block scales; a wave's 128x128 = 4x4 blocks of
 //    32x32 in the same 256 AGPRs; a k-tile (128 fp8 k) = 2 k-halves x 16 MFMAs, each 4x a 16x16x32 bf16 MFMA, so the
 //    k-tile takes the time of the bf16 k-tile (64 k) and every gap holds 4x the issue slots.
-//  * fragment (32 rows at rb, k-half h): lane l holds row rb + (l & 31), bytes 64h + 32(l >> 5) .. +31 of the row
-//    (two 16-B chunks).  A and B use the same lane -> k map, so the product sums matching k whatever the
-//    instruction's internal k order.
+//  * fragment (32 rows at rb, k-half h): lane l holds row rb + (l & 31), 16-B chunks 4h + (l >> 5) and
+//    4h + 2 + (l >> 5) of the row: the instruction's two 32-k blocks are bytes 0-15 and 16-31 of every lane, so an
+//    MX block of 32 consecutive k of the row is one block of the instruction (FragF8, tools/mx_probe.py).
 //  * epilogue: C = acc * sa[m] * sb[n] (per-row scales of A and of B = the output column), then the usual epilogue.
 struct F8Scales {
   const float* sa;   // [M] row scales of A (activation rows)
   const float* sb;   // [N] (GEGLU: [2 I], gate rows then up rows) row scales of B (weight rows)
   int64_t na, nb;    // readable entries of sa / sb
   int64_t geglu_I;   // GEGLU: rows per weight half (tile column c < 128 -> gate row, else up row I + ..), else 0
+  // MX mode (gemm4mx_kernel): OCP MX E8M0 block scales, one per 32 k of a row, tile-major: the 4 scale bytes of row r
+  // in 128-k tile t at [t * m?_ld + 4 r] (svla_quant_mx_rows' layout); GEGLU B: the gate rows then the up rows of one
+  // [2 I] scale matrix.  m?_bytes bounds the buffer (rows past it read scale byte 0 over zero-filled data).
+  const uint8_t* ma;
+  const uint8_t* mb;
+  int64_t ma_ld, mb_ld, ma_bytes, mb_bytes;
 };
 
 struct FragF8 {
   i32x8 v;
   __device__ __forceinline__ void load(const char* img, int rb, int h, int lane) {
+    // The MFMA reads bytes 0-15 of every lane as k of its first 32-k block (lane half g: k = 16 g + e) and bytes
+    // 16-31 as its second block (k = 32 + 16 g + e), each block scaled by the E8M0 byte of lane half 0 / 1
+    // respectively (measured, tools/mx_probe.py).  So lane half g takes chunk g of each 32-byte MX block of the
+    // k-half: the first block (tile chunks 4h, 4h + 1) and the second (4h + 2, 4h + 3), and an MX block of the data
+    // is a hardware block of the instruction.
     const int row = rb + (lane & 31);
-    const int c0 = 4 * h + 2 * (lane >> 5);
+    const int g = lane >> 5;
     const char* base = img + row * 128;
-    const u32x4 lo = *reinterpret_cast<const u32x4*>(base + ((c0 ^ (row & 7)) << 4));
-    const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ (row & 7)) << 4));
+    const int sw = (row >> 1) & 7;  // the fp8 image swizzle (op4_setup, FSW)
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(base + (((4 * h + g) ^ sw) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((4 * h + 2 + g) ^ sw) << 4));
     v = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   }
 };
@@ -1514,22 +1535,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, 
   return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, n, 0x00020000);
 }
 
-// fp8 k-tile schedule (32 MFMA slots): F1 reads at 0..7, RB1, A pieces (2 per slot) from F8_DA0, B pieces from
-// F8_DB0, RB2, then the 8 F0 reads of the next k-tile
-#ifndef F8_RB1
+// fp8 k-tile schedule (32 MFMA slots of 64 cycles): F1 reads at 0..7, RB1 after slot 9, then ONE LDS-DMA piece a
+// slot -- A pieces 0..7 at slots 10..17, B pieces at slots 18..22 and 24..26 (a piece costs ~60 issue cycles: two a
+// slot, as in rounds 2-4, held each slot past its 64-cycle MFMA) -- the MX scale pieces at slot 27, RB2 after slot
+// 23 (vmcnt(13): the 13 pieces of k-tile kt+2 issued so far may stay in flight), then the 8 F0 reads of the next
+// k-tile.
 #define F8_RB1 9
-#endif
-#ifndef F8_DA0
-#define F8_DA0 10
-#endif
-#ifndef F8_DB0
-#define F8_DB0 15
-#endif
-#ifndef F8_RB2
 #define F8_RB2 23
-#endif
-static_assert(F8_RB1 >= 8 && F8_DA0 > F8_RB1 && F8_DB0 >= F8_DA0 + 4 && F8_RB2 >= F8_DB0 + 4 && F8_RB2 + 8 < 32,
-              "fp8 schedule knobs out of order");
+#define F8_P0 10    // first piece slot
+#define F8_NPRE 13  // pieces issued before RB2 (slots F8_P0 .. F8_RB2 - 1)
+__host__ __device__ constexpr int f8_piece(int x) {  // piece index issued in slot x, or -1
+  return (x >= F8_P0 && x < F8_RB2) ? x - F8_P0 : (x > F8_RB2 && x <= F8_RB2 + 16 - F8_NPRE) ? x - F8_RB2 - 1 + F8_NPRE : -1;
+}
+static_assert(F8_RB2 - F8_P0 == F8_NPRE && f8_piece(F8_RB2 + 3) == 15 && F8_RB2 + 4 < 31, "fp8 schedule");
 
 #define P4_FOR_ACC(BODY)                           \
   _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) \
@@ -1538,7 +1556,7 @@ static_assert(F8_RB1 >= 8 && F8_DA0 > F8_RB1 && F8_DB0 >= F8_DA0 + 4 && F8_RB2 >
 // The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
 // template are also instantiated for the host, where the device-only helpers they call fail to substitute and
 // the kernel stub silently disappears.
-template <int LA, int LB, bool F8 = false, bool GG = false>
+template <int LA, int LB, bool F8 = false, bool GG = false, bool MX = false>
 __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
                                            const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
                                            const SKArgs& sk, const F8Scales& fs) {
@@ -1587,6 +1605,19 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
   auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w); };
   auto pieceB_full = [&](const char* kb_, int n, char* img) { op4_piece(kb_, vfb[n], n * sb.rs, n, img, w); };
+  // MX: each wave stages the E8M0 scales of its 64 image rows of A and of B for a k-tile (two 4-B-per-lane LDS-DMA
+  // instructions of 256 B) into the k-tile's 2 KiB scale region behind the two operand stages (row i of an image at
+  // byte 4 i: A at 0, B at 1024).  k units here are pairs of fp8 values, so a k-tile of 64 units is one 128-k MX tile.
+  uint32_t vma = 0, vmb = 0;  // per-lane byte offsets of this wave's scale rows (the tile's rows 64 w + lane)
+  auto mx_pieces = [&](int kt, int stage_idx) {
+    if constexpr (MX) {
+      char* const reg = smem + 2 * STAGE + stage_idx * 2048 + 256 * w;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc_n(fs.ma, fs.ma_bytes), (LDS_AS void*)reg, 4, vma,
+                                               (uint32_t)(kt * fs.ma_ld), 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc_n(fs.mb, fs.mb_bytes), (LDS_AS void*)(reg + 1024), 4, vmb,
+                                               (uint32_t)(kt * fs.mb_ld), 0, 0);
+    }
+  };
   auto issue_all = [&](int kt, char* stage) {
     const int64_t k0 = (int64_t)kt * BK;
     const char* const ka = abase + k0 * ksa;
@@ -1595,12 +1626,18 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     for (int n = 0; n < 8; ++n) pieceA(ka, kvA - k0, n, stage);
 #pragma unroll
     for (int n = 0; n < 8; ++n) pieceB(kbb, kvB - k0, n, stage + OPB);
+    if constexpr (MX) mx_pieces(kt, stage == smem ? 0 : 1);
   };
   auto stage_first = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
-    op4_setup<LA>(A, m0, rvA, w, lane, sa);
-    op4_setup<LB>(B, n0, rvB, w, lane, sb);
+    op4_setup<LA, F8>(A, m0, rvA, w, lane, sa);
+    op4_setup<LB, F8>(B, n0, rvB, w, lane, sb);
     abase = op4_base<LA>(A, m0, w >> 1);
     bbase = op4_base<LB>(B, n0, w >> 1);
+    if constexpr (MX) {
+      const int i = 64 * w + lane;  // image row staged by this lane
+      vma = (uint32_t)((m0 + i) * 4);
+      vmb = (uint32_t)(4 * (fs.geglu_I ? (i < 128 ? (n0 >> 1) + i : fs.geglu_I + (n0 >> 1) + (i - 128)) : n0 + i));
+    }
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       vfa[n] = op4_voff(sa, n, (int64_t)1 << 40);
@@ -1622,8 +1659,12 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       stage_first(m0, n0, kb, ke, lane);
-      if (nq > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (nq > 1) {
+        if constexpr (MX) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");  // 16 operand + 2 scale pieces a k-tile
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     P8_BARRIER();
     using T = std::true_type;
@@ -1655,6 +1696,35 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     for (int i = 0; i < 4; ++i) f0a[i].load(smem, 128 * wr + 32 * i, 0, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) f0b[j].load(smem + OPB, 128 * wc + 32 * j, 0, lane);
+    // MX: the MFMA of k-half h scales its two k-blocks (MX blocks 2 h and 2 h + 1 of the k-tile, FragF8) by the
+    // bytes that lane halves 0 and 1 pass: lane l passes byte 2 h + (l >> 5) of its row's scale dword.  tA / tB: the dwords of the lane's rows (read once per k-tile, after the barrier that makes the
+    // tile visible); sA0 / sB0 (k-half 0) and sA1 / sB1 (k-half 1): the scale byte shifted to byte 0, the operand the
+    // MFMA reads.  sA0 of the next tile is formed after the current tile's last k-half-0 MFMA, sA1 at the next tile's
+    // first MFMA (after the current tile's last k-half-1 MFMA).
+    uint32_t tA[4], tB[4];
+    int sA0[4], sB0[4], sA1[4], sB1[4];
+    const int sh0 = 8 * (lane >> 5), sh1 = 8 * (2 + (lane >> 5));
+    auto read_sc = [&](int stage_idx) {
+      if constexpr (MX) {
+        const LDS_AS uint32_t* r = (const LDS_AS uint32_t*)(smem + 2 * STAGE + stage_idx * 2048);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tA[i] = r[128 * wr + 32 * i + (lane & 31)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tB[j] = r[256 + 128 * wc + 32 * j + (lane & 31)];
+      }
+    };
+    auto form0 = [&]() {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { sA0[i] = (int)(tA[i] >> sh0); sB0[i] = (int)(tB[i] >> sh0); }
+    };
+    auto form1 = [&]() {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { sA1[i] = (int)(tA[i] >> sh1); sB1[i] = (int)(tB[i] >> sh1); }
+    };
+    if constexpr (MX) {
+      read_sc(0);
+      form0();
+    }
     auto ktile8 = [&](int kt, auto DMA, auto NEXT, auto FULLK) {
       char* const cur = smem + ((kt - kb) & 1) * STAGE;
       char* const nxt = smem + (((kt - kb) & 1) ^ 1) * STAGE;
@@ -1666,8 +1736,14 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       static_for<0, 32>([&](auto XC) {
         constexpr int x = decltype(XC)::value;
         constexpr int y = x & 15, ii = y >> 2, jj = y & 3;
-        if constexpr (x < 16) agpr_mfma_f8<ii * 4 + jj>(f0a[ii].v, f0b[jj].v, s127);
-        else agpr_mfma_f8<ii * 4 + jj>(f1a[ii].v, f1b[jj].v, s127);
+        if constexpr (MX) {
+          if constexpr (x < 16) agpr_mfma_mx<ii * 4 + jj>(f0a[ii].v, f0b[jj].v, sA0[ii], sB0[jj]);
+          else agpr_mfma_mx<ii * 4 + jj>(f1a[ii].v, f1b[jj].v, sA1[ii], sB1[jj]);
+          if constexpr (x == 0) form1();  // this tile's k-half-1 scales (tA still holds this tile's dwords)
+        } else {
+          if constexpr (x < 16) agpr_mfma_f8<ii * 4 + jj>(f0a[ii].v, f0b[jj].v, s127);
+          else agpr_mfma_f8<ii * 4 + jj>(f1a[ii].v, f1b[jj].v, s127);
+        }
         if constexpr (x < 4) f1a[x].load(cur, 128 * wr + 32 * x, 1, lane);
         else if constexpr (x < 8) f1b[x - 4].load(cur + OPB, 128 * wc + 32 * (x - 4), 1, lane);
         if constexpr (x == F8_RB1) {
@@ -1675,30 +1751,29 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           __builtin_amdgcn_s_barrier();
         }
         if constexpr (decltype(DMA)::value) {
-          if constexpr (x >= F8_DA0 && x < F8_DA0 + 4) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              if constexpr (decltype(FULLK)::value) pieceA_full(rsa, 2 * (x - F8_DA0) + u, cur);
-              else pieceA(rsa, kvA - k2, 2 * (x - F8_DA0) + u, cur);
-            }
+          constexpr int pc = f8_piece(x);
+          if constexpr (pc >= 0 && pc < 8) {
+            if constexpr (decltype(FULLK)::value) pieceA_full(rsa, pc, cur);
+            else pieceA(rsa, kvA - k2, pc, cur);
+          } else if constexpr (pc >= 8) {
+            if constexpr (decltype(FULLK)::value) pieceB_full(rsb, pc - 8, cur + OPB);
+            else pieceB(rsb, kvB - k2, pc - 8, cur + OPB);
           }
-          if constexpr (x >= F8_DB0 && x < F8_DB0 + 4) {
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              if constexpr (decltype(FULLK)::value) pieceB_full(rsb, 2 * (x - F8_DB0) + u, cur + OPB);
-              else pieceB(rsb, kvB - k2, 2 * (x - F8_DB0) + u, cur + OPB);
-            }
-          }
+          if constexpr (MX && x == F8_RB2 + 4) mx_pieces(kt + 2, (kt - kb) & 1);  // after the 16 operand pieces
         }
         if constexpr (decltype(NEXT)::value) {
           if constexpr (x == F8_RB2) {
-            if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            // k-tile kt+1 (pieces and, MX, its scale pieces, all issued in the previous k-tile) has landed once only
+            // the F8_NPRE pieces of k-tile kt+2 issued in this k-tile may be outstanding
+            if constexpr (decltype(DMA)::value) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
           }
           constexpr int r = x - F8_RB2 - 1;
           if constexpr (r >= 0 && r < 4) f0a[r].load(nxt, 128 * wr + 32 * r, 0, lane);
           else if constexpr (r >= 4 && r < 8) f0b[r - 4].load(nxt + OPB, 128 * wc + 32 * (r - 4), 0, lane);
+          if constexpr (MX && r == 0) read_sc(((kt - kb) & 1) ^ 1);  // the next tile's scale dwords
+          if constexpr (MX && x == 31) form0();                      // after this tile's last k-half-0 MFMA
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -2061,9 +2136,17 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     // column l&31), scaled by the row scales of A and B on the way into the image
     auto wp8 = [&](int pass, float* Ei) {
       if ((pass >> 1) == wr) {
-        const __amdgpu_buffer_rsrc_t ra = make_rsrc_n(fs.sa, fs.na * 4), rb = make_rsrc_n(fs.sb, fs.nb * 4);
         float csc[4];
         f32x4 rsc[2][4];
+        if constexpr (MX) {  // the block scales were applied by the MFMA
+#pragma unroll
+          for (int j = 0; j < 4; ++j) csc[j] = 1.f;
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rsc[ii][q] = f32x4{1.f, 1.f, 1.f, 1.f};
+        } else {
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc_n(fs.sa, fs.na * 4), rb = make_rsrc_n(fs.sb, fs.nb * 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int c = 128 * wc + 32 * j + (lane & 31);
@@ -2077,6 +2160,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
             const int64_t m = m0 + 64 * pass + 32 * ii + 8 * q + 4 * (lane >> 5);
             rsc[ii][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (uint32_t)(m * 4), 0, 0));
           }
+        }
         auto rows = [&](auto H) {
           static_for<0, 32>([&](auto IJ) {
             constexpr int ii = decltype(IJ)::value >> 4, j = (decltype(IJ)::value >> 2) & 3, q4 = decltype(IJ)::value & 3;
@@ -2288,6 +2372,11 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel_00g(int64_t M, int64_t N,
 __global__ __launch_bounds__(256, 1) void gemm4f8_kernel(int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B,
                                                          CDesc Cd, svla_epilogue E, SKArgs sk, F8Scales fs) {
   gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, true>(M, N, K, A, B, Cd, E, sk, fs);
+}
+// MX: per-32-k E8M0 block scales of both operands fed to the MFMA (staged by LDS-DMA beside the operand tiles)
+__global__ __launch_bounds__(256, 1) void gemm4mx_kernel(int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B,
+                                                         CDesc Cd, svla_epilogue E, SKArgs sk, F8Scales fs) {
+  gemm4_body<SVLA_LAYOUT_KC, SVLA_LAYOUT_KC, true, false, true>(M, N, K, A, B, Cd, E, sk, fs);
 }
 
 template <auto KERN>
@@ -2910,6 +2999,15 @@ using svla::num_cus;
 #define G4_SKMIN 4
 #endif
 
+#ifndef G4_NOSK
+#define G4_NOSK 0  // diagnostic builds: 1 = the 4-wave kernel never splits tiles (data-parallel rounds only)
+#endif
+#ifndef G4_SKMIN_NK
+#define G4_SKMIN_NK 64  // fewest k-tiles per tile for the 4-wave kernel's stream-K schedule (launch4)
+#endif
+#ifndef G8_SKMIN_NK
+#define G8_SKMIN_NK 0  // the same for the 8-phase kernel (launch8); 0 = no floor
+#endif
 // 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
 size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }
 
@@ -2929,8 +3027,8 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;  // last wave nearly full: nothing to balance
   const size_t need = sk_workspace_bytes(G);
-  if (ctx.variant != 2 && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
-      sk_tiles * sk.nk >= 8 * G) {
+  if (ctx.variant != 2 && sk.nk >= G8_SKMIN_NK && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 &&
+      sk_tiles < 2 * G && sk_tiles * sk.nk >= 8 * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
@@ -2966,7 +3064,13 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   if (sk_tiles * sk.nk < G4_SKMIN * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;
   const size_t need = sk_workspace_bytes(G);
-  if (ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G && sk_tiles * sk.nk >= G4_SKMIN * G) {
+  // stream-K only from 64 k-tiles a tile: below that the slab hand-off costs more than the data-parallel tail round
+  // it replaces (tools/gemm_ab.py, profiles/r5e_gemm_ab_nosk.txt, same box, interleaved: data-parallel rounds were
+  // 3-7 % faster for q|k|v fwd, o fwd / dgrad and down dgrad at 32-36 k-tiles and 34-37 % faster for sub-wave grids
+  // (252 tiles at K = 2048, SigLIP o fwd); stream-K stays 3-19 % ahead from 64 k-tiles up: q|k|v dgrad, down fwd,
+  // gate/up dgrad / wgrad, every weight gradient)
+  if (!G4_NOSK && sk.nk >= G4_SKMIN_NK && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
+      sk_tiles * sk.nk >= G4_SKMIN * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
@@ -2987,6 +3091,16 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
       lds_set = true;                                                                                \
     }                                                                                                \
     hipLaunchKernelGGL(gemm4_kernel_##LA_##LB_, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);   \
+  }
+  if (fs && fs->ma) {  // MX block scales: 2 KiB of scale rows per operand stage behind the operand images
+    static bool lds_set = false;
+    constexpr int lds = p4::LDS + 2 * 2048;
+    if (!lds_set) {
+      (void)hipFuncSetAttribute((const void*)gemm4mx_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      lds_set = true;
+    }
+    hipLaunchKernelGGL(gemm4mx_kernel, grid, block, lds, s, M, N, K, A, B, Cd, E, sk, *fs);
+    return svla::check_launch("gemm4 mxfp8");
   }
   if (fs) {
     static bool lds_set = false;
@@ -3018,6 +3132,7 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 
 int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K) {
   SVLA_CHECK_ARG(op != nullptr, "gemm: operand %s is NULL", name);
@@ -3059,6 +3174,11 @@ extern "C" size_t svla_gemm_workspace_bytes(void) { return sk_workspace_bytes(nu
 extern "C" int svla_diag_g4_stamps(void* host, size_t bytes) {  // diagnostic builds only (not in svla.h)
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g4_stamps), bytes < sizeof(g4_stamps) ? bytes : sizeof(g4_stamps)) ==
                  hipSuccess ? 0 : 2;
+}
+extern "C" int svla_diag_g4_stamps_clear(void) {  // zero the stamp table (blocks of an earlier, larger grid)
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g4_stamps)) != hipSuccess) return 2;
+  return hipMemset(p, 0, sizeof(g4_stamps)) == hipSuccess ? 0 : 2;
 }
 #endif
 
@@ -3398,14 +3518,13 @@ extern "C" int svla_softcap_ce_rows(int64_t M, int64_t N, void* logits, int64_t 
 // ------------------------------------------------------------------------------------------------------------
 // fp8 e4m3 GEMM (BASELINE configs[4]): both operands KC fp8 with per-row fp32 scales, the 4-wave kernel in fp8 mode.
 // ------------------------------------------------------------------------------------------------------------
-extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const float* a_scale,
-                             const svla_operand* B, const float* b_scale, void* const* c_ptr,
-                             const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc, const svla_epilogue* epi,
-                             void* workspace, size_t ws_bytes, void* stream) {
+namespace {
+int gemm_fp8_common(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B, F8Scales fs,
+                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
+                    const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream) {
   SVLA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 16 == 0, "gemm_fp8: sizes M=%lld N=%lld K=%lld (K multiple of 16)",
                  (long long)M, (long long)N, (long long)K);
-  SVLA_CHECK_ARG(A && B && epi && a_scale && b_scale, "gemm_fp8: NULL argument");
-  SVLA_CHECK_ARG(aligned16(a_scale) && aligned16(b_scale), "gemm_fp8: scales must be 16-B aligned");
+  SVLA_CHECK_ARG(A && B && epi, "gemm_fp8: NULL argument");
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   for (const svla_operand* op : {A, B}) {
     SVLA_CHECK_ARG(op->layout == SVLA_LAYOUT_KC, "gemm_fp8: operands must be KC (reduction dim contiguous)");
@@ -3456,9 +3575,6 @@ extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand
   B2.ld /= 2;
   A2.k_valid /= 2;
   B2.k_valid /= 2;
-  F8Scales fs;
-  fs.sa = a_scale;
-  fs.sb = b_scale;
   fs.na = A->r_valid > 0 ? A->r_valid : M;
   fs.nb = geglu ? 2 * B->seg_start[1] : (B->r_valid > 0 ? B->r_valid : N);
   fs.geglu_I = geglu ? B->seg_start[1] : 0;
@@ -3467,4 +3583,45 @@ extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand
   ctx.ws_bytes = workspace ? ws_bytes : 0;
   ctx.variant = 0;
   return launch4(M, N, K / 2, A2, B2, C, *epi, ctx, (hipStream_t)stream, &fs);
+}
+}  // namespace
+
+extern "C" int svla_gemm_fp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const float* a_scale,
+                             const svla_operand* B, const float* b_scale, void* const* c_ptr,
+                             const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc, const svla_epilogue* epi,
+                             void* workspace, size_t ws_bytes, void* stream) {
+  SVLA_CHECK_ARG(a_scale && b_scale && aligned16(a_scale) && aligned16(b_scale),
+                 "gemm_fp8: row scales must be non-NULL and 16-B aligned");
+  F8Scales fs;
+  memset(&fs, 0, sizeof(fs));
+  fs.sa = a_scale;
+  fs.sb = b_scale;
+  return gemm_fp8_common(M, N, K, A, B, fs, c_ptr, c_seg_start, c_nseg, ldc, epi, workspace, ws_bytes, stream);
+}
+
+extern "C" int svla_gemm_mxfp8(int64_t M, int64_t N, int64_t K, const svla_operand* A, const void* a_mx,
+                               int64_t a_mx_ld, int64_t a_mx_bytes, const svla_operand* B, const void* b_mx,
+                               int64_t b_mx_ld, int64_t b_mx_bytes, void* const* c_ptr, const int64_t* c_seg_start,
+                               int32_t c_nseg, int64_t ldc, const svla_epilogue* epi, void* workspace,
+                               size_t ws_bytes, void* stream) {
+  SVLA_CHECK_ARG(a_mx && b_mx && ((uintptr_t)a_mx & 3) == 0 && ((uintptr_t)b_mx & 3) == 0,
+                 "gemm_mxfp8: block scales must be non-NULL and 4-B aligned");
+  SVLA_CHECK_ARG(K % 128 == 0 && (A->k_valid == 0 || A->k_valid % 128 == 0) && (B->k_valid == 0 || B->k_valid % 128 == 0),
+                 "gemm_mxfp8: K and k_valid must be multiples of 128 (whole MX k-tiles)");
+  const int64_t ra = A->r_valid > 0 ? A->r_valid : M;
+  const int64_t rb = epi->kind == SVLA_EPI_GEGLU ? N : (B->r_valid > 0 ? B->r_valid : N);
+  SVLA_CHECK_ARG(a_mx_ld >= 4 * ra && b_mx_ld >= 4 * rb && a_mx_ld % 4 == 0 && b_mx_ld % 4 == 0,
+                 "gemm_mxfp8: scale tile strides must cover 4 bytes per row");
+  SVLA_CHECK_ARG(a_mx_bytes >= (K / 128 - 1) * a_mx_ld + 4 * ra && b_mx_bytes >= (K / 128 - 1) * b_mx_ld + 4 * rb &&
+                     a_mx_bytes < ((int64_t)1 << 31) && b_mx_bytes < ((int64_t)1 << 31),
+                 "gemm_mxfp8: scale buffers too small (or >= 2 GiB)");
+  F8Scales fs;
+  memset(&fs, 0, sizeof(fs));
+  fs.ma = (const uint8_t*)a_mx;
+  fs.mb = (const uint8_t*)b_mx;
+  fs.ma_ld = a_mx_ld;
+  fs.mb_ld = b_mx_ld;
+  fs.ma_bytes = a_mx_bytes;
+  fs.mb_bytes = b_mx_bytes;
+  return gemm_fp8_common(M, N, K, A, B, fs, c_ptr, c_seg_start, c_nseg, ldc, epi, workspace, ws_bytes, stream);
 }

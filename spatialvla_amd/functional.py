@@ -278,12 +278,17 @@ class LinearFn(torch.autograd.Function):
 WEIGHT_EPOCH = [0]
 # fp8 projections: the input-gradient (dgrad) GEMMs run in e4m3 too (the weight-gradient GEMMs stay bf16)
 FP8_DGRAD = [True]
+# scaling of the fp8 operands: "mx" = OCP MX block scales (one E8M0 scale per 32 k, applied by the MFMA; the product
+# path), "row" = one fp32 scale per row applied in the epilogue (round 2-4)
+FP8_SCALING = [os.environ.get("SVLA_FP8_SCALING", "mx")]
 
 
 class FP8Weights:
-    """Row-wise e4m3 copies of one Gemma2 layer's projection weights (BASELINE configs[4]): q|k|v [4096, H],
-    o [H, 2048], gate|up [2I, H], down [H, I], each with its per-row fp32 scales (svla_quant_fp8_rows).  Rebuilt
-    lazily when a weight moved, was modified in place, or the optimizer stepped (WEIGHT_EPOCH)."""
+    """e4m3 copies of one Gemma2 layer's projection weights (BASELINE configs[4]): q|k|v [4096, H], o [H, 2048],
+    gate|up [2I, H], down [H, I].  MX scaling: the forward copy W (MX blocks along the input dim K) and, for dgrad,
+    W^T (blocks along the output dim N: the dgrad GEMM's reduction) each quantised from bf16 (svla_quant_mx_rows);
+    row scaling: per-row fp32 scales, W^T the byte transpose of the forward copy.  Rebuilt lazily when a weight
+    moved, was modified in place, or the optimizer stepped (WEIGHT_EPOCH)."""
 
     def __init__(self):
         self._key = None
@@ -294,23 +299,29 @@ class FP8Weights:
         mats = K._merge_rows(list(mats))
         return mats[0] if len(mats) == 1 else torch.cat(mats, 0)
 
-    def get(self, name, mats):
-        key = (WEIGHT_EPOCH[0],) + tuple((m.data_ptr(), m._version) for m in mats)
+    def _entry(self, name, mats):
+        key = (WEIGHT_EPOCH[0], FP8_SCALING[0]) + tuple((m.data_ptr(), m._version) for m in mats)
         hit = self.mats.get(name)
-        if hit is None or hit[0] != key:
-            q, s = K.quant_fp8_rows(self._rows(mats))
-            hit = (key, q, s, None)
-            self.mats[name] = hit
-        return hit[1], hit[2]
+        if hit is None or hit["key"] != key:
+            w = self._rows(mats)
+            q, s = K.quant_mx_rows(w) if FP8_SCALING[0] == "mx" else K.quant_fp8_rows(w)
+            hit = self.mats[name] = {"key": key, "q": q, "s": s}
+        return hit
+
+    def get(self, name, mats):
+        e = self._entry(name, mats)
+        return e["q"], e["s"]
 
     def get_t(self, name, mats):
-        """(W_q^T [K, N] e4m3, the row scales s [N] of W_q): the byte transpose of the forward copy, for dgrad."""
-        self.get(name, mats)
-        key, q, s, qt = self.mats[name]
-        if qt is None:
-            qt = K.transpose_u8(q)
-            self.mats[name] = (key, q, s, qt)
-        return qt, s
+        """The dgrad operand: MX -- (e4m3 W^T [K, N], its MX scales); row -- (the byte transpose of the forward copy,
+        the forward copy's row scales s [N])."""
+        e = self._entry(name, mats)
+        if "qt" not in e:
+            if FP8_SCALING[0] == "mx":
+                e["qt"], e["st"] = K.quant_mx_rows(self._rows(mats).t().contiguous())
+            else:
+                e["qt"], e["st"] = K.transpose_u8(e["q"]), e["s"]
+        return e["qt"], e["st"]
 
     def ones(self, n, device):
         o = self.mats.get(("ones", n))
@@ -320,19 +331,27 @@ class FP8Weights:
 
 
 def _fp8_linear(x, f8, name, mats, out, **kw):
-    """out = epi(x @ cat(mats)^T) with both operands quantised row-wise to e4m3 (x per call, weights cached)."""
-    xq, xs = K.quant_fp8_rows(x)
+    """out = epi(x @ cat(mats)^T) with both operands quantised to e4m3 (x per call, weights cached)."""
     wq, ws = f8.get(name, mats)
-    K.gemm_fp8(xq, xs, wq, ws, out, **kw)
+    if FP8_SCALING[0] == "mx":
+        xq, xs = K.quant_mx_rows(x)
+        K.gemm_mxfp8(xq, xs, wq, ws, out, **kw)
+    else:
+        xq, xs = K.quant_fp8_rows(x)
+        K.gemm_fp8(xq, xs, wq, ws, out, **kw)
 
 
 def _fp8_dgrad(dy, f8, name, mats, out):
-    """out[M, K] = dy[M, N] @ cat(mats)[N, K] on the fp8 GEMM.  The forward's e4m3 weight W ~ diag(s_w) W_q is
-    reused transposed: dy's columns are scaled by s_w before dy is quantised per row, so
-    out = s_dy[m] * sum_n q_dy[m, n] W_q[n, k] -- one e4m3 GEMM against the byte-transposed W_q."""
-    wt, sw = f8.get_t(name, mats)
-    dq, ds = K.quant_fp8_rows(dy, colscale=sw)
-    K.gemm_fp8(dq, ds, wt, f8.ones(wt.shape[0], dy.device), out)
+    """out[M, K] = dy[M, N] @ cat(mats)[N, K] on the fp8 GEMM.  MX: dy quantised with blocks along N against the
+    MX copy of W^T.  Row scaling: the forward's e4m3 weight W ~ diag(s_w) W_q reused transposed -- dy's columns are
+    scaled by s_w before dy is quantised per row, so out = s_dy[m] * sum_n q_dy[m, n] W_q[n, k]."""
+    wt, st = f8.get_t(name, mats)
+    if FP8_SCALING[0] == "mx":
+        dq, ds = K.quant_mx_rows(dy)
+        K.gemm_mxfp8(dq, ds, wt, st, out)
+    else:
+        dq, ds = K.quant_fp8_rows(dy, colscale=st)
+        K.gemm_fp8(dq, ds, wt, f8.ones(wt.shape[0], dy.device), out)
 
 
 # ------------------------------------------------------------------------------------ Gemma2 blocks

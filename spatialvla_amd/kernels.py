@@ -296,6 +296,71 @@ def quant_fp8_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Opt
     return q, scale
 
 
+class MXScales:
+    """E8M0 block scales of an MX-quantised [rows, K] matrix in svla_quant_mx_rows' tile-major layout: a uint8 buffer
+    of K/128 k-tiles, each `ld` bytes (4 per row, rows padded to a multiple of 256 so every 256-row tile's scale rows
+    are in the buffer)."""
+
+    def __init__(self, rows: int, K: int, device, buf: Optional[torch.Tensor] = None):
+        self.rows, self.K = rows, K
+        self.ld = 4 * ((rows + 255) // 256 * 256)
+        n = (K // 128) * self.ld
+        self.buf = buf if buf is not None else torch.empty(n, dtype=torch.uint8, device=device)
+        _req(self.buf.dtype == torch.uint8 and self.buf.numel() >= n and self.buf.is_contiguous(), "MXScales: buffer")
+
+    def exponents(self) -> torch.Tensor:
+        """[rows, K/32] int32 exponents X (scale = 2^X): the layout undone, for tests."""
+        t = self.buf[:(self.K // 128) * self.ld].view(self.K // 128, self.ld // 4, 4)[:, :self.rows]
+        return (t.permute(1, 0, 2).reshape(self.rows, self.K // 32).to(torch.int32) - 127)
+
+
+def quant_mx_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, sc: Optional[MXScales] = None):
+    """OCP MX e4m3 quantisation of rows (svla_quant_mx_rows): one E8M0 scale 2^X per 32 consecutive k, X =
+    clamp(floor(log2(amax)) - 8, -127, 127), q = e4m3(clamp(x * 2^-X, +-448)).  Returns (q [rows, K] e4m3,
+    MXScales)."""
+    _chk_bf16(x, "quant_mx_rows")
+    rows, K = x.shape
+    _req(K % 128 == 0, f"quant_mx_rows: K={K} must be a multiple of 128")
+    if q is None:
+        q = torch.empty(rows, K, dtype=FP8, device=x.device)
+    if sc is None:
+        sc = MXScales(rows, K, x.device)
+    _req(q.dtype == FP8 and q.shape == (rows, K) and q.stride(1) == 1, "quant_mx_rows: q must be [rows, K] e4m3")
+    _req(sc.rows >= rows and sc.K == K, "quant_mx_rows: scale buffer shape")
+    L.check(L.lib().svla_quant_mx_rows(rows, K, x.data_ptr(), _ld(x), q.data_ptr(), q.stride(0), sc.buf.data_ptr(),
+                                       sc.ld, _stream()), "svla_quant_mx_rows")
+    return q, sc
+
+
+def gemm_mxfp8(xq: torch.Tensor, xs: MXScales, wq: torch.Tensor, ws: MXScales, out: torch.Tensor,
+               kind=L.EPI_STORE, geglu_I: int = 0, **epi_kw):
+    """out = epi(sum_k 2^(Xa + Xb) xq wq^T) on the MX fp8 MFMA kernel (svla_gemm_mxfp8); wq and ws as gemm_fp8's
+    (geglu_I > 0: gate rows then up rows of one matrix, one scale matrix)."""
+    M, K = xq.shape
+    N = wq.shape[0]
+    _req(wq.shape[1] == K and xs.K == K and ws.K == K, f"gemm_mxfp8: K mismatch ({K}, {wq.shape[1]}, {xs.K}, {ws.K})")
+    _req(xs.rows >= M and ws.rows >= N, "gemm_mxfp8: scale rows")
+    A = _operand_fp8([xq])
+    if geglu_I:
+        B = _operand_fp8([wq[:geglu_I], wq[geglu_I:]], L.SEG_GEGLU, [0, geglu_I])
+    else:
+        B = _operand_fp8([wq])
+    cp = (ctypes.c_void_p * 4)(out.data_ptr(), None, None, None)
+    cs = (ctypes.c_int64 * 5)(0, 0, 0, 0, 0)
+    wsp = gemm_workspace()
+    e = _epi(kind, **epi_kw)
+    rec = launch_timer.get("geglu_fp8") if geglu_I else None
+    if rec is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+    L.check(L.lib().svla_gemm_mxfp8(M, N, K, ctypes.byref(A), xs.buf.data_ptr(), xs.ld, xs.buf.numel(),
+                                    ctypes.byref(B), ws.buf.data_ptr(), ws.ld, ws.buf.numel(), cp, cs, 1, _ld(out),
+                                    ctypes.byref(e), wsp.data_ptr(), wsp.numel(), _stream()), "svla_gemm_mxfp8")
+    if rec is not None:
+        e1.record(torch.cuda.current_stream())
+        rec.append((e0, e1, M, N, K))
+
+
 def transpose_u8(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[c, r] = x[r, c] for a 1-byte-element matrix (e4m3 weight copies), svla_transpose_u8."""
     _req(x.is_cuda and x.element_size() == 1 and x.dim() == 2 and x.stride(1) == 1, "transpose_u8: 1-byte matrix")

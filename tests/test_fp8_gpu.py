@@ -72,8 +72,12 @@ def test_fp8_dgrad_gemm(cuda):
     w = (torch.randn(N, Kd, device=cuda, generator=g) * 0.02).to(BF)
     f8 = Fn.FP8Weights()
     out = torch.empty(M, Kd, dtype=BF, device=cuda)
-    Fn._fp8_dgrad(dy, f8, "w", (w,), out)
-    wq, ws = f8.get("w", (w,))
+    prev, Fn.FP8_SCALING[0] = Fn.FP8_SCALING[0], "row"
+    try:
+        Fn._fp8_dgrad(dy, f8, "w", (w,), out)
+        wq, ws = f8.get("w", (w,))
+    finally:
+        Fn.FP8_SCALING[0] = prev
     dq, ds = K.quant_fp8_rows(dy, colscale=ws)
     exact = (dq.float() * ds[:, None]) @ wq.float()
     bf = dy.float() @ w.float()
@@ -182,3 +186,109 @@ def test_gemma2_layer_fp8_vs_bf16(cuda):
     layer.set_fp8_projections(False)
     y3, _, _ = run()
     assert rel(y2 - x, y3 - x) < 0.12, "fp8 weight copy not refreshed after an in-place update"
+
+
+# ------------------------------------------------------------------------------------------------ OCP MX scaling
+def ref_quant_mx(x):
+    """OCP MX (spec v1.0) e4m3 restatement on the CPU: per 32-k block, X = clamp(ceil(log2(amax / 448)), -127, 127)
+    (amax = 0 or subnormal: -127), q = e4m3(clamp(x * 2^-X, +-448)).  Returns (q, X [rows, K/32] int32)."""
+    xf = x.float().cpu()
+    rows, k = xf.shape
+    blk = xf.view(rows, k // 32, 32)
+    amax = blk.abs().amax(2)
+    bits = amax.view(torch.int32)
+    e = ((bits >> 23) & 0xFF) - 127 - 8 + ((bits & 0x7FFFFF) > 0x600000).int()
+    X = torch.where(((bits >> 23) & 0xFF) == 0, torch.full_like(e, -127), e).clamp(-127, 127)
+    assert bool((blk.abs() * torch.exp2(-X.float())[..., None] <= 448).all())  # nothing saturates
+    q = (blk * torch.exp2(-X.float())[..., None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(rows, k)
+    return q, X
+
+
+def _mx_data(rows, k, g, device):
+    """Random rows whose 32-k blocks span 2^-20 .. 2^20 in magnitude (so per-block scales matter), with an all-zero
+    block, a block of bf16 subnormals and a row of zeros."""
+    x = torch.randn(rows, k, device=device, generator=g)
+    mag = torch.exp2(torch.randint(-20, 21, (rows, k // 32), device=device, generator=g).float())
+    x = (x.view(rows, k // 32, 32) * mag[..., None]).view(rows, k)
+    x[0, :32] = 0
+    x[1, 32:64] = 1e-39
+    x[2, :] = 0
+    return x.to(BF)
+
+
+@pytest.mark.parametrize("rows,k", [(37, 2304), (300, 9216), (5, 2048), (64, 128), (259, 18432)])
+def test_quant_mx_rows_bitexact(cuda, rows, k):
+    g = torch.Generator(device=cuda).manual_seed(rows * 7 + k)
+    x = _mx_data(rows, k, g, cuda)
+    q, sc = K.quant_mx_rows(x)
+    qr, Xr = ref_quant_mx(x)
+    assert torch.equal(sc.exponents().cpu(), Xr)
+    assert torch.equal(q.view(torch.uint8).cpu(), qr.view(torch.uint8))
+
+
+def _dequant_mx(q, sc):
+    X = sc.exponents()
+    rows, k = q.shape
+    return (q.float().view(rows, k // 32, 32) * torch.exp2(X.float())[..., None]).view(rows, k)
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 4096, 2304), (9984, 2304, 2048), (300, 2304, 9216), (256, 512, 128),
+                                   (2000, 1280, 4096), (9984, 2304, 18432)])
+def test_gemm_mxfp8_store(cuda, m, n, k):
+    """The MX kernel against the fp32 product of the dequantised operands (block scales varying 2^-20..2^20 inside
+    every row of both operands, so a wrong lane -> block scale map is an O(1) error), and against the bf16 product."""
+    g = torch.Generator(device=cuda).manual_seed(m + n + k)
+    x = _mx_data(m, k, g, cuda)
+    w = (_mx_data(n, k, g, cuda).float() * 0.02).to(BF)
+    xq, xs = K.quant_mx_rows(x)
+    wq, ws = K.quant_mx_rows(w)
+    out = torch.full((m, n), float("nan"), dtype=BF, device=cuda)
+    K.gemm_mxfp8(xq, xs, wq, ws, out)
+    exact = _dequant_mx(xq, xs) @ _dequant_mx(wq, ws).T
+    bf = x.float() @ w.float().T
+    e_k, e_q = rel(out, exact), rel(out, bf)
+    print(f"mxfp8 gemm {m}x{n}x{k}: vs dequantised fp32 {e_k:.2e}, vs unquantised {e_q:.2e}")
+    assert torch.isfinite(out.float()).all()
+    assert e_k < 4e-3 and e_q < 6e-2
+
+
+def test_fp8_mx_dgrad_gemm(cuda):
+    """dX = dY @ W on the MX path (functional._fp8_dgrad): dY quantised with MX blocks along N against the MX copy of
+    W^T (blocks along N, from the bf16 weight).  Within 4e-3 of the exact product of the quantised operands, within
+    6e-2 of the bf16 product."""
+    from spatialvla_amd import functional as Fn
+    g = torch.Generator(device=cuda).manual_seed(9)
+    M, N, Kd = 2000, 18432, 2304
+    dy = torch.randn(M, N, device=cuda, generator=g).to(BF)
+    w = (torch.randn(N, Kd, device=cuda, generator=g) * 0.02).to(BF)
+    f8 = Fn.FP8Weights()
+    out = torch.empty(M, Kd, dtype=BF, device=cuda)
+    prev, Fn.FP8_SCALING[0] = Fn.FP8_SCALING[0], "mx"
+    try:
+        Fn._fp8_dgrad(dy, f8, "w", (w,), out)
+        wt, st = f8.get_t("w", (w,))
+    finally:
+        Fn.FP8_SCALING[0] = prev
+    dq, ds = K.quant_mx_rows(dy)
+    exact = _dequant_mx(dq, ds) @ _dequant_mx(wt, st).T
+    bf = dy.float() @ w.float()
+    e_k, e_q = rel(out, exact), rel(out, bf)
+    print(f"mx dgrad: vs quantised-operand product {e_k:.2e}, vs bf16 {e_q:.2e}")
+    assert e_k < 4e-3 and e_q < 6e-2
+
+
+def test_gemm_mxfp8_geglu(cuda):
+    """Gemma2 gate|up GeGLU epilogue on the MX kernel (one [2I] weight and scale matrix, gate rows then up rows)."""
+    m, hdim, inter = 700, 2304, 1536
+    g = torch.Generator(device=cuda).manual_seed(31)
+    x = torch.randn(m, hdim, device=cuda, generator=g).to(BF)
+    w = (torch.randn(2 * inter, hdim, device=cuda, generator=g) * 0.02).to(BF)
+    xq, xs = K.quant_mx_rows(x)
+    wq, ws = K.quant_mx_rows(w)
+    h, gg, uu = (torch.empty(m, inter, dtype=BF, device=cuda) for _ in range(3))
+    K.gemm_mxfp8(xq, xs, wq, ws, h, kind=L.EPI_GEGLU, geglu_I=inter, out1=gg, out2=uu)
+    exact = _dequant_mx(xq, xs) @ _dequant_mx(wq, ws).T
+    ge, ue = exact[:, :inter].to(BF), exact[:, inter:].to(BF)
+    he = (torch.nn.functional.gelu(ge.float(), approximate="tanh").to(BF).float() * ue.float()).to(BF)
+    print(f"mxfp8 geglu: g {rel(gg, ge):.2e} u {rel(uu, ue):.2e} h {rel(h, he):.2e}")
+    assert rel(gg, ge) < 4e-3 and rel(uu, ue) < 4e-3 and rel(h, he) < 6e-3

@@ -154,6 +154,7 @@ _NORM_SUFFIXES = ("layernorm.weight", "layer_norm1.weight", "layer_norm2.weight"
 
 DRIFT_MAX = 3.2e-2     # largest non-q/k full-tensor gradient error (measured 3.11e-2 r3, 3.12e-2 r4)
 DRIFT_MEDIAN = 2.8e-2  # median over all tensors (measured 2.72e-2 r3 and r4)
+DRIFT_COUNT = 14       # non-q/k tensors above 3e-2 (measured 12 r3; 10 r4p -> 14 r4r, DESIGN.md §2 "drift count")
 
 
 def _full_tol(name: str) -> float:
@@ -242,15 +243,15 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
     # drift guard: the named 4e-2 exceptions may not absorb a general loss of accuracy.  Bounded at the
     # measured round-3 level: the largest non-q/k error (3.11e-2 r3, 3.12e-2 r4: every one a gate_proj / norm weight)
     # at 3.2e-2, far inside the 4e-2 exception, and the median over all 707 tensors (2.72e-2 r3 and r4) at 2.8e-2.
-    # The count of tensors just above 3e-2 is reported, not bounded: 12 in r3, 14 in r4 with the stored-dS attention
-    # backward (Delta and dQ summed in another order), all within 3.0-3.12e-2 -- a step function of values sitting
-    # on the threshold, which the max and median above bound instead.
+    # The count of non-q/k tensors above 3e-2 is bounded too, at its r4 level (12 in r3; 10 in r4p -> 14 in r4r with
+    # the stored-dS attention backward: the four new ones sit at 3.00-3.01e-2, root cause in DESIGN.md §2).
     over = sorted((e, n) for n, e in full_rel.items() if e > H.GRAD_TOL and not _qk_exception(n))
     med = _pct(full_rel.values(), 50)
     print(f"4B drift guard: {len(over)} non-q/k tensors above {H.GRAD_TOL} (max {over[-1][0] if over else 0:.4f}), "
           f"median {med:.4f}")
     assert not over or over[-1][0] <= DRIFT_MAX, over[-6:]
     assert med <= DRIFT_MEDIAN, med
+    assert len(over) <= DRIFT_COUNT, over
 
 
 @pytest.mark.timeout(600)
@@ -300,6 +301,14 @@ def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
     assert st["lse"] <= FP8_TOL["lse"]
     assert st["agree_025"] >= FP8_TOL["agree_025"]
     assert max(st["gradnorm"].values()) < FP8_TOL["gradnorm"], worst
+    # the bounds this golden can hold for fp8 (deterministic kernels, so these are exact run to run): argmax agreement
+    # on rows with a reference margin > 0.05 (0.73 measured r5 with MX block scales; 0.72 r4 with row scales) and the
+    # confident action rows (5 of 9 agree, r4 and r5).  The random-init golden's logits are nearly flat (median
+    # top-1/top-2 margin 0.16, action rows <= 0.28) against an fp8 logit error of 0.13-0.14 rel-L2, so a near-tie
+    # row flips with the quantisation noise; 0.90 at margin 0.05 is not reachable with 3-bit mantissas here.
+    assert st["agree_005"] >= FP8_TOL["agree_005"], st["agree_005"]
+    assert st["action_rows_conf_agree"] >= FP8_TOL["action_rows_agree"], (st["action_rows_conf_agree"],
+                                                                          st["action_rows_conf"])
 
 
 # configs[4] tolerances vs the reference's bf16: e4m3 keeps 3 mantissa bits (relative step 2^-3 at the top of a
@@ -307,7 +316,8 @@ def test_full4b_fp8_train_step_vs_reference(model4b, gold, cuda):
 # Measured r3: loss 13.0387 vs 13.0677 (2.9e-2), action logits rel-L2 0.138, 256-column logits 0.129, lse 2.1e-3,
 # argmax agreement 0.95 on rows with a reference margin > 0.25, worst gradient norm 6.2e-2 (SigLIP layer norms:
 # the fp8 error of the Gemma2 input-gradient GEMMs reaches them through the projector).
-FP8_TOL = {"loss": 0.05, "logits": 0.15, "lse": 1e-2, "agree_025": 0.9, "gradnorm": 0.1}
+FP8_TOL = {"loss": 0.05, "logits": 0.15, "lse": 1e-2, "agree_025": 0.9, "gradnorm": 0.1, "agree_005": 0.72,
+           "action_rows_agree": 5}
 
 
 @pytest.mark.timeout(900)

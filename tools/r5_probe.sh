@@ -16,6 +16,19 @@ step() {
   if [ $rc -gt 1 ]; then echo "[$name] stopping: crash or timeout"; exit $rc; fi
   return 0
 }
+if [ -n "$TESTS" ]; then
+  step pytest 900 python -u -m pytest tests -m gpu -k "$TESTS" ${PYX--x} -v -s --timeout 600 --timeout-method thread > $O/pytest.txt 2>&1
+  tail -5 $O/pytest.txt
+  mkdir -p $O/parity && cp gpurun_out/parity/*.json $O/parity/ 2>/dev/null
+fi
+if [ -n "$BLOCK_AB" ]; then
+  step block_ab 300 python -u tools/block_lib_ab.py spatialvla_amd/libsvla.so $BLOCK_AB 5 > $O/block_ab.txt 2>&1
+  cat $O/block_ab.txt
+fi
+if [ -n "$MXDBG" ]; then
+  step mxdbg 120 python -u tools/mx_debug.py > $O/mx_debug.txt 2>&1
+  cat $O/mx_debug.txt
+fi
 if [ -n "$LIST" ]; then timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1; fi
 if [ -n "$STAMPS" ]; then
   step stamps 300 python -u tools/stamps_multi.py $STAMPS -- $STAMP_SHAPES > $O/stamps.txt 2>&1
@@ -40,6 +53,15 @@ if [ -n "$GEMM_PMC" ]; then
     step gemm_pmc 400 tools/gemm_pmc2.sh $TAG ${shp//,/ } > $O/gemm_pmc_$shp.log 2>&1
   done
   for f in $O/*_svla.txt $O/*_torch.txt; do echo "== $f"; cat $f; done
+fi
+if [ -n "$FP8_PMC" ]; then
+  for arm in $FP8_PMC; do
+    step fp8_run 120 python3 tools/fp8_pmc_one.py $arm 9984 18432 2304 20 >> $O/fp8_runs.txt 2>&1
+    step fp8_pmc1 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d /tmp/f8p1_$arm -o p1 --output-format csv -- python3 tools/fp8_pmc_one.py $arm 9984 18432 2304 10 > /dev/null 2>&1
+    step fp8_pmc2 180 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE -d /tmp/f8p2_$arm -o p2 --output-format csv -- python3 tools/fp8_pmc_one.py $arm 9984 18432 2304 10 > /dev/null 2>&1
+    python tools/pmc_table.py /tmp/f8p1_$arm /tmp/f8p2_$arm > $O/fp8_pmc_$arm.txt 2>&1
+  done
+  cat $O/fp8_runs.txt; grep -A16 "gemm4" $O/fp8_pmc_*.txt
 fi
 if [ -n "$BENCH" ]; then
   step bench 600 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err

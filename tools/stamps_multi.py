@@ -8,7 +8,7 @@ import torch
 from spatialvla_amd import kernels as K, _lib as L
 
 sep = sys.argv.index("--")
-libs = [(os.path.basename(p), L.load(os.path.abspath(p))) for p in sys.argv[1:sep]]
+libs = [(os.path.basename(p), L.load(os.path.abspath(p), strict=False)) for p in sys.argv[1:sep]]
 shapes = []
 for s in sys.argv[sep + 1:]:
     f = s.split(",")
@@ -34,10 +34,18 @@ for M, N, Kd, lay in shapes:
         buf = np.zeros((16384, 4, 14), dtype=np.uint64)
         fn = lib.svla_diag_g4_stamps
         fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        torch.cuda.synchronize()
+        lib.svla_diag_g4_stamps_clear()
         f(); torch.cuda.synchronize()
         assert fn(buf.ctypes.data, buf.nbytes) == 0
         s = buf.astype(np.float64)
         s = s[s[:, 0, 7] > 0]
+        tot = s[:, :, 7].max(1)  # per block: the slowest wave
+        order = np.argsort(tot)
+        pb = lambda b: (f"total {tot[b]:.0f} = dp k-tiles {s[b, 0, 13]:.0f}, sk k-tiles {s[b, 0, 12]:.0f} in "
+                        f"{s[b, 0, 11]:.0f}, tiles {s[b, 0, 6]:.0f}, epilogue {s[b, 0, 5]:.0f}")
+        print(f"    blocks {len(s)}: total ticks min {tot.min():.0f} median {np.median(tot):.0f} max {tot.max():.0f}; "
+              f"slowest block: {pb(order[-1])}; median block: {pb(order[len(order) // 2])}", flush=True)
         nt = s[..., 6].sum(0)[0]
         ml = s[..., 3] + s[..., 4]
         sk_t, sk_n, dp_n = s[..., 11], s[..., 12], s[..., 13]
