@@ -411,6 +411,15 @@ int svla_zoe_attractor(int B, int H, int W, int n_att, int n_bins, const void* a
  * (b, t) = [hidden(b, 1 + t), hidden(b, 0)] -- the values torch.cat(hidden_states) + permute + torch.cat((tokens,
  * readout), -1) produce, in one pass; C % 8 == 0, 16-B aligned. */
 int svla_zoe_readout_cat(int64_t B, int64_t T, int64_t C, const void* hidden, void* out, void* stream);
+/* process_zoe (model/modeling_spatialvla.py:99-110) in one pass: out[b,c] = bf16(bf16(bicubic(reflect_pad(x, pad))
+ * - mean[c]) / std[c]) at OH x OW, bicubic as torch's upsample_bicubic2d with align_corners=True (A = -0.75, border
+ * taps clamped, fp32, one bf16 rounding), TF.normalize's sub and div each rounded to bf16.  x, out bf16 NCHW
+ * contiguous; C <= 4; mean/std host arrays of C floats (their bf16 values). */
+int svla_zoe_preprocess(int B, int C, int H, int W, int pad, int OH, int OW, const void* x, const float* mean,
+                        const float* stdv, void* out, void* stream);
+/* The depth resize of model/modeling_spatialvla.py:318-323: out[b] = bicubic(depth[b], size (OH+2pad) x (OW+2pad),
+ * align_corners=True)[pad:-pad, pad:-pad], bf16 [B][IH][IW] -> bf16 [B][OH][OW]; only the kept pixels computed. */
+int svla_zoe_depth_resize(int B, int IH, int IW, int pad, int OH, int OW, const void* depth, void* out, void* stream);
 /* Bilinear resize of a channels-last bf16 map [B, H1, W1, C] -> [B, H2, W2, C] with torch's
  * upsample_bilinear2d semantics (transformers ZoeDepthFeatureFusionLayer.forward interpolate(scale_factor=2,
  * align_corners=True) and the relative head's nn.Upsample, called from modeling_spatialvla.py:317-323's Zoe

@@ -139,6 +139,8 @@ SIGNATURES = {
     "svla_zoe_readout_cat": (c_i32, [c_i64] * 3 + [c_vp] * 3),
     "svla_zoe_attractor": (c_i32, [c_i32] * 5 + [c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_f32, c_i32,
                                    c_i32, c_vp, ctypes.POINTER(c_i64), c_vp]),
+    "svla_zoe_preprocess": (c_i32, [c_i32] * 7 + [c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f32), c_vp, c_vp]),
+    "svla_zoe_depth_resize": (c_i32, [c_i32] * 6 + [c_vp, c_vp, c_vp]),
     "svla_zoe_metric_tail": (c_i32, [c_i32] * 9 + [c_vp, ctypes.POINTER(c_i64)] * 4 + [c_vp] + [c_f32] * 4
                              + [c_vp, c_vp]),
 }

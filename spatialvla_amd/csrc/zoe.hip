@@ -464,3 +464,171 @@ extern "C" int svla_upsample_bilinear_nhwc(int B, int C, int H1, int W1, int H2,
                      (hipStream_t)stream, a);
   return svla::check_launch("upsample_bilinear_nhwc");
 }
+
+// ---------------------------------------------------------------------------------------------
+// process_zoe (reference model/modeling_spatialvla.py:99-110) and the depth resize after the estimator (:318-323)
+// as one pass each, instead of pad + upsample_bicubic2d + sub + div (and upsample_bicubic2d + crop + copy) on ATen.
+//  * zoe_preprocess: out[b,c,oy,ox] = bf16(bf16(bicubic(reflect_pad(x, P))[oy,ox] - mean_c) / std_c): the padded
+//    (H+2P)x(W+2P) image is never formed (a tap at padded coordinate p reads x at reflect(p - P)); bicubic as torch's
+//    upsample_bicubic2d (align_corners=True: source = scale * dst, scale = (in - 1) / (out - 1); A = -0.75; taps
+//    clamped to the padded image's border), fp32, rounded to bf16 once; TF.normalize's sub and div each rounded to
+//    bf16 as torch's bf16 elementwise kernels do.
+//  * zoe_depth_resize: out[b,y,x] = bf16(bicubic(depth[b], size (H+2P)x(W+2P))[y+P, x+P]): only the rows and
+//    columns the crop [..., P:-P, P:-P] keeps are computed.
+// Two contraction forms of torch's expressions (V): 0 = as hipcc contracts them under -ffp-contract=fast, 1 = every
+// product and sum rounded separately; tests/test_model_gpu.py compares both with the stock ops.
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct ZoePre {
+  int B, C, H, W, P, OH, OW;
+  float scale_h, scale_w;
+  float mean[4], stdv[4];
+  const bf16_t* x;
+  bf16_t* out;
+};
+
+template <int V>
+__device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
+  constexpr float A = -0.75f;
+  if constexpr (V == 0) {
+    auto cc1 = [](float x) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; };
+    auto cc2 = [](float x) { return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A; };
+    c[0] = cc2(t + 1.f);
+    c[1] = cc1(t);
+    c[2] = cc1(1.f - t);
+    c[3] = cc2((1.f - t) + 1.f);
+  } else {
+    auto cc1 = [](float x) {
+      return __fadd_rn(__fmul_rn(__fmul_rn(__fsub_rn(__fmul_rn(A + 2.f, x), A + 3.f), x), x), 1.f);
+    };
+    auto cc2 = [](float x) {
+      return __fsub_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fsub_rn(__fmul_rn(A, x), 5.f * A), x), 8.f * A), x), 4.f * A);
+    };
+    c[0] = cc2(__fadd_rn(t, 1.f));
+    c[1] = cc1(t);
+    const float x2 = __fsub_rn(1.f, t);
+    c[2] = cc1(x2);
+    c[3] = cc2(__fadd_rn(x2, 1.f));
+  }
+}
+
+template <int V>
+__device__ __forceinline__ float cubic_1d(float x0, float x1, float x2, float x3, const float c[4]) {
+  if constexpr (V == 0) return x0 * c[0] + x1 * c[1] + x2 * c[2] + x3 * c[3];
+  else return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(x0, c[0]), __fmul_rn(x1, c[1])), __fmul_rn(x2, c[2])),
+                        __fmul_rn(x3, c[3]));
+}
+
+__device__ __forceinline__ int reflect_idx(int p, int n) {  // F.pad reflect for one overhang (p in (-n, 2n - 1))
+  return p < 0 ? -p : (p >= n ? 2 * (n - 1) - p : p);
+}
+
+// bicubic sample of a (virtually padded) image at output (oy, ox): fetch(yy, xx) reads the unpadded source
+template <int V, typename Fetch>
+__device__ __forceinline__ float bicubic_at(int oy, int ox, float sh, float sw, int IH, int IW, Fetch fetch) {
+  const float ry = sh * (float)oy, rx = sw * (float)ox;
+  const int iy = (int)floorf(ry), ix = (int)floorf(rx);
+  const float ty = ry - (float)iy, tx = rx - (float)ix;
+  float cx[4], cy[4], rows[4];
+  cubic_coeffs<V>(tx, cx);
+  cubic_coeffs<V>(ty, cy);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int yy = min(max(iy - 1 + k, 0), IH - 1);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = fetch(yy, min(max(ix - 1 + j, 0), IW - 1));
+    rows[k] = cubic_1d<V>(v[0], v[1], v[2], v[3], cx);
+  }
+  return cubic_1d<V>(rows[0], rows[1], rows[2], rows[3], cy);
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void zoe_preprocess_kernel(ZoePre a) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.C * a.OH * a.OW;
+  if (idx >= total) return;
+  const int ox = (int)(idx % a.OW);
+  int64_t r = idx / a.OW;
+  const int oy = (int)(r % a.OH);
+  r /= a.OH;
+  const int c = (int)(r % a.C);
+  const int b = (int)(r / a.C);
+  const bf16_t* src = a.x + ((int64_t)b * a.C + c) * a.H * a.W;
+  const int PH = a.H + 2 * a.P, PW = a.W + 2 * a.P;
+  auto fetch = [&](int py, int px) {
+    return bf2f(src[(int64_t)reflect_idx(py - a.P, a.H) * a.W + reflect_idx(px - a.P, a.W)]);
+  };
+  const float v = round_bf(bicubic_at<V>(oy, ox, a.scale_h, a.scale_w, PH, PW, fetch));
+  const float y = round_bf(v - a.mean[c]);
+  a.out[idx] = f2bf(__fdiv_rn(y, a.stdv[c]));
+}
+
+struct ZoeDepthRs {
+  int B, IH, IW, P, OH, OW;  // OH x OW: the cropped output; the resize target is (OH + 2P) x (OW + 2P)
+  float scale_h, scale_w;
+  const bf16_t* depth;
+  bf16_t* out;
+};
+
+template <int V>
+__global__ __launch_bounds__(256) void zoe_depth_resize_kernel(ZoeDepthRs a) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)a.B * a.OH * a.OW;
+  if (idx >= total) return;
+  const int x = (int)(idx % a.OW);
+  int64_t r = idx / a.OW;
+  const int y = (int)(r % a.OH);
+  const int b = (int)(r / a.OH);
+  const bf16_t* src = a.depth + (int64_t)b * a.IH * a.IW;
+  auto fetch = [&](int yy, int xx) { return bf2f(src[(int64_t)yy * a.IW + xx]); };
+  a.out[idx] = f2bf(bicubic_at<V>(y + a.P, x + a.P, a.scale_h, a.scale_w, a.IH, a.IW, fetch));
+}
+
+int g_zoe_bicubic_variant = 0;  // diagnostic switch (svla_diag_zoe_bicubic_variant), 0 in the product
+}  // namespace
+
+extern "C" int svla_diag_zoe_bicubic_variant(int v) {  // diagnostics only (not in svla.h)
+  SVLA_CHECK_ARG(v == 0 || v == 1, "zoe bicubic variant %d", v);
+  g_zoe_bicubic_variant = v;
+  return 0;
+}
+
+extern "C" int svla_zoe_preprocess(int B, int C, int H, int W, int pad, int OH, int OW, const void* x,
+                                   const float* mean, const float* stdv, void* out, void* stream) {
+  SVLA_CHECK_ARG(B > 0 && C > 0 && C <= 4 && H > 1 && W > 1 && pad >= 0 && pad < H && pad < W && OH > 1 && OW > 1,
+                 "zoe_preprocess: bad sizes (C <= 4, reflect pad < H, W)");
+  SVLA_CHECK_ARG(x && mean && stdv && out, "zoe_preprocess: NULL pointer");
+  ZoePre a;
+  a.B = B; a.C = C; a.H = H; a.W = W; a.P = pad; a.OH = OH; a.OW = OW;
+  a.scale_h = (float)(H + 2 * pad - 1) / (float)(OH - 1);
+  a.scale_w = (float)(W + 2 * pad - 1) / (float)(OW - 1);
+  for (int i = 0; i < 4; ++i) {
+    a.mean[i] = i < C ? mean[i] : 0.f;
+    a.stdv[i] = i < C ? stdv[i] : 1.f;
+  }
+  a.x = (const bf16_t*)x;
+  a.out = (bf16_t*)out;
+  const int64_t total = (int64_t)B * C * OH * OW;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (g_zoe_bicubic_variant) hipLaunchKernelGGL(zoe_preprocess_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(zoe_preprocess_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  return svla::check_launch("zoe_preprocess");
+}
+
+extern "C" int svla_zoe_depth_resize(int B, int IH, int IW, int pad, int OH, int OW, const void* depth, void* out,
+                                     void* stream) {
+  SVLA_CHECK_ARG(B > 0 && IH > 1 && IW > 1 && pad >= 0 && OH > 0 && OW > 0, "zoe_depth_resize: bad sizes");
+  SVLA_CHECK_ARG(depth && out, "zoe_depth_resize: NULL pointer");
+  ZoeDepthRs a;
+  a.B = B; a.IH = IH; a.IW = IW; a.P = pad; a.OH = OH; a.OW = OW;
+  a.scale_h = (float)(IH - 1) / (float)(OH + 2 * pad - 1);
+  a.scale_w = (float)(IW - 1) / (float)(OW + 2 * pad - 1);
+  a.depth = (const bf16_t*)depth;
+  a.out = (bf16_t*)out;
+  const int64_t total = (int64_t)B * OH * OW;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (g_zoe_bicubic_variant) hipLaunchKernelGGL(zoe_depth_resize_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(zoe_depth_resize_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  return svla::check_launch("zoe_depth_resize");
+}

@@ -870,6 +870,35 @@ def zoe_attractor(attractors: torch.Tensor, centres: torch.Tensor, alpha: float,
     return out
 
 
+# ---------------------------------------------------------------------------------------- Zoe pre/post resize
+def zoe_preprocess(x: torch.Tensor, pad: int, size, mean, std) -> torch.Tensor:
+    """process_zoe (reference modeling_spatialvla.py:99-110) in one kernel: reflect pad, bicubic resize to `size`
+    (align_corners=True) and (x - mean) / std with the reference's bf16 roundings.  x bf16 [B, C, H, W]."""
+    _chk_bf16(x, "zoe_preprocess")
+    _req(x.dim() == 4 and x.is_contiguous() and x.shape[1] <= 4, "zoe_preprocess: x must be contiguous [B, C<=4, H, W]")
+    B, C, H, W = x.shape
+    OH, OW = size
+    out = torch.empty(B, C, OH, OW, dtype=x.dtype, device=x.device)
+    m = (ctypes.c_float * C)(*[float(v) for v in mean])
+    sd = (ctypes.c_float * C)(*[float(v) for v in std])
+    L.check(L.lib().svla_zoe_preprocess(B, C, H, W, int(pad), OH, OW, x.data_ptr(), m, sd, out.data_ptr(), _stream()),
+            "zoe_preprocess")
+    return out
+
+
+def zoe_depth_resize(depth: torch.Tensor, pad: int, size) -> torch.Tensor:
+    """F.interpolate(depth[:, None], size + 2 pad, bicubic, align_corners=True)[..., pad:-pad, pad:-pad] (reference
+    modeling_spatialvla.py:318-323) in one kernel.  depth bf16 [B, IH, IW] -> [B, 1, OH, OW]."""
+    _chk_bf16(depth, "zoe_depth_resize")
+    _req(depth.dim() == 3 and depth.is_contiguous(), "zoe_depth_resize: depth must be contiguous [B, IH, IW]")
+    B, IH, IW = depth.shape
+    OH, OW = size
+    out = torch.empty(B, 1, OH, OW, dtype=depth.dtype, device=depth.device)
+    L.check(L.lib().svla_zoe_depth_resize(B, IH, IW, int(pad), OH, OW, depth.data_ptr(), out.data_ptr(), _stream()),
+            "zoe_depth_resize")
+    return out
+
+
 # ---------------------------------------------------------------------------------------- Zoe DPT neck resize
 def upsample_bilinear_cl(x: torch.Tensor, size=None, scale_factor=None, align_corners: bool = False):
     """torch.nn.functional.interpolate(x, size / scale_factor, mode="bilinear", align_corners) for a channels-last

@@ -81,8 +81,14 @@ def _zoe_norm_consts(dtype, device):
 
 
 def process_zoe(pixel_values, pad_mode="reflect", output_size=(384, 512)):
-    """Reference :99-110 (ZoeDepth preprocessing)."""
+    """Reference :99-110 (ZoeDepth preprocessing): reflect pad 31, bicubic to 384^2 (align_corners), normalise.  On
+    the GPU (bf16) one libsvla kernel (svla_zoe_preprocess); other devices / dtypes run the stock ops."""
     ph, pw = 31, 31
+    if pixel_values.is_cuda and pixel_values.dtype == torch.bfloat16 and pad_mode == "reflect":
+        C = pixel_values.shape[1]  # mean / std as the bf16 values TF.normalize uses on a bf16 image
+        return (K.zoe_preprocess(pixel_values.contiguous(), ph, (384, 384),
+                                 [float(torch.tensor(v, dtype=torch.bfloat16)) for v in ZOE_MEAN[:C]],
+                                 [float(torch.tensor(v, dtype=torch.bfloat16)) for v in ZOE_STD[:C]]), ph, pw)
     images = F.pad(pixel_values, (pw, pw, ph, ph), mode=pad_mode)
     images = F.interpolate(images, size=(384, 384), mode="bicubic", align_corners=True)
     mean, std = _zoe_norm_consts(images.dtype, images.device)
@@ -225,6 +231,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         zoe_pv, ph, pw = process_zoe(pixel_values, pad_mode="reflect")
         pvh, pvw = pixel_values.shape[-2:]
         depth = self.vision_zoe_model(pixel_values=zoe_pv).predicted_depth
+        if depth.is_cuda and depth.dtype == torch.bfloat16:  # resize + crop in one kernel (svla_zoe_depth_resize)
+            return K.zoe_depth_resize(depth.contiguous(), ph, (pvh, pvw))
         depth = F.interpolate(depth.unsqueeze(1), size=(pvh + 2 * ph, pvw + 2 * pw), mode="bicubic",
                               align_corners=True)[..., ph:-ph, pw:-pw]
         return depth.contiguous()

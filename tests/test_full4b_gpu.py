@@ -327,6 +327,7 @@ def test_full4b_train_step_b32_adamw(model4b, cuda):
     optimizer step moves the shared model's weights away from the golden's."""
     from spatialvla_amd import presets
     from spatialvla_amd.engine import TrainEngine
+    model4b.__dict__.pop("predict_depth", None)  # an earlier test's golden-depth (B=1) override: run Zoe at B=32
     model4b.train()
     model4b.vision_zoe_model.eval()
     eng = TrainEngine(model4b, lr=2e-5, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0)

@@ -559,3 +559,40 @@ def test_output_attentions_vs_oracle(cuda):
     for a, r in zip(out.attentions, sink):
         assert a.shape == r.shape and a.dtype == torch.bfloat16
         assert H.rel_l2(a, r) < 2e-2
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_zoe_preprocess_and_depth_resize(cuda, variant):
+    """process_zoe (reference :99-110: reflect pad 31 -> bicubic 384^2 align_corners -> normalize) and the depth
+    resize + crop (:318-323) as single kernels against the stock torch ops on the same bf16 inputs.  Two contraction
+    forms of torch's bicubic expression are built (svla_diag_zoe_bicubic_variant); the product form (0) must agree
+    to one bf16 rounding everywhere, and the measured fraction of differing elements is printed and bounded."""
+    import torch.nn.functional as F
+    from spatialvla_amd import kernels as Kn, _lib as L
+    from spatialvla_amd.modeling_spatialvla import ZOE_MEAN, ZOE_STD
+    L.lib().svla_diag_zoe_bicubic_variant(variant)
+    try:
+        torch.manual_seed(3)
+        x = torch.rand(4, 3, 224, 224, device=cuda).to(torch.bfloat16)
+        got = Kn.zoe_preprocess(x, 31, (384, 384), [float(torch.tensor(v, dtype=torch.bfloat16)) for v in ZOE_MEAN],
+                                [float(torch.tensor(v, dtype=torch.bfloat16)) for v in ZOE_STD])
+        ref = F.interpolate(F.pad(x, (31, 31, 31, 31), mode="reflect"), size=(384, 384), mode="bicubic",
+                            align_corners=True)
+        mean = torch.tensor(ZOE_MEAN, dtype=torch.bfloat16, device=cuda).view(1, -1, 1, 1)
+        std = torch.tensor(ZOE_STD, dtype=torch.bfloat16, device=cuda).view(1, -1, 1, 1)
+        ref = (ref - mean) / std
+        d = (torch.rand(4, 384, 384, device=cuda) * 5 + 0.3).to(torch.bfloat16)
+        gd = Kn.zoe_depth_resize(d, 31, (224, 224))
+        rd = F.interpolate(d.unsqueeze(1), size=(286, 286), mode="bicubic", align_corners=True)[..., 31:-31, 31:-31]
+    finally:
+        L.lib().svla_diag_zoe_bicubic_variant(0)
+    # the interpolated values are rounded to bf16 once: a contraction-order difference moves a value by one bf16
+    # step of its magnitude, at most 2^-7 of the largest magnitude (depth: a step at 4..8 is 2^-5, 2^-7.4 of a 5.3
+    # maximum; preprocess outputs (v - 0.5) / 0.5 carry a step of v in [0.5, 1) as 2^-7 absolute, 2^-8 of range 2)
+    for name, a, b, scale in (("preprocess", got, ref, 2.0), ("depth", gd, rd, float(rd.float().abs().max()))):
+        diff = (a.float() != b.float()).float().mean().item()
+        dmax = ((a.float() - b.float()).abs().max() / scale).item()
+        print(f"zoe {name} variant {variant}: elements differing {diff:.3e}, max diff {dmax:.2e} of the value range")
+        assert a.shape == b.shape
+        if variant == 0:
+            assert dmax <= 2 ** -7 and diff <= 1e-2, (name, diff, dmax)

@@ -63,6 +63,14 @@ if [ -n "$FP8_PMC" ]; then
   done
   cat $O/fp8_runs.txt; grep -A16 "gemm4" $O/fp8_pmc_*.txt
 fi
+if [ -n "$GEGLU_AB" ]; then
+  step geglu_ab 300 python -u tools/geglu_ab.py $GEGLU_AB > $O/geglu_ab.txt 2>&1
+  cat $O/geglu_ab.txt
+fi
+if [ -n "$GEMM_BENCH" ]; then
+  step gemm_bench 400 python -u tools/gemm_bench.py > $O/gemm_bench.txt 2>&1
+  cat $O/gemm_bench.txt
+fi
 if [ -n "$BENCH" ]; then
   step bench 600 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err
   head -c 2500 $O/bench.json; echo
