@@ -50,8 +50,21 @@ __device__ __forceinline__ float softcap_bf16_tab(float v, float cap, float icap
 constexpr int TANH_TAB_BYTES = sizeof(svla_tanh_bf16_tab);
 static_assert(TANH_TAB_BYTES % 16 == 0, "table copied in 16-B pieces");
 
+// The GeGLU kernel's LDS copy of the gelu table (gelu_bf16_lut, svla_common.h): the direct epilogue looks up 128
+// elements per lane per 256 x 256 tile, where gelu_tanh's ~30 VALU and two transcendentals made it VALU-bound (one
+// wave per SIMD).
+constexpr int GELU_TAB_BYTES = sizeof(svla_gelu_bf16_tab);
+static_assert(GELU_TAB_BYTES % 16 == 0, "table copied in 16-B pieces");
+__device__ __forceinline__ void gelu_tab_to_lds(char* dst) {
+  for (int t = threadIdx.x; t < GELU_TAB_BYTES / 16; t += blockDim.x)
+    *(LDS_AS u32x4*)(dst + 16 * t) = reinterpret_cast<const u32x4*>(svla_gelu_bf16_tab)[t];
+}
+
 #ifndef G4_STAMPS
 #define G4_STAMPS 0
+#endif
+#ifndef G4_GELU_LUT
+#define G4_GELU_LUT 1
 #endif
 constexpr int BK = 64;
 constexpr int GROUP_M = 8;
@@ -245,7 +258,7 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         pre[j] = round_bf(v[j] + b[j]);
-        v[j] = gelu_tanh(pre[j]);
+        v[j] = gelu_bf16(pre[j]);
       }
       store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
       store8(cp, v, nv);
@@ -287,7 +300,7 @@ __device__ __forceinline__ void epi_chunk(const svla_epilogue& E, int kind, bf16
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float dh = round_bf(v[j]);
-        float act = round_bf(gelu_tanh(g[j]));
+        float act = gelu_bf16(g[j]);
         float dact = round_bf(dh * u[j]);
         du[j] = dh * act;
         dg[j] = dact * gelu_tanh_grad(g[j]);
@@ -351,7 +364,7 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
         for (int j = 0; j < 8; ++j) {
           g[it0][j] = round_bf(g[it0][j]);
           u[it0][j] = round_bf(u[it0][j]);
-          h[j] = round_bf(gelu_tanh(g[it0][j])) * u[it0][j];
+          h[j] = gelu_bf16(g[it0][j]) * u[it0][j];
         }
         store8(cbase + (m - cm0) * ldc + n, h, I - n);
         store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g[it0], I - n);
@@ -465,7 +478,7 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           pre[j] = round_bf(x[j] + b[j]);
-          x[j] = gelu_tanh(pre[j]);
+          x[j] = gelu_bf16(pre[j]);
         }
         store8((bf16_t*)E.out1 + m * E.ld_out1 + n, pre, nv);
         store8(cp, x, nv);
@@ -498,7 +511,7 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float dh = round_bf(x[j]);
-          const float act = round_bf(gelu_tanh(g[j]));
+          const float act = gelu_bf16(g[j]);
           const float dact = round_bf(dh * u[j]);
           du[j] = dh * act;
           dg[j] = dact * gelu_tanh_grad(g[j]);
@@ -598,7 +611,7 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           for (int j = 0; j < 8; ++j) {
             g[j] = round_bf(pg[j]);
             u[j] = round_bf(pu[j]);
-            h[j] = round_bf(gelu_tanh(g[j])) * u[j];
+            h[j] = gelu_bf16(g[j]) * u[j];
           }
           store8(cbase + (m - cm0) * Cd.ld + n, h, I - n);
           store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
@@ -1278,6 +1291,7 @@ constexpr int BM = 256, BN = 256, NTH = 256;
 constexpr int OPB = BM * BK * 2;  // bytes per operand image per buffer (32 KiB)
 constexpr int STAGE = 2 * OPB;    // A | B
 constexpr int LDS = 2 * STAGE;    // 128 KiB (the 66.5 KiB epilogue image reuses it)
+constexpr int LDS_GELU = LDS + GELU_TAB_BYTES;  // the GeGLU kernel: the gelu table behind the operand stages
 static_assert(64 * (BN + 4) * 4 + TANH_TAB_BYTES <= LDS, "epilogue image + tanh table must fit");
 static_assert(G4_RB1 >= 15 * G4_RS && G4_DA0 > G4_RB1 && G4_DB0 >= G4_DA0 + 8 * G4_DST &&
                   G4_RB2 >= G4_DB0 + 8 * G4_DST - 1 && G4_RB2 + 1 + 15 * G4_RS < 128,
@@ -1956,6 +1970,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       });
      } else {
       const int64_t ncol = (n0 >> 1) + 64 * wc + cofs;
+      const LDS_AS unsigned short* const gtab = (const LDS_AS unsigned short*)(smem + LDS);  // gelu_tab_to_lds
       static_for<0, 8>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const int64_t m = m0 + 128 * wr + 16 * i + r;
@@ -1965,20 +1980,29 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
           f32x4 gb = agpr_get<i * 8 + 4 * P_ + 2>(), ub = agpr_get<i * 8 + 4 * P_ + 3>();
           swap4(ga, gb);
           swap4(ua, ub);
-          float gv[8], uv[8], hv[8];
+          // g and u rounded to bf16 once, in their stored packed form; h = bf16(bf16(gelu(g)) u) (gelu_bf16_lut)
+          const u32x4 gp = {pack2(ga[0], ga[1]), pack2(ga[2], ga[3]), pack2(gb[0], gb[1]), pack2(gb[2], gb[3])};
+          const u32x4 up = {pack2(ua[0], ua[1]), pack2(ua[2], ua[3]), pack2(ub[0], ub[1]), pack2(ub[2], ub[3])};
+          u32x4 hp;
+#if !G4_GELU_LUT  // diagnostic A/B: the fp32 formula
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            hp[q] = pack2(round_bf(gelu_tanh(__uint_as_float(gp[q] << 16))) * __uint_as_float(up[q] << 16),
+                          round_bf(gelu_tanh(__uint_as_float(gp[q] & 0xffff0000u))) * __uint_as_float(up[q] & 0xffff0000u));
+#else
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            gv[q] = round_bf(ga[q]);
-            gv[4 + q] = round_bf(gb[q]);
-            uv[q] = round_bf(ua[q]);
-            uv[4 + q] = round_bf(ub[q]);
+            const float h0 = gelu_bf16_lut(gp[q] & 0xffffu, __uint_as_float(gp[q] << 16), gtab) *
+                             __uint_as_float(up[q] << 16);
+            const float h1 = gelu_bf16_lut(gp[q] >> 16, __uint_as_float(gp[q] & 0xffff0000u), gtab) *
+                             __uint_as_float(up[q] & 0xffff0000u);
+            hp[q] = pack2(h0, h1);
           }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) hv[q] = round_bf(gelu_tanh(gv[q])) * uv[q];
+#endif
           const int64_t n = ncol + 32 * P_;
-          *reinterpret_cast<u32x4*>(cbase + (m - cm0) * Cd.ld + n) = pack8(hv);
-          *reinterpret_cast<u32x4*>((bf16_t*)E.out1 + m * E.ld_out1 + n) = pack8(gv);
-          *reinterpret_cast<u32x4*>((bf16_t*)E.out2 + m * E.ld_out2 + n) = pack8(uv);
+          *reinterpret_cast<u32x4*>(cbase + (m - cm0) * Cd.ld + n) = hp;
+          *reinterpret_cast<u32x4*>((bf16_t*)E.out1 + m * E.ld_out1 + n) = gp;
+          *reinterpret_cast<u32x4*>((bf16_t*)E.out2 + m * E.ld_out2 + n) = up;
         });
       });
      }
@@ -2038,7 +2062,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #pragma unroll
               for (int q = 0; q < 8; ++q) {
                 bb[q] = round_bf(v[q] + bb[q]);  // pre-activation, saved for backward
-                v[q] = gelu_tanh(bb[q]);
+                v[q] = gelu_bf16(bb[q]);
               }
               *reinterpret_cast<u32x4*>((bf16_t*)E.out1 + m * E.ld_out1 + nb + 32 * p) = pack8(bb);
             } else if constexpr (KIND == SVLA_EPI_BIAS_RESID) {
@@ -2246,6 +2270,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   };
   int tile, kb, ke, st;
   bool have = next_item(tile, kb, ke, st), pre = false;
+  if constexpr (GG) {  // read by the direct GeGLU epilogue, after the first mainloop's barriers
+    if (E.kind == SVLA_EPI_GEGLU) gelu_tab_to_lds(smem + LDS);
+  }
 #pragma unroll 1
   while (have) {
     int t;
@@ -2509,7 +2536,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(int M, int64_t rows, int64_t 
         if (lane == 0 && n < rows) {
           if constexpr (GEGLU) {
             const float g = round_bf(v[0]), u = round_bf(v[1]);
-            c[m * ldc + n] = f2bf(round_bf(gelu_tanh(g)) * u);
+            c[m * ldc + n] = f2bf(gelu_bf16(g) * u);
             ((bf16_t*)E.out1)[m * E.ld_out1 + n] = f2bf(g);
             ((bf16_t*)E.out2)[m * E.ld_out2 + n] = f2bf(u);
           } else {
@@ -2765,7 +2792,7 @@ __global__ __launch_bounds__(256) void gemv_pf_kernel(int M, int64_t rows, int64
         if (lane == 0 && n < rows) {
           if constexpr (GEGLU) {
             const float g = round_bf(v[0]), u = round_bf(v[1]);
-            c[m * ldc + n] = f2bf(round_bf(gelu_tanh(g)) * u);
+            c[m * ldc + n] = f2bf(gelu_bf16(g) * u);
             ((bf16_t*)E.out1)[m * E.ld_out1 + n] = f2bf(g);
             ((bf16_t*)E.out2)[m * E.ld_out2 + n] = f2bf(u);
           } else {
@@ -2958,7 +2985,7 @@ __global__ __launch_bounds__(256) void gemv_norm2_kernel(int M, int64_t rows, in
       if (lane == 0) {
         if constexpr (GEGLU) {
           const float g = round_bf(v[0]), u = round_bf(v[1]);
-          c[m * ldc + r0] = f2bf(round_bf(gelu_tanh(g)) * u);
+          c[m * ldc + r0] = f2bf(gelu_bf16(g) * u);
           ((bf16_t*)E.out1)[m * E.ld_out1 + r0] = f2bf(g);
           ((bf16_t*)E.out2)[m * E.ld_out2 + r0] = f2bf(u);
         } else {
@@ -3117,10 +3144,11 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
       (E.kind == SVLA_EPI_ROPE && E.rope_D == 256 && la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC)) {
     static bool lds_set = false;
     if (!lds_set) {
-      (void)hipFuncSetAttribute((const void*)gemm4_kernel_00g, hipFuncAttributeMaxDynamicSharedMemorySize, p4::LDS);
+      (void)hipFuncSetAttribute((const void*)gemm4_kernel_00g, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                p4::LDS_GELU);
       lds_set = true;
     }
-    hipLaunchKernelGGL(gemm4_kernel_00g, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);
+    hipLaunchKernelGGL(gemm4_kernel_00g, grid, block, p4::LDS_GELU, s, M, N, K, A, B, Cd, E, sk);
     return svla::check_launch("gemm4 geglu");
   }
   if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH4(0, 0)

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, co
   unpack8(*reinterpret_cast<const u32x4*>(u + m * ldu + c), uv);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float act = round_bf(gelu_tanh(gv[j]));
+    const float act = gelu_bf16(gv[j]);
     const float dact = round_bf(d[j] * uv[j]);
     ou[j] = d[j] * act;
     og[j] = dact * gelu_tanh_grad(gv[j]);
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void gelu_rows_kernel(int64_t M, int64_t N, co
     for (int j = 0; j < 8; ++j) o[j] = v[j] * gelu_tanh_grad(p[j]);
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = MODE == 0 ? gelu_tanh(v[j]) : gelu_erf(v[j]);
+    for (int j = 0; j < 8; ++j) o[j] = MODE == 0 ? gelu_bf16(v[j]) : gelu_erf(v[j]);
   }
   *reinterpret_cast<u32x4*>(y + m * ldy + c) = pack8(o);
 }

@@ -7,6 +7,7 @@
 #include <stdio.h>
 
 #include "../../include/svla.h"
+#include "gelu_bf16_table.h"
 
 typedef uint16_t bf16_t;  // raw bf16 bits in global memory
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -80,6 +81,26 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
   return 0.5f * x * (1.0f + fast_tanh(u));
+}
+// bf16(gelu_tanh(g)) of a bf16 g (bits b in the low 16 bits, value gf): 2^-9 <= |g| < 8 from the table of
+// tools/gen_gelu_table.py (in LDS for the GeGLU GEMM's direct epilogue, in global memory elsewhere), |g| < 2^-9 ->
+// g / 2 (exact), g >= 8 -> g, g <= -8 -> -0, -inf / negative NaN -> NaN.  Bitwise the reference's fp32 op sequence
+// (gelu_pytorch_tanh on a bf16 tensor: fp32 0.5 g (1 + tanh(k0 (g + k1 g^3))), correctly rounded tanh, cast to
+// bf16) on all 65536 bf16 inputs, which the generator checks exhaustively; ~12 VALU and one 2-B load instead of
+// gelu_tanh's ~30 VALU and two transcendentals.  Every bf16-input GELU(tanh) of the library goes through it, so the
+// forward activation and the one the backward passes recompute are the same bits.
+template <typename TabPtr>
+__device__ __forceinline__ float gelu_bf16_lut(uint32_t b, float gf, TabPtr tab) {
+  const uint32_t a = b & 0x7fffu, s = b >> 15;
+  const uint32_t idx = a - (uint32_t)SVLA_GELU_TAB_LO;
+  const float tv =
+      __uint_as_float((uint32_t)tab[min(idx, (uint32_t)SVLA_GELU_TAB_N - 1u) + s * SVLA_GELU_TAB_N] << 16);
+  const float hi = s ? (a < 0x7f80u ? -0.0f : __uint_as_float(0x7fc00000u)) : gf;
+  return idx < (uint32_t)SVLA_GELU_TAB_N ? tv : (a < (uint32_t)SVLA_GELU_TAB_LO ? gf * 0.5f : hi);
+}
+// the same for a float holding a bf16 value, from the global-memory table
+__device__ __forceinline__ float gelu_bf16(float g) {
+  return gelu_bf16_lut(__float_as_uint(g) >> 16, g, svla_gelu_bf16_tab);
 }
 // torch GELU(approximate="none") in fp32: x/2 * (1 + erf(x / sqrt(2)))
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }

@@ -1018,3 +1018,49 @@ def test_gemm4_rope_paired_bitwise(cuda, M):
         rot = torch.cat([-seg[:, 128:], seg[:, :128]], -1)
         ref[:, 256 * h:256 * (h + 1)] = (seg * c).to(BF).float() + (rot * s).to(BF).float()
     assert rel_l2(outs[3], ref) < 5e-3
+
+
+def _gelu_lut(cuda):
+    """bf16 bits -> bf16 bits of the reference's gelu_tanh over all 65536 inputs (tools/gen_gelu_table.py's fp32 op
+    sequence with a correctly rounded tanh; the kernels' band table + closed-form bands equal it exhaustively)."""
+    import numpy as np
+    from tools.gen_gelu_table import gelu_ref_bits
+    lut = gelu_ref_bits(np.arange(65536, dtype=np.uint32)).astype(np.int32)
+    return torch.from_numpy(lut).to(cuda)
+
+
+def _apply_lut(lut, x):
+    idx = x.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
+    return (lut[idx.long()].to(torch.int16)).view(BF)
+
+
+@pytest.mark.parametrize("M", [2048, 2085])  # interior 256 x 256 tiles (direct epilogue) / a ragged last row block
+def test_geglu_gelu_table_bitwise(cuda, M):
+    """Every bf16-input GELU(tanh) goes through the gelu table (svla_common.h gelu_bf16_lut): the GeGLU GEMM (4-wave
+    direct epilogue from the LDS copy, LDS-path epilogue on edge tiles), the GEGLU_BWD recomputation of the
+    activation, svla_geglu_bwd and svla_gelu_rows are bitwise bf16(lut(g) * u) / lut(x) of their own bf16 inputs;
+    against torch's own F.gelu(approximate="tanh") (ROCm tanhf) the fraction of differing activations is printed and
+    bounded."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(21)
+    K, I = 512, 1024
+    lut = _gelu_lut(cuda)
+    x = _r(M, K)
+    wg, wu = _r(I, K, scale=0.12), _r(I, K, scale=0.12)
+    h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    Kn.linear_geglu_fwd(x, wg, wu, h, g, u)
+    act = _apply_lut(lut, g)
+    assert torch.equal(h, (act.float() * u.float()).to(BF))
+    theirs = F.gelu(g.float(), approximate="tanh").to(BF)
+    frac = (theirs != act).float().mean().item()
+    print(f"gelu table vs torch F.gelu(tanh) on {g.numel()} GEMM outputs: differing {frac:.2e}")
+    assert frac <= 1e-3
+    # backward: svla_geglu_bwd's du = bf16(dh * act) with the same act
+    dh = _r(M, I)
+    dg, du = torch.empty_like(g), torch.empty_like(g)
+    Kn.geglu_bwd(dh, g, u, dg, du)
+    assert torch.equal(du, (dh.float() * act.float()).to(BF))
+    # svla_gelu_rows mode 0
+    y = torch.empty_like(g)
+    Kn.gelu_rows(0, g, y)
+    assert torch.equal(y, act)

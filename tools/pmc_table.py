@@ -12,11 +12,11 @@ def main():
     vals = defaultdict(lambda: defaultdict(list))
     durs = {}
     for d in sys.argv[1:]:
-        for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]
                 vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        for f in glob.glob(os.path.join(d, "*kernel_stats.csv")):
+        for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 durs[r["Name"].replace("(anonymous namespace)::", "").split("(")[0][:70]] = float(r["AverageNs"]) / 1e3
     for k in sorted(set(vals) | set(durs)):

@@ -63,6 +63,16 @@ if [ -n "$FP8_PMC" ]; then
   done
   cat $O/fp8_runs.txt; grep -A16 "gemm4" $O/fp8_pmc_*.txt
 fi
+if [ -n "$ATT_PMC" ]; then
+  for spec in $ATT_PMC; do  # e.g. gemma2:fwd gemma2:bwd beit:fwd
+    shp=${spec%%:*}; what=${spec##*:}; d=/tmp/att_${shp}_${what}
+    step att_trace 120 rocprofv3 --kernel-trace --stats -d ${d}_t -o t --output-format csv -- python3 tools/attn_one.py $shp $what 10 > /dev/null 2>&1
+    step att_pmc1 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d ${d}_1 -o p1 --output-format csv -- python3 tools/attn_one.py $shp $what 10 > /dev/null 2>&1
+    step att_pmc2 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d ${d}_2 -o p2 --output-format csv -- python3 tools/attn_one.py $shp $what 10 > /dev/null 2>&1
+    python tools/pmc_table.py ${d}_t ${d}_1 ${d}_2 > $O/attn_pmc_${shp}_${what}.txt 2>&1
+    cat $O/attn_pmc_${shp}_${what}.txt
+  done
+fi
 if [ -n "$GEGLU_AB" ]; then
   step geglu_ab 300 python -u tools/geglu_ab.py $GEGLU_AB > $O/geglu_ab.txt 2>&1
   cat $O/geglu_ab.txt
