@@ -40,6 +40,44 @@ def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
+# Weight gradients on a side stream (SVLA_WGRAD_STREAM=0: all on the current stream).  A projection's weight-gradient
+# GEMM reads only dY and X, so it can run beside the input-gradient GEMM and whatever follows that on the main stream
+# (the attention backward, the GeGLU derivative pass).  The GEMMs run one workgroup per CU with a tile count that
+# rarely divides 256 (o dgrad: 312 tiles, the last round fills 56 CUs), so the second kernel takes the CUs the first
+# leaves idle.  Outputs are independent and every kernel's reduction order is fixed by its own tiling, so results are
+# bitwise those of the serial order.  Safe with the caching allocator: join() makes the main stream wait for the side
+# stream before the Function returns, i.e. before autograd frees any input the side stream reads.
+WGRAD_STREAM = [os.environ.get("SVLA_WGRAD_STREAM", "1") != "0"]
+_side_streams: dict = {}
+
+
+class _SideWork:
+    """run(fn): fn on the side stream, after everything issued on the main stream so far; join(): the main stream
+    waits for the side stream."""
+    __slots__ = ("on", "main", "side")
+
+    def __init__(self, like: torch.Tensor):
+        self.on = WGRAD_STREAM[0] and like.is_cuda and not torch.cuda.is_current_stream_capturing()
+        if self.on:
+            dev = like.device
+            self.main = torch.cuda.current_stream(dev)
+            s = _side_streams.get(dev)
+            if s is None:
+                s = _side_streams[dev] = torch.cuda.Stream(dev)
+            self.side = s
+
+    def run(self, fn):
+        if not self.on:
+            return fn()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            return fn()
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
 class ResidualSlot:
     """Hand-off of a residual-stream gradient between the two consumers of one tensor: the residual branch
     (add + post-norm, or a GEMM epilogue's residual input) and the pre-norm that reads the same tensor.  The
@@ -415,13 +453,15 @@ class GemmaAttentionFn(torch.autograd.Function):
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         dattn = _empty(M, qd, like=x)
         f8 = ctx.f8 if FP8_DGRAD[0] else None
+        # each weight gradient is queued on the side stream before the main-stream work it may overlap
+        side = _SideWork(x)
+        dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
+        if dwo is not None:
+            side.run(lambda: K.linear_wgrad(dout, attn, [dwo], accumulate=acc))
         if f8 is not None:
             _fp8_dgrad(dout, f8, "o", (wo,), dattn)
         else:
             K.linear_dgrad(dout, [wo], dattn)
-        dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
-        if dwo is not None:
-            K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
         dqkv = torch.empty_like(qkv)
         a = K.attn_args(cfg.B, cfg.L, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, kv_class, cfg.window,
@@ -429,23 +469,26 @@ class GemmaAttentionFn(torch.autograd.Function):
         ld = dqkv.stride(0)
         K.attn_bwd(a, attn, dattn, lse, dqkv[:, :qd], ld, dqkv[:, qd:qd + kd], ld, dqkv[:, qd + kd:], ld)
         dx = None
+        dests = [_grad_dest(w, ctx.needs_input_grad[1 + i]) for i, w in enumerate((wq, wk, wv))]
+
+        def qkv_wgrad():
+            if all(d[0] is not None for d in dests) and len({d[1] for d in dests}) == 1:
+                K.linear_wgrad(dqkv, x, [d[0] for d in dests], accumulate=dests[0][1])
+            else:
+                off = 0
+                for (dw, acc_i, _), w in zip(dests, (wq, wk, wv)):
+                    n = w.shape[0]
+                    if dw is not None:
+                        K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
+                    off += n
+        side.run(qkv_wgrad)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             if f8 is not None:
                 _fp8_dgrad(dqkv, f8, "qkv", (wq, wk, wv), dx)
             else:
                 K.linear_dgrad(dqkv, [wq, wk, wv], dx)
-        rets = []
-        dests = [_grad_dest(w, ctx.needs_input_grad[1 + i]) for i, w in enumerate((wq, wk, wv))]
-        if all(d[0] is not None for d in dests) and len({d[1] for d in dests}) == 1:
-            K.linear_wgrad(dqkv, x, [d[0] for d in dests], accumulate=dests[0][1])
-        else:
-            off = 0
-            for (dw, acc_i, _), w in zip(dests, (wq, wk, wv)):
-                n = w.shape[0]
-                if dw is not None:
-                    K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
-                off += n
+        side.join()
         rets = [d[2] for d in dests]
         return (dx, *rets, ret_wo, None, None, None, None, None, None)
 
@@ -578,9 +621,10 @@ class GemmaMLPFn(torch.autograd.Function):
         x, wg, wu, wd, g, u, h = ctx.saved_tensors
         dout = _c(dout)
         M, I = g.shape
+        side = _SideWork(x)
         dwd, acc, ret_wd = _grad_dest(wd, ctx.needs_input_grad[3])
         if dwd is not None:
-            K.linear_wgrad(dout, h, [dwd], accumulate=acc)
+            side.run(lambda: K.linear_wgrad(dout, h, [dwd], accumulate=acc))
         dgu = _empty(M, 2 * I, like=x)
         f8 = ctx.f8 if FP8_DGRAD[0] else None
         # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (in the down dgrad's epilogue
@@ -591,6 +635,18 @@ class GemmaMLPFn(torch.autograd.Function):
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
         K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+        dg_, accg, retg = _grad_dest(wg, ctx.needs_input_grad[1])
+        du_, accu, retu = _grad_dest(wu, ctx.needs_input_grad[2])
+
+        def gate_up_wgrad():
+            if dg_ is not None and du_ is not None and accg == accu:
+                K.linear_wgrad(dgu, x, [dg_, du_], accumulate=accg)
+            else:
+                if dg_ is not None:
+                    K.linear_wgrad(_c(dgu[:, :I]), x, [dg_], accumulate=accg)
+                if du_ is not None:
+                    K.linear_wgrad(_c(dgu[:, I:]), x, [du_], accumulate=accu)
+        side.run(gate_up_wgrad)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
@@ -598,15 +654,7 @@ class GemmaMLPFn(torch.autograd.Function):
                 _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx)
             else:
                 K.linear_dgrad(dgu, [wg, wu], dx)
-        dg_, accg, retg = _grad_dest(wg, ctx.needs_input_grad[1])
-        du_, accu, retu = _grad_dest(wu, ctx.needs_input_grad[2])
-        if dg_ is not None and du_ is not None and accg == accu:
-            K.linear_wgrad(dgu, x, [dg_, du_], accumulate=accg)
-        else:
-            if dg_ is not None:
-                K.linear_wgrad(_c(dgu[:, :I]), x, [dg_], accumulate=accg)
-            if du_ is not None:
-                K.linear_wgrad(_c(dgu[:, I:]), x, [du_], accumulate=accu)
+        side.join()
         return dx, retg, retu, ret_wd, None
 
 
@@ -652,41 +700,53 @@ class SiglipAttentionFn(torch.autograd.Function):
         M, Hd = x.shape
         nig = ctx.needs_input_grad
         dattn = torch.empty_like(attn)
-        K.linear_dgrad(dout, [wo], dattn)
+        # weight and bias gradients on the side stream (_SideWork), each queued before the main-stream work it may
+        # overlap; every gradient buffer is allocated here, on the main stream
+        side = _SideWork(x)
         dwo, acc, ret_wo = _grad_dest(wo, nig[8])
-        if dwo is not None:
-            K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
-        ret_bo = _bias_grad(dout, bo, nig[9])
+        dbo, accbo, ret_bo = _grad_dest(bo, nig[9])
+
+        def o_grads():
+            if dwo is not None:
+                K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
+            if dbo is not None:
+                K.colsum_bf16(dout, dbo, accumulate=accbo)
+        side.run(o_grads)
+        K.linear_dgrad(dout, [wo], dattn)
         dqkv = torch.empty_like(qkv)
         a = K.attn_args(cfg.B, cfg.L, cfg.H, cfg.H, cfg.D, qkv[:, :Hd], qkv.stride(0), qkv[:, Hd:2 * Hd],
                         qkv.stride(0), qkv[:, 2 * Hd:], qkv.stride(0), cfg.scale)
         ld = dqkv.stride(0)
         K.attn_bwd(a, attn, dattn, lse, dqkv[:, :Hd], ld, dqkv[:, Hd:2 * Hd], ld, dqkv[:, 2 * Hd:], ld)
-        dx = torch.empty_like(x) if nig[0] else None
-        if dx is not None:
-            K.linear_dgrad(dqkv, [wq, wk, wv], dx)
         rets = []
         dws = [_grad_dest(w, nig[2 + 2 * i]) for i, w in enumerate((wq, wk, wv))]
-        if all(d[0] is not None for d in dws) and len({d[1] for d in dws}) == 1:
-            # q, k and v weight gradients in one GEMM (C row segments): three 1152x1152 wgrads launched
-            # separately filled ~20 of the 256 CUs each
-            K.linear_wgrad(dqkv, x, [d[0] for d in dws], accumulate=dws[0][1])
-        else:
-            for i, (dw, accw, _r) in enumerate(dws):
-                if dw is not None:
-                    K.linear_wgrad(_c(dqkv[:, i * Hd:(i + 1) * Hd]), x, [dw], accumulate=accw)
         bds = [_grad_dest(b, nig[3 + 2 * i]) for i, b in enumerate((bq, bk, bv))]
         cat = None
         if all(d[0] is not None for d in bds) and len({d[1] for d in bds}) == 1:
             cat = _cat_views([d[0] for d in bds])
             if cat.data_ptr() != bds[0][0].data_ptr():  # not back to back (no engine flat buffer): a copy, unusable
                 cat = None
-        if cat is not None:  # the q|k|v bias gradients in one column sum over dqkv (engine: adjacent in the flat grad)
-            K.colsum_bf16(dqkv, cat, accumulate=bds[0][1])
-        else:
-            for i, (db, accb, _r) in enumerate(bds):
-                if db is not None:
-                    K.colsum_bf16(dqkv[:, i * Hd:(i + 1) * Hd], db, accumulate=accb)  # strided view, no copy
+
+        def qkv_grads():
+            if all(d[0] is not None for d in dws) and len({d[1] for d in dws}) == 1:
+                # q, k and v weight gradients in one GEMM (C row segments): three 1152x1152 wgrads launched
+                # separately filled ~20 of the 256 CUs each
+                K.linear_wgrad(dqkv, x, [d[0] for d in dws], accumulate=dws[0][1])
+            else:
+                for i, (dw, accw, _r) in enumerate(dws):
+                    if dw is not None:
+                        K.linear_wgrad(_c(dqkv[:, i * Hd:(i + 1) * Hd]), x, [dw], accumulate=accw)
+            if cat is not None:  # the q|k|v bias gradients in one column sum over dqkv (engine: adjacent in the flat grad)
+                K.colsum_bf16(dqkv, cat, accumulate=bds[0][1])
+            else:
+                for i, (db, accb, _r) in enumerate(bds):
+                    if db is not None:
+                        K.colsum_bf16(dqkv[:, i * Hd:(i + 1) * Hd], db, accumulate=accb)  # strided view, no copy
+        side.run(qkv_grads)
+        dx = torch.empty_like(x) if nig[0] else None
+        if dx is not None:
+            K.linear_dgrad(dqkv, [wq, wk, wv], dx)
+        side.join()
         for i in range(3):
             rets += [dws[i][2], bds[i][2]]
         dres = dout
@@ -728,23 +788,35 @@ class SiglipMLPFn(torch.autograd.Function):
         x, w1, b1, w2, b2, pre, act = ctx.saved_tensors
         dout = _c(dout)
         nig = ctx.needs_input_grad
+        side = _SideWork(x)  # weight / bias gradients beside the input-gradient chain (as SiglipAttentionFn)
         dw2, acc2, ret_w2 = _grad_dest(w2, nig[4])
-        if dw2 is not None:
-            K.linear_wgrad(dout, act, [dw2], accumulate=acc2)
-        ret_b2 = _bias_grad(dout, b2, nig[5])
+        db2, accb2, ret_b2 = _grad_dest(b2, nig[5])
+
+        def fc2_grads():
+            if dw2 is not None:
+                K.linear_wgrad(dout, act, [dw2], accumulate=acc2)
+            if db2 is not None:
+                K.colsum_bf16(dout, db2, accumulate=accb2)
+        side.run(fc2_grads)
         dpre = torch.empty_like(pre)
         if GELU_PASS[0]:
             K.linear_dgrad(dout, [w2], dpre)
             K.gelu_rows(K.GELU_TANH_BWD, dpre, dpre, pre=pre)
         else:
             K.linear_dgrad(dout, [w2], dpre, kind=L.EPI_GELU_BWD, in0=pre)
+        dw1, acc1, ret_w1 = _grad_dest(w1, nig[2])
+        db1, accb1, ret_b1 = _grad_dest(b1, nig[3])
+
+        def fc1_grads():
+            if dw1 is not None:
+                K.linear_wgrad(dpre, x, [dw1], accumulate=acc1)
+            if db1 is not None:
+                K.colsum_bf16(dpre, db1, accumulate=accb1)
+        side.run(fc1_grads)
         dx = torch.empty_like(x) if nig[0] else None
         if dx is not None:
             K.linear_dgrad(dpre, [w1], dx)
-        dw1, acc1, ret_w1 = _grad_dest(w1, nig[2])
-        if dw1 is not None:
-            K.linear_wgrad(dpre, x, [dw1], accumulate=acc1)
-        ret_b1 = _bias_grad(dpre, b1, nig[3])
+        side.join()
         dres = dout
         if ctx.slot is not None:  # handed to layer_norm2's backward (ResidualSlot)
             ctx.slot.put(dout)

@@ -66,15 +66,16 @@ def run(use_slot, iters=10):
 if len(sys.argv) > 2 and sys.argv[1] == "flag":
     from spatialvla_amd import modeling_gemma2 as MG
     from spatialvla_amd import kernels as Kn
-    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS}[sys.argv[2]]
-    gs = {}
+    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS, "wgrad_stream": Fn.WGRAD_STREAM}[sys.argv[2]]
+    gs, ws = {}, {}
     for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
         for mode in (0, 1):
             sw[0] = bool(mode)
             (f, t), gx = run(True)
             gs[mode] = gx
+            ws[mode] = flat_g.clone()
             print(f"{sys.argv[2]}={mode} fwd {f:.3f} ms  fwd+bwd {t:.3f} ms", flush=True)
-    print("x.grad bitwise equal:", torch.equal(gs[0], gs[1]))
+    print("x.grad bitwise equal:", torch.equal(gs[0], gs[1]), " weight grads bitwise equal:", torch.equal(ws[0], ws[1]))
     sys.exit(0)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 if len(sys.argv) > 2:  # profile mode: one configuration only (for rocprofv3 --kernel-trace)

@@ -25,6 +25,10 @@ if [ -n "$BLOCK_AB" ]; then
   step block_ab 300 python -u tools/block_lib_ab.py spatialvla_amd/libsvla.so $BLOCK_AB 5 > $O/block_ab.txt 2>&1
   cat $O/block_ab.txt
 fi
+if [ -n "$BLOCK_FLAG" ]; then
+  step block_flag 300 python -u tools/block_ab.py flag $BLOCK_FLAG 6 > $O/block_flag.txt 2>&1
+  cat $O/block_flag.txt
+fi
 if [ -n "$MXDBG" ]; then
   step mxdbg 120 python -u tools/mx_debug.py > $O/mx_debug.txt 2>&1
   cat $O/mx_debug.txt
