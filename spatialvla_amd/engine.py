@@ -33,6 +33,7 @@ import re
 import torch
 import torch.distributed as dist
 
+from . import functional as Fn
 from . import kernels as K
 
 BF16 = torch.bfloat16
@@ -120,6 +121,7 @@ class ZeroExchange:
         end = self.ready_end.get(point)
         if end is None or self.world == 1:
             return
+        Fn.join_side_work()  # weight gradients still running on the side stream (functional._SideWork)
         for b, (s, e) in enumerate(self.buckets):
             if e <= end and b not in self._rs:
                 self._reduce_scatter(b)

@@ -45,19 +45,35 @@ def _c(t):
 # (the attention backward, the GeGLU derivative pass).  The GEMMs run one workgroup per CU with a tile count that
 # rarely divides 256 (o dgrad: 312 tiles, the last round fills 56 CUs), so the second kernel takes the CUs the first
 # leaves idle.  Outputs are independent and every kernel's reduction order is fixed by its own tiling, so results are
-# bitwise those of the serial order.  Safe with the caching allocator: join() makes the main stream wait for the side
-# stream before the Function returns, i.e. before autograd frees any input the side stream reads.
+# bitwise those of the serial order.
+# When every weight gradient of a Function goes to the engine's flat buffer (nothing returned to autograd), the main
+# stream does not wait for the side stream at the Function's end (SVLA_WGRAD_DEFER=0: it does): the side work keeps
+# overlapping the next layers' backward.  The tensors it reads are marked with record_stream, so the caching allocator
+# does not hand their memory out again before the side stream has read them, and the main stream waits for the side
+# stream at the end of the backward pass (an autograd engine callback) and wherever the engine hands gradients to
+# a collective (join_side_work, TrainEngine's bucket hooks).
 WGRAD_STREAM = [os.environ.get("SVLA_WGRAD_STREAM", "1") != "0"]
+WGRAD_DEFER = [os.environ.get("SVLA_WGRAD_DEFER", "1") != "0"]
 _side_streams: dict = {}
+_join_queued: dict = {}  # device -> main stream the end-of-backward callback will make wait
+
+
+def join_side_work():
+    """Make the stream that queued side-stream weight gradients wait for all of them."""
+    for dev, main in list(_join_queued.items()):
+        main.wait_stream(_side_streams[dev])
+        del _join_queued[dev]
 
 
 class _SideWork:
-    """run(fn): fn on the side stream, after everything issued on the main stream so far; join(): the main stream
-    waits for the side stream."""
-    __slots__ = ("on", "main", "side")
+    """run(fn, *reads): fn on the side stream, after everything issued on the main stream so far (reads: the tensors
+    fn reads); join(*returned): the main stream waits for the side stream now, or -- when no returned gradient buffer
+    is given and deferral is on -- at the end of the backward pass."""
+    __slots__ = ("on", "main", "side", "reads")
 
     def __init__(self, like: torch.Tensor):
         self.on = WGRAD_STREAM[0] and like.is_cuda and not torch.cuda.is_current_stream_capturing()
+        self.reads = []
         if self.on:
             dev = like.device
             self.main = torch.cuda.current_stream(dev)
@@ -66,16 +82,27 @@ class _SideWork:
                 s = _side_streams[dev] = torch.cuda.Stream(dev)
             self.side = s
 
-    def run(self, fn):
+    def run(self, fn, *reads):
         if not self.on:
             return fn()
         self.side.wait_stream(self.main)
+        self.reads.extend(reads)
         with torch.cuda.stream(self.side):
             return fn()
 
-    def join(self):
-        if self.on:
+    def join(self, *returned):
+        if not self.on:
+            return
+        if not WGRAD_DEFER[0] or any(r is not None for r in returned):
             self.main.wait_stream(self.side)
+            return
+        for t in self.reads:
+            if t is not None:
+                t.record_stream(self.side)
+        dev = self.main.device
+        if dev not in _join_queued:
+            _join_queued[dev] = self.main
+            torch.autograd.Variable._execution_engine.queue_callback(join_side_work)
 
 
 class ResidualSlot:
@@ -457,7 +484,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         side = _SideWork(x)
         dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
         if dwo is not None:
-            side.run(lambda: K.linear_wgrad(dout, attn, [dwo], accumulate=acc))
+            side.run(lambda: K.linear_wgrad(dout, attn, [dwo], accumulate=acc), dout, attn)
         if f8 is not None:
             _fp8_dgrad(dout, f8, "o", (wo,), dattn)
         else:
@@ -481,15 +508,15 @@ class GemmaAttentionFn(torch.autograd.Function):
                     if dw is not None:
                         K.linear_wgrad(_c(dqkv[:, off:off + n]), x, [dw], accumulate=acc_i)
                     off += n
-        side.run(qkv_wgrad)
+        side.run(qkv_wgrad, dqkv, x)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             if f8 is not None:
                 _fp8_dgrad(dqkv, f8, "qkv", (wq, wk, wv), dx)
             else:
                 K.linear_dgrad(dqkv, [wq, wk, wv], dx)
-        side.join()
         rets = [d[2] for d in dests]
+        side.join(*rets, ret_wo)
         return (dx, *rets, ret_wo, None, None, None, None, None, None)
 
 
@@ -624,7 +651,7 @@ class GemmaMLPFn(torch.autograd.Function):
         side = _SideWork(x)
         dwd, acc, ret_wd = _grad_dest(wd, ctx.needs_input_grad[3])
         if dwd is not None:
-            side.run(lambda: K.linear_wgrad(dout, h, [dwd], accumulate=acc))
+            side.run(lambda: K.linear_wgrad(dout, h, [dwd], accumulate=acc), dout, h)
         dgu = _empty(M, 2 * I, like=x)
         f8 = ctx.f8 if FP8_DGRAD[0] else None
         # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (in the down dgrad's epilogue
@@ -646,7 +673,7 @@ class GemmaMLPFn(torch.autograd.Function):
                     K.linear_wgrad(_c(dgu[:, :I]), x, [dg_], accumulate=accg)
                 if du_ is not None:
                     K.linear_wgrad(_c(dgu[:, I:]), x, [du_], accumulate=accu)
-        side.run(gate_up_wgrad)
+        side.run(gate_up_wgrad, dgu, x)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
@@ -654,7 +681,7 @@ class GemmaMLPFn(torch.autograd.Function):
                 _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx)
             else:
                 K.linear_dgrad(dgu, [wg, wu], dx)
-        side.join()
+        side.join(retg, retu, ret_wd)
         return dx, retg, retu, ret_wd, None
 
 
@@ -711,7 +738,7 @@ class SiglipAttentionFn(torch.autograd.Function):
                 K.linear_wgrad(dout, attn, [dwo], accumulate=acc)
             if dbo is not None:
                 K.colsum_bf16(dout, dbo, accumulate=accbo)
-        side.run(o_grads)
+        side.run(o_grads, dout, attn)
         K.linear_dgrad(dout, [wo], dattn)
         dqkv = torch.empty_like(qkv)
         a = K.attn_args(cfg.B, cfg.L, cfg.H, cfg.H, cfg.D, qkv[:, :Hd], qkv.stride(0), qkv[:, Hd:2 * Hd],
@@ -742,13 +769,13 @@ class SiglipAttentionFn(torch.autograd.Function):
                 for i, (db, accb, _r) in enumerate(bds):
                     if db is not None:
                         K.colsum_bf16(dqkv[:, i * Hd:(i + 1) * Hd], db, accumulate=accb)  # strided view, no copy
-        side.run(qkv_grads)
+        side.run(qkv_grads, dqkv, x)
         dx = torch.empty_like(x) if nig[0] else None
         if dx is not None:
             K.linear_dgrad(dqkv, [wq, wk, wv], dx)
-        side.join()
         for i in range(3):
             rets += [dws[i][2], bds[i][2]]
+        side.join(*rets, ret_wo, ret_bo)
         dres = dout
         if ctx.slot is not None:  # handed to layer_norm1's backward (ResidualSlot)
             ctx.slot.put(dout)
@@ -797,7 +824,7 @@ class SiglipMLPFn(torch.autograd.Function):
                 K.linear_wgrad(dout, act, [dw2], accumulate=acc2)
             if db2 is not None:
                 K.colsum_bf16(dout, db2, accumulate=accb2)
-        side.run(fc2_grads)
+        side.run(fc2_grads, dout, act)
         dpre = torch.empty_like(pre)
         if GELU_PASS[0]:
             K.linear_dgrad(dout, [w2], dpre)
@@ -812,11 +839,11 @@ class SiglipMLPFn(torch.autograd.Function):
                 K.linear_wgrad(dpre, x, [dw1], accumulate=acc1)
             if db1 is not None:
                 K.colsum_bf16(dpre, db1, accumulate=accb1)
-        side.run(fc1_grads)
+        side.run(fc1_grads, dpre, x)
         dx = torch.empty_like(x) if nig[0] else None
         if dx is not None:
             K.linear_dgrad(dpre, [w1], dx)
-        side.join()
+        side.join(ret_w1, ret_b1, ret_w2, ret_b2)
         dres = dout
         if ctx.slot is not None:  # handed to layer_norm2's backward (ResidualSlot)
             ctx.slot.put(dout)

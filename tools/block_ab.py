@@ -66,7 +66,7 @@ def run(use_slot, iters=10):
 if len(sys.argv) > 2 and sys.argv[1] == "flag":
     from spatialvla_amd import modeling_gemma2 as MG
     from spatialvla_amd import kernels as Kn
-    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS, "wgrad_stream": Fn.WGRAD_STREAM}[sys.argv[2]]
+    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS, "wgrad_stream": Fn.WGRAD_STREAM, "wgrad_defer": Fn.WGRAD_DEFER}[sys.argv[2]]
     gs, ws = {}, {}
     for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
         for mode in (0, 1):
