@@ -1327,21 +1327,24 @@ struct Op4 {
 //      holds rows r and r + 8, which the r & 7 swizzle puts on one 16-B slot of the bank row (2-way: 45 % of the
 //      fp8 kernel's LDS cycles were conflict cycles, r5d PMC); (r >> 1) & 7 spreads the group over all 16 slots.
 //      (r >> 1) & 7 of piece n's rows is (4 n + (lane >> 4)) & 7: two voffset variants, even and odd pieces.
-template <int LAYOUT, bool FSW = false>
+template <int LAYOUT, bool FSW = false, int BMX = 256>
 __device__ __forceinline__ void op4_setup(const svla_operand& op, int64_t r0, int64_t rv, int w, int lane,
                                           Op4<LAYOUT>& st) {
+  static_assert(BMX == 256 || (LAYOUT == SVLA_LAYOUT_KC && !FSW), "192-row tiles: bf16 KC operands only");
+  constexpr int PPW = BMX / 32, HALF = BMX / 2;  // pieces per wave, rows per wave pair
   const int64_t ldb = op.ld * 2;
   if (LAYOUT == SVLA_LAYOUT_KC) {
     const int gc = FSW ? (lane & 7) ^ (lane >> 4) : (lane & 7) ^ (lane >> 3);  // row & 7 == lane >> 3
     const int gc1 = FSW ? (lane & 7) ^ (4 + (lane >> 4)) : gc;
     st.kq = gc * 8;
     st.kq1 = gc1 * 8;
-    const int row = 64 * w + (lane >> 3);
-    const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + (row & 127) : r0 + row;
+    const int row = 8 * PPW * w + (lane >> 3);
+    const int rh = row - HALF * (w >> 1);  // row inside the wave pair's half (op4_base)
+    const int64_t grow = (op.seg_dim == SVLA_SEG_GEGLU) ? (r0 >> 1) + rh : r0 + row;
     const int64_t nv = (rv - grow + 7) / 8;
-    st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, 8);
-    st.v0 = (uint32_t)((row & 127) * ldb + gc * 16);
-    st.v1 = (uint32_t)((row & 127) * ldb + gc1 * 16);
+    st.nvalid = grow >= rv ? 0 : (int)min<int64_t>(nv, PPW);
+    st.v0 = (uint32_t)(rh * ldb + gc * 16);
+    st.v1 = (uint32_t)(rh * ldb + gc1 * 16);
     st.ok0 = st.ok1 = true;
     st.rs = __builtin_amdgcn_readfirstlane((uint32_t)(8 * ldb));
   } else {
@@ -1375,18 +1378,19 @@ __device__ __forceinline__ uint32_t op4_voff(const Op4<SVLA_LAYOUT_RC>& st, int 
 #ifndef G4_AUX
 #define G4_AUX 0  // cache-policy bits of the operand LDS-DMA (1 sc0, 2 nt, 16 sc1)
 #endif
-__device__ __forceinline__ void op4_piece(const char* kbase, uint32_t voff, uint32_t soff, int n, char* img, int w) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(kbase), (LDS_AS void*)(img + (8 * w + n) * 1024), 16, voff, soff,
-                                           0, G4_AUX);
+__device__ __forceinline__ void op4_piece(const char* kbase, uint32_t voff, uint32_t soff, int n, char* img, int w,
+                                          int ppw = 8) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(kbase), (LDS_AS void*)(img + (ppw * w + n) * 1024), 16, voff,
+                                           soff, 0, G4_AUX);
 }
 
 // base address of the wave's 128-outer half of the operand tile at k = 0 (GEGLU: half 0 = gate, 1 = up tensor)
-template <int LAYOUT>
+template <int LAYOUT, int BMX = 256>
 __device__ __forceinline__ const char* op4_base(const svla_operand& op, int64_t r0, int half) {
   if (LAYOUT == SVLA_LAYOUT_KC && op.seg_dim == SVLA_SEG_GEGLU)
     return (const char*)((const bf16_t*)op.ptr[half] + (r0 >> 1) * op.ld);
   int64_t rb = 0;
-  const int64_t rh = r0 + 128 * half;
+  const int64_t rh = r0 + (BMX / 2) * half;
   const bf16_t* p = seg_ptr(op, rh, rb);
   return (const char*)(p + (rh - rb) * (LAYOUT == SVLA_LAYOUT_KC ? op.ld : 1));
 }
@@ -1570,16 +1574,29 @@ static_assert(F8_RB2 - F8_P0 == F8_NPRE && f8_piece(F8_RB2 + 3) == 15 && F8_RB2 
 // The kernel body is a __device__ function template wrapped by four plain kernels: the lambdas of a __global__
 // template are also instantiated for the host, where the device-only helpers they call fail to substitute and
 // the kernel stub silently disappears.
-template <int LA, int LB, bool F8 = false, bool GG = false, bool MX = false>
+// BMX: tile rows, 256 or 192 (RA = BMX / 32 A fragments and LDS-DMA pieces a wave; 192: bf16, KC A, data-parallel,
+// direct-epilogue kinds on whole tiles only -- launch4's choice for grids that 256-row tiles quantise badly)
+template <int LA, int LB, bool F8 = false, bool GG = false, bool MX = false, int BMX = 256>
 __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, const svla_operand& A,
                                            const svla_operand& B, const CDesc& Cd, const svla_epilogue& E,
                                            const SKArgs& sk, const F8Scales& fs) {
   using namespace p4;
+  static_assert(BMX == 256 || (BMX == 192 && !F8 && !GG && LA == SVLA_LAYOUT_KC), "192-row tiles: bf16, KC A");
+  constexpr int RA = BMX / 32, HALF = BMX / 2;  // A fragments (and A pieces) a wave; rows of a wave row
+  constexpr int NS = 16 * RA;                   // MFMA slots of a k-tile (two k-halves of RA x 8)
+  // k-tile schedule (slots): F1 reads 0 .. RA + 7, RB1, A pieces from DA0, B pieces from DB0 (every G4_DST), RB2,
+  // then the RA + 8 F0 reads of the next k-tile; the 256-row values are the tuned G4_* knobs
+  constexpr int S_RB1 = BMX == 256 ? G4_RB1 : 19, S_DA0 = BMX == 256 ? G4_DA0 : 21;
+  constexpr int S_DB0 = BMX == 256 ? G4_DB0 : S_DA0 + RA * G4_DST;
+  constexpr int S_RB2 = BMX == 256 ? G4_RB2 : S_DB0 + 8 * G4_DST - 1;
+  static_assert(S_RB1 >= (RA + 7) * G4_RS && S_DA0 > S_RB1 && S_DB0 >= S_DA0 + RA * G4_DST &&
+                    S_RB2 >= S_DB0 + 8 * G4_DST - 1 && S_RB2 + 1 + (RA + 7) * G4_RS < NS,
+                "gemm4 k-tile schedule out of order");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t_in = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(t_in >> 6);
   const int wr = w >> 1, wc = w & 1;
-  const int tiles_n = (int)((N + BN - 1) / BN), tiles_m = (int)((M + BM - 1) / BM);
+  const int tiles_n = (int)((N + BN - 1) / BN), tiles_m = (int)((M + BMX - 1) / BMX);
   const int L = xcd_remap(blockIdx.x, sk.grid);
   const int nk = sk.nk;
   const int64_t rvA = A.r_valid > 0 ? A.r_valid : M;
@@ -1591,7 +1608,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     const int group = G4_GROUP_M * tiles_n;
     const int first_m = (tile / group) * G4_GROUP_M;
     const int gsz = min(tiles_m - first_m, G4_GROUP_M);
-    m0 = (int64_t)(first_m + (tile % group) % gsz) * BM;
+    m0 = (int64_t)(first_m + (tile % group) % gsz) * BMX;
     n0 = (int64_t)((tile % group) / gsz) * BN;
   };
 
@@ -1615,9 +1632,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
   // piece n of the wave for the k-tile at krem = valid k extent left (KC: per-lane chunk check, RC: k-row check)
   // (the LDS-DMA itself lives in a __device__ function: lambdas of a kernel template are instantiated for the
   // host too, where the address-space cast would be a substitution failure and the kernel stub would vanish)
-  auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w); };
+  auto pieceA = [&](const char* ka, int64_t krem, int n, char* img) { op4_piece(ka, op4_voff(sa, n, krem), n * sa.rs, n, img, w, RA); };
   auto pieceB = [&](const char* kb_, int64_t krem, int n, char* img) { op4_piece(kb_, op4_voff(sb, n, krem), n * sb.rs, n, img, w); };
-  auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w); };
+  auto pieceA_full = [&](const char* ka, int n, char* img) { op4_piece(ka, vfa[n], n * sa.rs, n, img, w, RA); };
   auto pieceB_full = [&](const char* kb_, int n, char* img) { op4_piece(kb_, vfb[n], n * sb.rs, n, img, w); };
   // MX: each wave stages the E8M0 scales of its 64 image rows of A and of B for a k-tile (two 4-B-per-lane LDS-DMA
   // instructions of 256 B) into the k-tile's 2 KiB scale region behind the two operand stages (row i of an image at
@@ -1637,15 +1654,15 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     const char* const ka = abase + k0 * ksa;
     const char* const kbb = bbase + k0 * ksb;
 #pragma unroll
-    for (int n = 0; n < 8; ++n) pieceA(ka, kvA - k0, n, stage);
+    for (int n = 0; n < RA; ++n) pieceA(ka, kvA - k0, n, stage);
 #pragma unroll
     for (int n = 0; n < 8; ++n) pieceB(kbb, kvB - k0, n, stage + OPB);
     if constexpr (MX) mx_pieces(kt, stage == smem ? 0 : 1);
   };
   auto stage_first = [&](int64_t m0, int64_t n0, int kb, int ke, const int lane) {
-    op4_setup<LA, F8>(A, m0, rvA, w, lane, sa);
+    op4_setup<LA, F8, BMX>(A, m0, rvA, w, lane, sa);
     op4_setup<LB, F8>(B, n0, rvB, w, lane, sb);
-    abase = op4_base<LA>(A, m0, w >> 1);
+    abase = op4_base<LA, BMX>(A, m0, w >> 1);
     bbase = op4_base<LB>(B, n0, w >> 1);
     if constexpr (MX) {
       const int i = 64 * w + lane;  // image row staged by this lane
@@ -1675,6 +1692,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       stage_first(m0, n0, kb, ke, lane);
       if (nq > 1) {
         if constexpr (MX) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");  // 16 operand + 2 scale pieces a k-tile
+        else if constexpr (BMX == 192) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");  // 6 + 8 pieces a k-tile
         else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1804,7 +1822,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
       else frag4_load<LB>(f, img, 128 * wc, j, ks, lane);
     };
 #pragma unroll
-    for (int i = 0; i < 8; ++i) frag4_load<LA>(f0a[i], smem, 128 * wr, i, 0, lane);
+    for (int i = 0; i < RA; ++i) frag4_load<LA>(f0a[i], smem, HALF * wr, i, 0, lane);
 #pragma unroll
     for (int j = 0; j < 8; ++j) loadB(f0b[j], smem + OPB, j, 0);
 
@@ -1827,17 +1845,17 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #endif
       __builtin_amdgcn_sched_barrier(0);
       if (G4_PRIO) __builtin_amdgcn_s_setprio(3);
-      static_for<0, 128>([&](auto XC) {
+      static_for<0, NS>([&](auto XC) {
         constexpr int x = decltype(XC)::value;
-        constexpr int y = x & 63, ii = y >> 3, jj = y & 7;
+        constexpr int y = x % (NS / 2), ii = y >> 3, jj = y & 7;
         // swapped operands: quad (ii, jj) accumulates C^T, so a lane holds 4 consecutive columns of one row
-        if constexpr (x < 64) agpr_mfma<ii * 8 + jj>(f0b[jj].get(), f0a[ii].get());
+        if constexpr (x < NS / 2) agpr_mfma<ii * 8 + jj>(f0b[jj].get(), f0a[ii].get());
         else agpr_mfma<ii * 8 + jj>(f1b[jj].get(), f1a[ii].get());
         if constexpr (G4_ABL & 2) {
-        } else if constexpr (x % G4_RS == 0 && x / G4_RS < 8) frag4_load<LA>(f1a[x / G4_RS], cur, 128 * wr, x / G4_RS, 1, lane);
-        else if constexpr (x % G4_RS == 0 && x / G4_RS < 16)
-          loadB(f1b[x / G4_RS - 8], cur + OPB, x / G4_RS - 8, 1);
-        if constexpr (x == G4_RB1) {
+        } else if constexpr (x % G4_RS == 0 && x / G4_RS < RA) frag4_load<LA>(f1a[x / G4_RS], cur, HALF * wr, x / G4_RS, 1, lane);
+        else if constexpr (x % G4_RS == 0 && x / G4_RS < RA + 8)
+          loadB(f1b[x / G4_RS - RA], cur + OPB, x / G4_RS - RA, 1);
+        if constexpr (x == S_RB1) {
 #if G4_STAMPS
           unsigned long long t1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1848,32 +1866,36 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
 #endif
         }
         if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) {
-          if constexpr (x >= G4_DA0 && x < G4_DA0 + 8 * G4_DST && (x - G4_DA0) % G4_DST == 0) {
-            if constexpr (decltype(FULLK)::value) pieceA_full(rsa, (x - G4_DA0) / G4_DST, cur);
-            else pieceA(rsa, kvA - k2, (x - G4_DA0) / G4_DST, cur);
+          if constexpr (x >= S_DA0 && x < S_DA0 + RA * G4_DST && (x - S_DA0) % G4_DST == 0) {
+            if constexpr (decltype(FULLK)::value) pieceA_full(rsa, (x - S_DA0) / G4_DST, cur);
+            else pieceA(rsa, kvA - k2, (x - S_DA0) / G4_DST, cur);
           }
-          if constexpr (x >= G4_DB0 && x < G4_DB0 + 8 * G4_DST && (x - G4_DB0) % G4_DST == 0) {
-            if constexpr (decltype(FULLK)::value) pieceB_full(rsb, (x - G4_DB0) / G4_DST, cur + OPB);
-            else pieceB(rsb, kvB - k2, (x - G4_DB0) / G4_DST, cur + OPB);
+          if constexpr (x >= S_DB0 && x < S_DB0 + 8 * G4_DST && (x - S_DB0) % G4_DST == 0) {
+            if constexpr (decltype(FULLK)::value) pieceB_full(rsb, (x - S_DB0) / G4_DST, cur + OPB);
+            else pieceB(rsb, kvB - k2, (x - S_DB0) / G4_DST, cur + OPB);
           }
         }
         if constexpr (decltype(NEXT)::value) {
-          if constexpr (x == G4_RB2) {
+          if constexpr (x == S_RB2) {
 #if G4_STAMPS
             unsigned long long t2 = __builtin_amdgcn_s_memtime();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
-            if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (decltype(DMA)::value && !(G4_ABL & 1)) {
+              if constexpr (BMX == 192) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+              else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            } else {
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             if constexpr (!(G4_ABL & 4)) __builtin_amdgcn_s_barrier();
 #if G4_STAMPS
             stmp[2] += __builtin_amdgcn_s_memtime() - t2;
 #endif
           }
-          constexpr int r0 = x - G4_RB2 - 1;
+          constexpr int r0 = x - S_RB2 - 1;
           constexpr int r = (r0 >= 0 && r0 % G4_RS == 0 && !(G4_ABL & 2)) ? r0 / G4_RS : -1;
-          if constexpr (r >= 0 && r < 8) frag4_load<LA>(f0a[r], nxt, 128 * wr, r, 0, lane);
-          else if constexpr (r >= 8 && r < 16) loadB(f0b[r - 8], nxt + OPB, r - 8, 0);
+          if constexpr (r >= 0 && r < RA) frag4_load<LA>(f0a[r], nxt, HALF * wr, r, 0, lane);
+          else if constexpr (r >= RA && r < RA + 8) loadB(f0b[r - RA], nxt + OPB, r - RA, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
@@ -1909,7 +1931,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     const int kind = E.kind;
     if (!(kind == SVLA_EPI_STORE || (GG && (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE)))) return false;
     if (GG && kind == SVLA_EPI_STORE) return false;  // the paired kernel runs GEGLU and head-256 ROPE only
-    if (m0 + BM > M || n0 + BN > N) return false;
+    if (m0 + BMX > M || n0 + BN > N) return false;
     int cs = 0;
 #pragma unroll
     for (int i = 1; i < 4; ++i)
@@ -2026,9 +2048,9 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         }
         const LDS_AS unsigned short* ltab = (const LDS_AS unsigned short*)smem;
         const float cap = E.cap, icap = 1.0f / E.cap;
-        static_for<0, 8>([&](auto I) {
+        static_for<0, RA>([&](auto I) {
           constexpr int i = decltype(I)::value;
-          const int64_t m = m0 + 128 * wr + 16 * i + r;
+          const int64_t m = m0 + HALF * wr + 16 * i + r;
           bf16_t* const rowp = cbase + (m - cm0) * Cd.ld + nb;
           u32x4 old[4];
           if (HAS_IN0 || (KIND == SVLA_EPI_STORE && acc)) {  // the row block's four chunks in flight at once
@@ -2153,6 +2175,10 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
         else rows(std::integral_constant<int, 0>{});
       }
     };
+    if constexpr (BMX != 256) {  // whole tiles of direct-epilogue kinds only (launch4 checks)
+      direct_epilogue(m0, n0, lane);
+      return;
+    }
     if constexpr (!F8) {
       if (direct_epilogue(m0, n0, lane)) return;
     }
@@ -2266,7 +2292,7 @@ __device__ __forceinline__ void gemm4_body(int64_t M, int64_t N, int64_t K, cons
     if constexpr (F8) return false;
     const int kind = E.kind;
     const bool k_ok = GG ? (kind == SVLA_EPI_GEGLU || kind == SVLA_EPI_ROPE) : kind == SVLA_EPI_STORE;
-    return k_ok && m0 + BM <= M && n0 + BN <= N;
+    return k_ok && m0 + BMX <= M && n0 + BN <= N;
   };
   int tile, kb, ke, st;
   bool have = next_item(tile, kb, ke, st), pre = false;
@@ -2391,6 +2417,15 @@ SVLA_GEMM4_KERNEL(0, 1)
 SVLA_GEMM4_KERNEL(1, 0)
 SVLA_GEMM4_KERNEL(1, 1)
 #undef SVLA_GEMM4_KERNEL
+// 192-row tiles (KC A and B): the o and down projections, whose 256-row grids leave most of a last round idle
+// (9984 rows: 39 x 9 = 351 tiles on 256 CUs -> 52 x 9 = 468)
+#define SVLA_GEMM4_KERNEL192(LB_)                                                                           \
+  __global__ __launch_bounds__(256, 1) void gemm4_kernel_0##LB_##_192(                                       \
+      int64_t M, int64_t N, int64_t K, svla_operand A, svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) { \
+    gemm4_body<SVLA_LAYOUT_KC, LB_, false, false, false, 192>(M, N, K, A, B, Cd, E, sk, F8Scales{});        \
+  }
+SVLA_GEMM4_KERNEL192(0)
+#undef SVLA_GEMM4_KERNEL192
 // Gemma2 gate|up: B fragments paired gate/up per output block, GeGLU straight from the accumulators
 __global__ __launch_bounds__(256, 1) void gemm4_kernel_00g(int64_t M, int64_t N, int64_t K, svla_operand A,
                                                            svla_operand B, CDesc Cd, svla_epilogue E, SKArgs sk) {
@@ -3077,8 +3112,51 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   return svla::check_launch("gemm8");
 }
 
+#ifndef G4_192
+#define G4_192 1  // diagnostic builds: 0 = never the 192-row tiles
+#endif
+// fraction of the CU-rounds a data-parallel grid of t tiles keeps busy
+static double dp_fill(int64_t t, int G) { return (double)t / (double)(((t + G - 1) / G) * G); }
+
 int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
             const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s, const F8Scales* fs = nullptr) {
+  // 192-row tiles, data-parallel: whole tiles (M % 192, N % 256), KC A without row segments, one C segment, a direct
+  // epilogue kind, and a grid the 256-row tiles fill badly -- 9984 x 2304 (o fwd, q|k|v dgrad): 351 tiles on 256
+  // CUs keep 69 % of two rounds busy, 468 tiles of 3/4 the work 91 %
+  // Epilogue STORE (the direct epilogue's kind on plain tiles); up to 192 k-tiles: longer k-loops amortise the
+  // stream-K hand-off of the 256-row grid better (gate/up dgrad, 288 k-tiles: 0.670 ms stream-K vs 0.723 ms here;
+  // down fwd, 144: 0.345 vs 0.303; o fwd 0.100 -> 0.084 ms; profiles/r5q_gemm_ab_192.txt).  B KC only, i.e. the
+  // forward projections x W^T: the input-gradient GEMMs (B = W read RC) were 12-16 % faster alone too, but in the
+  // layer backward their weight-gradient partner runs beside them on the side stream (functional._SideWork) and
+  // already fills the CUs the 256-row grid leaves idle -- there the 192-row grid took them away from it (block A/B:
+  // forward -20 us, backward +20 us, profiles/r5r_*).
+  if (G4_192 && !fs && A.layout == SVLA_LAYOUT_KC && B.layout == SVLA_LAYOUT_KC && E.kind == SVLA_EPI_STORE &&
+      M % 192 == 0 && N % 256 == 0 && Cd.n == 1 && A.nseg <= 1 && B.seg_dim != SVLA_SEG_GEGLU &&
+      (K + BK - 1) / BK <= 192) {
+    const int G = num_cus();
+    const int64_t t256 = ((M + 255) / 256) * (N / 256), t192 = (M / 192) * (N / 256);
+    if (t192 >= G && dp_fill(t192, G) >= dp_fill(t256, G) + 0.15) {
+      SKArgs sk;
+      memset(&sk, 0, sizeof(sk));
+      sk.nk = (int)((K + BK - 1) / BK);
+      sk.dp_tiles = (int)t192;
+      sk.grid = (int)t192;
+      dim3 grid((unsigned)sk.grid), block(p4::NTH);
+#define SVLA_LAUNCH4_192(LB_)                                                                                \
+  {                                                                                                          \
+    static bool lds_set = false;                                                                             \
+    if (!lds_set) {                                                                                          \
+      (void)hipFuncSetAttribute((const void*)gemm4_kernel_0##LB_##_192, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                p4::LDS);                                                                    \
+      lds_set = true;                                                                                        \
+    }                                                                                                        \
+    hipLaunchKernelGGL(gemm4_kernel_0##LB_##_192, grid, block, p4::LDS, s, M, N, K, A, B, Cd, E, sk);         \
+  }
+      SVLA_LAUNCH4_192(0)
+#undef SVLA_LAUNCH4_192
+      return svla::check_launch("gemm4 (192-row tiles)");
+    }
+  }
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   SKArgs sk;
   memset(&sk, 0, sizeof(sk));

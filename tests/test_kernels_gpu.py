@@ -1064,3 +1064,43 @@ def test_geglu_gelu_table_bitwise(cuda, M):
     y = torch.empty_like(g)
     Kn.gelu_rows(0, g, y)
     assert torch.equal(y, act)
+
+
+@pytest.mark.parametrize("lay", ["nt", "nn"])
+def test_gemm4_192_row_tiles(cuda, lay):
+    """The 4-wave GEMM's 192-row tiles (launch4 picks them for forward projections of 9984 x 2304: 468 tiles instead
+    of 351 on 256 CUs; nn = an input-gradient layout, which keeps the 256-row tiles): a K with a ragged last k-tile,
+    STORE with alpha and accumulate (BIAS stays on the 256-row tiles), against torch in fp32 and against the same product at M = 9984 + 64 (not a multiple of 192:
+    the 256-row kernel) row for row."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(31)
+    M, N, K = 9984, 2304, 416
+    a = _r(M + 64, K)
+    if lay == "nt":
+        w = _r(N, K, scale=0.1)
+        B = Kn._operand([w], L.LAYOUT_KC)
+        ref = a.float() @ w.float().T
+    else:
+        w = _r(K, N, scale=0.1)
+        B = Kn._operand([w], L.LAYOUT_RC)
+        ref = a.float() @ w.float()
+    c = torch.empty(M, N, dtype=BF, device=cuda)
+    Kn.gemm(M, N, K, Kn._operand([a[:M]], L.LAYOUT_KC), B, [c], [0], N, Kn._epi())
+    big = torch.empty(M + 64, N, dtype=BF, device=cuda)
+    Kn.gemm(M + 64, N, K, Kn._operand([a], L.LAYOUT_KC), B, [big], [0], N, Kn._epi())
+    torch.cuda.synchronize()
+    assert rel_l2(c, ref[:M]) < 5e-3
+    # same k order in every tile shape (no stream-K at K = 416): bitwise the 256-row tiles' result
+    assert torch.equal(c, big[:M])
+    # alpha + accumulate, and BIAS
+    c2 = c.clone()
+    Kn.gemm(M, N, K, Kn._operand([a[:M]], L.LAYOUT_KC), B, [c2], [0], N, Kn._epi(alpha=0.5, accumulate=True))
+    exp = (0.5 * c.float() + c.float()).to(BF)
+    assert (c2.float() - exp.float()).abs().max().item() <= 2e-2 * c.float().abs().max().item()
+    # BIAS keeps the 256-row tiles (LDS epilogue): the same values either way
+    bias = _r(N)
+    c3 = torch.empty_like(c)
+    Kn.gemm(M, N, K, Kn._operand([a[:M]], L.LAYOUT_KC), B, [c3], [0], N, Kn._epi(L.EPI_BIAS, bias=bias))
+    big3 = torch.empty_like(big)
+    Kn.gemm(M + 64, N, K, Kn._operand([a], L.LAYOUT_KC), B, [big3], [0], N, Kn._epi(L.EPI_BIAS, bias=bias))
+    assert torch.equal(c3, big3[:M]) and rel_l2(c3, ref[:M] + bias.float()) < 5e-3

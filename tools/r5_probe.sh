@@ -29,6 +29,15 @@ if [ -n "$BLOCK_FLAG" ]; then
   step block_flag 300 python -u tools/block_ab.py flag $BLOCK_FLAG 6 > $O/block_flag.txt 2>&1
   cat $O/block_flag.txt
 fi
+if [ -n "$TRACE_AB" ]; then  # in-situ block breakdown for the main library and for $TRACE_AB
+  step trace_a 180 rocprofv3 --kernel-trace --stats -d /tmp/tra -o t --output-format csv -- python3 tools/block_ab.py 1 1 5 > $O/trace_a.log 2>&1
+  python tools/block_trace.py /tmp/tra > $O/block_breakdown_main.txt 2>&1
+  export SVLA_LIB=$R/$TRACE_AB
+  step trace_b 180 rocprofv3 --kernel-trace --stats -d /tmp/trb -o t --output-format csv -- python3 tools/block_ab.py 1 1 5 > $O/trace_b.log 2>&1
+  unset SVLA_LIB
+  python tools/block_trace.py /tmp/trb > $O/block_breakdown_alt.txt 2>&1
+  paste $O/block_breakdown_main.txt $O/block_breakdown_alt.txt | cut -c1-200
+fi
 if [ -n "$MXDBG" ]; then
   step mxdbg 120 python -u tools/mx_debug.py > $O/mx_debug.txt 2>&1
   cat $O/mx_debug.txt
