@@ -58,6 +58,14 @@ _side_streams: dict = {}
 _join_queued: dict = {}  # device -> main stream the end-of-backward callback will make wait
 
 
+def side_stream(device) -> "torch.cuda.Stream":
+    """The per-device side stream (_SideWork's; the forward also runs the frozen Zoe estimator on it)."""
+    s = _side_streams.get(device)
+    if s is None:
+        s = _side_streams[device] = torch.cuda.Stream(device)
+    return s
+
+
 def join_side_work():
     """Make the stream that queued side-stream weight gradients wait for all of them."""
     for dev, main in list(_join_queued.items()):
@@ -77,10 +85,7 @@ class _SideWork:
         if self.on:
             dev = like.device
             self.main = torch.cuda.current_stream(dev)
-            s = _side_streams.get(dev)
-            if s is None:
-                s = _side_streams[dev] = torch.cuda.Stream(dev)
-            self.side = s
+            self.side = side_stream(dev)
 
     def run(self, fn, *reads):
         if not self.on:

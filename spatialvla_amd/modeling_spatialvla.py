@@ -24,6 +24,9 @@ from transformers.utils import ModelOutput
 
 from . import functional as Fn
 from . import zoe_fast
+
+# the Zoe depth + Ego3D encoding of the training forward on the side stream beside SigLIP (SVLA_ZOE_STREAM=0: serial)
+ZOE_STREAM = [os.environ.get("SVLA_ZOE_STREAM", "1") != "0"]
 from . import kernels as K
 from .configuration_spatialvla import SpatialVLAConfig
 from .modeling_gemma2 import Gemma2ForCausalLM, Gemma2KVCache, KVMask
@@ -285,13 +288,28 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         sig_in = torch.empty_like(pv)
         K.affine(pv, 1.0 / SIGLIP_STD[0], -SIGLIP_MEAN[0], sig_in)  # TF.normalize (:309)
         B = pv.shape[0]
-        feats = self.vision_tower(sig_in)                           # [B, np, Hv]
+        enc = None
+        if self.config.use_vision_zoe and depth is None and ZOE_STREAM[0] and pv.is_cuda and \
+                not torch.cuda.is_current_stream_capturing():
+            # the frozen Zoe estimator and the Ego3D encoding (no autograd) on the side stream, beside the SigLIP
+            # tower: two independent networks, each filling the CUs the other's kernel tails leave idle
+            main = torch.cuda.current_stream(pv.device)
+            side = Fn.side_stream(pv.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                enc = self.ego3d_features(intrinsic, self.predict_depth(pixel_values.to(dt)), kinv)
+            feats = self.vision_tower(sig_in)                       # [B, np, Hv]
+            main.wait_stream(side)
+            enc.record_stream(main)  # allocated on the side stream, read (and saved for backward) on this one
+        else:
+            feats = self.vision_tower(sig_in)                       # [B, np, Hv]
         Hv = feats.shape[-1]
         sel = feats.reshape(-1, Hv)
         if self.config.use_vision_zoe:
-            if depth is None:
-                depth = self.predict_depth(pixel_values.to(dt))
-            enc = self.ego3d_features(intrinsic, depth, kinv)  # kinv: precomputed outside a graph capture
+            if enc is None:
+                if depth is None:
+                    depth = self.predict_depth(pixel_values.to(dt))
+                enc = self.ego3d_features(intrinsic, depth, kinv)  # kinv: precomputed outside a graph capture
             sel = self.position_embedding_3d.forward_residual(enc, sel)
         lin = self.multi_modal_projector.linear
         img = Fn.LinearFn.apply(sel, lin.weight, lin.bias, None, 1.0 / (self.config.text_config.hidden_size ** 0.5))

@@ -94,6 +94,10 @@ if [ -n "$GEMM_BENCH" ]; then
   step gemm_bench 400 python -u tools/gemm_bench.py > $O/gemm_bench.txt 2>&1
   cat $O/gemm_bench.txt
 fi
+if [ -n "$AB_ENV" ]; then
+  step ab_env 1100 tools/ab_env.sh $AB_ENV ${AB_ROUNDS:-2} > $O/ab_env.txt 2>&1
+  cat $O/ab_env.txt
+fi
 if [ -n "$BENCH" ]; then
   step bench 600 python -u bench.py $BENCH_ARGS > $O/bench.json 2> $O/bench.err
   head -c 2500 $O/bench.json; echo
