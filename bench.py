@@ -343,8 +343,11 @@ def main():
         model.enable_fp8_projections(True)
     n_train = sum(p.numel() for p in model.parameters() if p.requires_grad)
     total = args.warmup + args.steps
+    # SVLA_OPT_OVERLAP=1: AdamW of step k beside step k+1's forward (TrainEngine overlap_optimizer); measured no
+    # faster at N=1 (216.3 vs 216.8 ms, profiles/r5w_step_ab_opt_overlap.txt), so the serial step is the default
     engine = TrainEngine(model, lr=2e-5, weight_decay=0.0, max_grad_norm=1.0, warmup_ratio=0.005,
-                         total_steps=max(total, 10), defer_host_checks=True)
+                         total_steps=max(total, 10), defer_host_checks=True,
+                         overlap_optimizer=os.environ.get("SVLA_OPT_OVERLAP", "0") != "0")
     log(f"[bench] rank {rank}/{world}: model built in {time.perf_counter() - t0:.1f}s, trainable {n_train / 1e9:.3f}B, "
         f"flat buffers {engine.numel / 1e9:.3f}B elems, buckets {len(engine.buckets)}")
     batches = [make_batch(cfgd, B, args.seed + 1000 * rank + s, device) for s in range(total)]

@@ -180,12 +180,18 @@ class TrainEngine:
     def __init__(self, model, lr: float = 2e-5, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  max_grad_norm: float = 1.0, warmup_ratio: float = 0.005, total_steps: int = 1000,
                  process_group=None, bucket_bytes: int = 256 << 20, overlap: bool = True, kernels=None,
-                 defer_host_checks: bool = False):
+                 defer_host_checks: bool = False, overlap_optimizer: bool = False):
         """kernels: the optimizer kernel module (sumsq / clip_scale / adamw); the libsvla wrappers unless a test
         injects a stand-in to exercise the exchange logic without a GPU.
         defer_host_checks: opt-in; the model's image-token count check (reference modeling_spatialvla.py:379-385)
-        is then raised from the next forward instead of the current one, so no step waits on a host read."""
+        is then raised from the next forward instead of the current one, so no step waits on a host read.
+        overlap_optimizer: opt-in; AdamW runs bucket by bucket on its own stream in the order the next forward needs
+        the parameters, and that forward waits per layer for its own bucket (the ZeRO-1 parameter wait points), so
+        the HBM-bound update overlaps the compute-bound forward.  The parameters, master weights and moments are then
+        final only once the next forward's wait points, `synchronize()`, `sync_params()` or `full_master()` ran:
+        code that reads them directly after `train_step` must call `synchronize()` first."""
         self.model = model
+        self._opt_events: Dict[int, object] = {}  # bucket -> event after its side-stream AdamW (overlap_optimizer)
         if defer_host_checks and hasattr(model, "defer_checks"):
             model.defer_checks = True
         self.K = kernels if kernels is not None else K
@@ -200,6 +206,10 @@ class TrainEngine:
         self.device = dev
         world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.world = world
+        self.overlap_opt = bool(overlap_optimizer) and dev.type == "cuda"
+        # its own stream: the forward's side stream (functional.side_stream) carries the frozen Zoe estimator, which
+        # must not queue behind the optimizer
+        self._opt_stream = torch.cuda.Stream(dev) if self.overlap_opt else None
 
         # ---- flat layout: parameters in backward order, buckets cut at parameter boundaries and padded to a
         # multiple of world * ALIGN elements (the ZeRO chunks of every rank are equal and aligned)
@@ -285,16 +295,17 @@ class TrainEngine:
         for b, (r, point) in first_wait.items():
             ex.wait_buckets.setdefault(point, []).append(b)
         self.gather_order = sorted(first_wait, key=lambda b: first_wait[b][0])
-        if world > 1:
+        self.opt_order = self.gather_order + [b for b in range(len(buckets)) if b not in first_wait]
+        if world > 1 or self.overlap_opt:
             lm = model.language_model.model
             vt = model.vision_tower.vision_model
-            if overlap:
+            if overlap and world > 1:
                 lm._svla_layer_grad_hook = lambda i: ex.on_grads_ready(("gemma", i))
                 vt._svla_layer_grad_hook = lambda i: ex.on_grads_ready(("siglip", i))
             for mod in (model, model.language_model, lm, vt):  # wait points: "pre", ("siglip", i), ("gemma", i), "head"
-                mod._svla_param_wait = ex.wait_params
+                mod._svla_param_wait = self._param_wait
             # inference entry points (predict_action) replay captured graphs that contain no wait points
-            model._svla_param_wait_all = ex.wait_all_params
+            model._svla_param_wait_all = self.sync_params
 
     # ------------------------------------------------------------------ optimizer
     def lr_at(self, step: int) -> float:
@@ -305,9 +316,27 @@ class TrainEngine:
             return self.lr * step / max(1, self.warmup_steps)
         return self.lr * max(0.0, (self.total_steps - step) / max(1, self.total_steps - self.warmup_steps))
 
+    def _param_wait(self, point):
+        """Forward wait point: the buckets whose first user is `point` -- their side-stream AdamW
+        (overlap_optimizer) and their all-gather (N > 1)."""
+        if self._opt_events:
+            cur = torch.cuda.current_stream(self.device)
+            for b in self.exchange.wait_buckets.get(point, ()):
+                ev = self._opt_events.pop(b, None)
+                if ev is not None:
+                    cur.wait_event(ev)
+        self.exchange.wait_params(point)
+
+    def synchronize(self):
+        """Make the current stream wait for every side-stream AdamW still in flight (overlap_optimizer)."""
+        if self._opt_events:
+            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+            self._opt_events.clear()
+
     def optimizer_step(self):
         """clip + AdamW on the owned chunks, then the parameter all-gathers (left in flight: the next forward's
-        layers wait for their own bucket)."""
+        layers wait for their own bucket).  overlap_optimizer: AdamW and the gathers go to the side stream, bucket
+        by bucket in the next forward's order, each followed by an event its wait point waits for."""
         self.step_count += 1
         lr = self.lr_at(self.step_count - 1)
         ex = self.exchange
@@ -321,8 +350,24 @@ class TrainEngine:
             torch.sum(self.sumsq_parts, 0, keepdim=True, out=self.sumsq)
             dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=ex.pg)
         Kx.clip_scale(self.sumsq, self.max_grad_norm, self.clip, self.gnorm)
-        from . import functional as Fn
         Fn.WEIGHT_EPOCH[0] += 1  # AdamW below rewrites the bf16 weights behind torch's version counters
+        if self.overlap_opt:
+            main = torch.cuda.current_stream(self.device)
+            side = self._opt_stream
+            side.wait_stream(main)  # the clip scale and every gradient are final
+            with torch.cuda.stream(side):
+                for b in self.opt_order:
+                    ex.land(b)
+                    o, c = ex.owned(b)
+                    so = self.shard_offsets[b]
+                    Kx.adamw(self.master[so:so + c], self.flat_param[o:o + c], self.flat_grad[o:o + c],
+                             self.m[so:so + c], self.v[so:so + c], lr, self.betas[0], self.betas[1], self.eps,
+                             self.wd, self.step_count, self.clip)
+                    ex.all_gather(b)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    self._opt_events[b] = ev
+            return
         if self.world == 1:
             Kx.adamw(self.master, self.flat_param, self.flat_grad, self.m, self.v, lr, self.betas[0], self.betas[1],
                     self.eps, self.wd, self.step_count, self.clip)
@@ -342,6 +387,7 @@ class TrainEngine:
         A batch without pixel_values leaves the vision-side gradients unwritten: they are zeroed (an unused
         parameter's gradient is zero, as in the reference's DeepSpeed step), not left at the previous step's."""
         out = self.model(**batch, return_dict=True)
+        self.synchronize()  # overlap_optimizer: every AdamW done before the backward rewrites the gradients
         out.loss.backward()
         if batch.get("pixel_values") is None:
             for o, n in self.vision_slices:
@@ -351,11 +397,13 @@ class TrainEngine:
         return out.loss.detach()
 
     def sync_params(self):
-        """Wait for every parameter all-gather still in flight (before evaluation or saving)."""
+        """Wait for every parameter update and all-gather still in flight (before evaluation or saving)."""
+        self.synchronize()
         self.exchange.wait_all_params()
 
     def full_master(self) -> torch.Tensor:
         """The fp32 master weights in the flat layout (gathered across ranks; tests / checkpoints)."""
+        self.synchronize()
         ex = self.exchange
         if self.world == 1:
             return self.master.clone()

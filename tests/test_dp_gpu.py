@@ -108,3 +108,23 @@ def test_dp2_train_step_equals_single_process(cuda):
             assert np.linalg.norm((m_got - p0) - d1) <= 0.1 * np.linalg.norm(d1), (n, r[0])
     for n in params1:  # ranks agree bitwise after the all-gather
         assert np.array_equal(res[0][3][n], res[1][3][n]), n
+
+
+def test_overlap_optimizer_equals_serial(cuda):
+    """TrainEngine(overlap_optimizer=True) (AdamW per bucket on the side stream, waited for per layer by the next
+    forward) gives bitwise the losses, fp32 masters and bf16 parameters of the serial optimizer step over the test's steps."""
+    from spatialvla_amd.engine import TrainEngine
+    depth = torch.rand(B_TOTAL, 1, 224, 224, generator=torch.Generator().manual_seed(9)).mul(3).add(0.5).to(cuda)
+    out = {}
+    for ov in (False, True):
+        torch.manual_seed(0)
+        model = H.build_hip_model(H.cfg_dict("tiny"), cuda)
+        model.predict_depth = lambda pv, _d=depth: _d
+        eng = TrainEngine(model, lr=1e-3, warmup_ratio=0.0, total_steps=100, max_grad_norm=1.0,
+                          bucket_bytes=1 << 16, overlap_optimizer=ov)
+        assert len(eng.buckets) > 4
+        losses = [eng.train_step(b).detach().clone() for b in _batches(cuda)]
+        eng.sync_params()
+        out[ov] = (torch.stack(losses).cpu(), eng.full_master().cpu(), eng.flat_param.clone().cpu())
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)

@@ -95,7 +95,7 @@ if [ -n "$GEMM_BENCH" ]; then
   cat $O/gemm_bench.txt
 fi
 if [ -n "$AB_ENV" ]; then
-  step ab_env 1100 tools/ab_env.sh $AB_ENV ${AB_ROUNDS:-2} > $O/ab_env.txt 2>&1
+  step ab_env 1100 tools/ab_env.sh $AB_ENV ${AB_ROUNDS:-2} $AB_VALS > $O/ab_env.txt 2>&1
   cat $O/ab_env.txt
 fi
 if [ -n "$BENCH" ]; then
