@@ -86,6 +86,10 @@ if [ -n "$ATT_PMC" ]; then
     cat $O/attn_pmc_${shp}_${what}.txt
   done
 fi
+if [ -n "$NORM_AB" ]; then
+  step norm_ab 300 python -u tools/norm_ab.py spatialvla_amd/libsvla.so $NORM_AB > $O/norm_ab.txt 2>&1
+  cat $O/norm_ab.txt
+fi
 if [ -n "$GEGLU_AB" ]; then
   step geglu_ab 300 python -u tools/geglu_ab.py $GEGLU_AB > $O/geglu_ab.txt 2>&1
   cat $O/geglu_ab.txt
