@@ -24,31 +24,11 @@
 #include "agpr.h"
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 #include "agpr_f8.h"
-#include "tanh_bf16_table.h"
+#include "softcap_tab.h"
 
 #include <type_traits>
 
 namespace {
-
-// Gemma2 final logit softcap (softcap_bf16 of svla_common.h) with tanh taken from a table: a = bf16(bf16(v) / cap) is
-// a bf16 value, and bf16(tanh(a)) is a for |a| < 2^-8, 1 for |a| >= 4, and a 1280-entry table in between
-// (tools/gen_tanh_table.py; a correctly rounded fp32 tanh cast to bf16, as the reference's bf16 tanh).  Replaces
-// the branch-free polynomial/exp tanh (~17 VALU ops and two transcendentals) of the lm_head epilogue.
-template <typename Tab, bool V_IS_BF16 = false>
-__device__ __forceinline__ float softcap_bf16_tab(float v, float cap, float icap, Tab tab) {
-  const float a = round_bf((V_IS_BF16 ? v : round_bf(v)) * icap);  // V_IS_BF16: v already a bf16 value
-  const uint32_t u = __float_as_uint(a);
-  const uint32_t ab = (u >> 16) & 0x7fffu;
-  const uint32_t lo = (uint32_t)SVLA_TANH_TAB_E0 << 7, hi = (uint32_t)SVLA_TANH_TAB_E1 << 7;
-  const uint32_t idx = ab < lo ? 0u : (ab >= hi ? 0u : ab - lo);
-  const uint32_t tb = tab[idx];
-  uint32_t rb = ab < lo ? ab : (ab >= hi ? 0x3f80u : tb);
-  if (ab > 0x7f80u) rb = ab;  // NaN stays NaN
-  const float t = __uint_as_float((((u >> 16) & 0x8000u) | rb) << 16);
-  return round_bf(t * cap);
-}
-constexpr int TANH_TAB_BYTES = sizeof(svla_tanh_bf16_tab);
-static_assert(TANH_TAB_BYTES % 16 == 0, "table copied in 16-B pieces");
 
 // The GeGLU kernel's LDS copy of the gelu table (gelu_bf16_lut, svla_common.h): the direct epilogue looks up 128
 // elements per lane per 256 x 256 tile, where gelu_tanh's ~30 VALU and two transcendentals made it VALU-bound (one
@@ -3514,112 +3494,6 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
 
 }  // namespace
 
-// ------------------------------------------------------------------------------------------------------------
-// Softcap + softmax statistics of raw lm_head logits, in place (svla_softcap_ce_rows).  A wave covers 512 columns of
-// a row (8 per lane, 16-B loads/stores), 16 lanes = one 128-column group: per lane {max, first argmax, sum exp} of
-// its 8 values, then the group combine of SOFTCAP_CE's LDS epilogue (same chunk partition, same butterfly), so the
-// statistics are bitwise the fused epilogue's.  Persistent blocks, the bf16 tanh table staged in LDS once per block.
-// ------------------------------------------------------------------------------------------------------------
-namespace {
-// softcap_bf16_tab on a packed bf16 pair, returning the packed bf16 results: the two roundings are one
-// v_cvt_pk_bf16_f32 each, and the range tests fold into one unsigned offset d = |a| - lo: d < NTAB indexes the table,
-// NTAB <= d <= 0x7f80 - lo (|a| >= 4, inf included) reads the sentinel entry tab[NTAB] = 1.0, and d beyond that (|a|
-// below the table: tanh(a) = a in bf16; NaN) keeps |a|.  Bitwise softcap_bf16_tab<_, true> of each element.
-constexpr uint32_t TAB_LO = (uint32_t)SVLA_TANH_TAB_E0 << 7, TAB_N = ((uint32_t)SVLA_TANH_TAB_E1 << 7) - TAB_LO;
-static_assert(TAB_N * 2 == TANH_TAB_BYTES, "table covers [E0, E1) exactly");
-template <typename Tab>
-__device__ __forceinline__ uint32_t softcap_pair_tab(uint32_t w, float cap, float icap, const Tab& tab) {
-  const uint32_t a = pack2(__uint_as_float(w << 16) * icap, __uint_as_float(w & 0xffff0000u) * icap);
-  uint32_t t[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t ab = (a >> (16 * h)) & 0x7fffu;
-    const uint32_t d = ab - TAB_LO;
-    const uint32_t tb = tab[min(d, TAB_N)];
-    const uint32_t rb = d > 0x7f80u - TAB_LO ? ab : tb;
-    t[h] = (((a >> (16 * h)) & 0x8000u) | rb) << 16;
-  }
-  return pack2(__uint_as_float(t[0]) * cap, __uint_as_float(t[1]) * cap);
-}
-
-__global__ __launch_bounds__(256) void softcap_rows_kernel(int64_t M, int64_t N, bf16_t* __restrict__ lg, int64_t ld,
-                                                           float cap, float* __restrict__ row_stats) {
-  __shared__ __attribute__((aligned(16))) unsigned short tab[TANH_TAB_BYTES / 2 + 8];  // + the 1.0 sentinel
-  if ((int)threadIdx.x < TANH_TAB_BYTES / 16)
-    reinterpret_cast<u32x4*>(tab)[threadIdx.x] = reinterpret_cast<const u32x4*>(svla_tanh_bf16_tab)[threadIdx.x];
-  if (threadIdx.x == 0) tab[TAB_N] = 0x3f80;
-  __syncthreads();
-  const float icap = 1.0f / cap;
-  const int lane = threadIdx.x & 63;
-  const int64_t cpr = (N + 511) / 512;          // 512-column chunks per row
-  const int64_t ntn = (N + 127) / 128;
-  const int64_t total = M * cpr;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
-  for (int64_t u = wid; u < total; u += nw) {
-    const int64_t m = u / cpr;
-    const int64_t n = (u - m * cpr) * 512 + 8 * lane;
-    const int64_t nv = N - n;
-    bf16_t* p = lg + m * ld + n;
-    float v[8];
-    float mx = -INFINITY, se = 0.f;
-    int am = 0x7fffffff;
-    if (nv >= 8) {  // whole 16-B chunk: packed pairs, the result words stored as they come
-      const u32x4 w = *reinterpret_cast<const u32x4*>(p);
-      u32x4 o;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = softcap_pair_tab(w[i], cap, icap, tab);
-      *reinterpret_cast<u32x4*>(p) = o;
-      unpack8(o, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (v[j] > mx) { mx = v[j]; am = (int)(n + j); }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) se += __expf(v[j] - mx);
-      if (mx == -INFINITY) se = 0.f;
-    } else if (nv > 0) {
-      load8f(p, v, nv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = softcap_bf16_tab<decltype(tab), true>(v[j], cap, icap, tab);  // v unpacked from bf16 logits
-        if (j < nv && v[j] > mx) { mx = v[j]; am = (int)(n + j); }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < nv) se += __expf(v[j] - mx);
-      if (mx == -INFINITY) se = 0.f;
-      store8(p, v, nv);
-    }
-    float gm = mx;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) gm = fmaxf(gm, __shfl_xor(gm, o, 64));
-    se = (mx == -INFINITY) ? 0.f : se * __expf(mx - gm);
-    am = (mx == gm) ? am : 0x7fffffff;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      se += __shfl_xor(se, o, 64);
-      am = min(am, __shfl_xor(am, o, 64));
-    }
-    if ((lane & 15) == 0 && nv > 0) {
-      float* rs = row_stats + (m * ntn + n / 128) * 3;
-      rs[0] = gm;
-      rs[1] = se;
-      rs[2] = __int_as_float(am);
-    }
-  }
-}
-}  // namespace
-
-extern "C" int svla_softcap_ce_rows(int64_t M, int64_t N, void* logits, int64_t ld, float cap, float* row_stats,
-                                    void* stream) {
-  SVLA_CHECK_ARG(M > 0 && N > 0 && ld >= N && ld % 8 == 0 && cap > 0.f, "softcap_ce_rows: M, N, ld (multiple of 8 "
-                 ">= N), cap > 0");
-  SVLA_CHECK_ARG(logits && row_stats && ((uintptr_t)logits & 15) == 0, "softcap_ce_rows: logits 16-B aligned");
-  const int64_t units = M * ((N + 511) / 512);
-  const int64_t blocks = std::min<int64_t>((units + 3) / 4, (int64_t)num_cus() * 8);
-  hipLaunchKernelGGL(softcap_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, M, N,
-                     (bf16_t*)logits, ld, cap, row_stats);
-  return svla::check_launch("softcap_ce_rows");
-}
 
 // ------------------------------------------------------------------------------------------------------------
 // fp8 e4m3 GEMM (BASELINE configs[4]): both operands KC fp8 with per-row fp32 scales, the 4-wave kernel in fp8 mode.

@@ -396,6 +396,29 @@ __device__ __forceinline__ void st_stream(T* p, T v) {
   else *p = v;
 }
 
+#ifndef ADAMW_U
+#define ADAMW_U 1  // 8-element groups per thread per iteration (diagnostic A/B)
+#endif
+#ifndef ADAMW_NTS
+#define ADAMW_NTS 0  // non-temporal stores only (diagnostic A/B)
+#endif
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+  if constexpr (ADAMW_NT || ADAMW_NTS) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void adamw_scalar(int64_t k, float* __restrict__ master, bf16_t* __restrict__ param,
+                                             const bf16_t* __restrict__ grad, float* __restrict__ m,
+                                             float* __restrict__ v, float lr, float b1, float b2, float eps, float wd,
+                                             float bc1, float bc2, float cs) {
+  const float gg = bf2f(grad[k]) * cs;
+  m[k] = b1 * m[k] + (1.f - b1) * gg;
+  v[k] = b2 * v[k] + (1.f - b2) * gg * gg;
+  const float upd = (m[k] / bc1) / (sqrtf(v[k] / bc2) + eps);
+  master[k] = master[k] - lr * (upd + wd * master[k]);
+  param[k] = f2bf(master[k]);
+}
+
 __global__ void adamw_kernel(int64_t n, float* __restrict__ master, bf16_t* __restrict__ param,
                              const bf16_t* __restrict__ grad, float* __restrict__ m, float* __restrict__ v, float lr,
                              float b1, float b2, float eps, float wd, float bc1, float bc2,
@@ -404,41 +427,73 @@ __global__ void adamw_kernel(int64_t n, float* __restrict__ master, bf16_t* __re
   // the two divides and the square root as 1-ulp hardware reciprocal / sqrt: the correctly rounded forms cost ~30
   // VALU instructions per element (the update agrees with torch.optim.AdamW to ~1e-7 relative)
   const float ibc1 = 1.0f / bc1, ibc2 = 1.0f / bc2;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n; i += stride) {
-    if (i + 8 <= n) {
-      float g[8];
-      unpack8(ld_stream(reinterpret_cast<const u32x4*>(grad + i)), g);
-      f32x4 p0 = ld_stream(reinterpret_cast<const f32x4*>(master + i)),
-            p1 = ld_stream(reinterpret_cast<const f32x4*>(master + i + 4));
-      f32x4 m0 = ld_stream(reinterpret_cast<const f32x4*>(m + i)), m1 = ld_stream(reinterpret_cast<const f32x4*>(m + i + 4));
-      f32x4 v0 = ld_stream(reinterpret_cast<const f32x4*>(v + i)), v1 = ld_stream(reinterpret_cast<const f32x4*>(v + i + 4));
-      float pp[8] = {p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
-      float mm[8] = {m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
-      float vv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  constexpr int U = ADAMW_U;
+  const int64_t gs = (int64_t)blockDim.x * 8;  // elements a block covers per group
+  const int64_t stride = (int64_t)gridDim.x * gs * U;
+  for (int64_t base = (int64_t)blockIdx.x * gs * U + threadIdx.x * 8; base < n; base += stride) {
+    if (base + (U - 1) * gs + 8 <= n) {
+      float g[U][8], pp[U][8], mm[U][8], vv[U][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gg = g[j] * cs;
-        mm[j] = b1 * mm[j] + (1.f - b1) * gg;
-        vv[j] = b2 * vv[j] + (1.f - b2) * gg * gg;
-        const float upd = (mm[j] * ibc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[j] * ibc2) + eps);
-        pp[j] = pp[j] - lr * (upd + wd * pp[j]);
+      for (int u = 0; u < U; ++u) {  // every load of the U groups in flight before any arithmetic
+        const int64_t i = base + u * gs;
+        unpack8(ld_stream(reinterpret_cast<const u32x4*>(grad + i)), g[u]);
+        const f32x4 p0 = ld_stream(reinterpret_cast<const f32x4*>(master + i)),
+                    p1 = ld_stream(reinterpret_cast<const f32x4*>(master + i + 4));
+        const f32x4 m0 = ld_stream(reinterpret_cast<const f32x4*>(m + i)),
+                    m1 = ld_stream(reinterpret_cast<const f32x4*>(m + i + 4));
+        const f32x4 v0 = ld_stream(reinterpret_cast<const f32x4*>(v + i)),
+                    v1 = ld_stream(reinterpret_cast<const f32x4*>(v + i + 4));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pp[u][q] = p0[q]; pp[u][4 + q] = p1[q];
+          mm[u][q] = m0[q]; mm[u][4 + q] = m1[q];
+          vv[u][q] = v0[q]; vv[u][4 + q] = v1[q];
+        }
       }
-      st_stream(reinterpret_cast<f32x4*>(master + i), f32x4{pp[0], pp[1], pp[2], pp[3]});
-      st_stream(reinterpret_cast<f32x4*>(master + i + 4), f32x4{pp[4], pp[5], pp[6], pp[7]});
-      st_stream(reinterpret_cast<f32x4*>(m + i), f32x4{mm[0], mm[1], mm[2], mm[3]});
-      st_stream(reinterpret_cast<f32x4*>(m + i + 4), f32x4{mm[4], mm[5], mm[6], mm[7]});
-      st_stream(reinterpret_cast<f32x4*>(v + i), f32x4{vv[0], vv[1], vv[2], vv[3]});
-      st_stream(reinterpret_cast<f32x4*>(v + i + 4), f32x4{vv[4], vv[5], vv[6], vv[7]});
-      st_stream(reinterpret_cast<u32x4*>(param + i), pack8(pp));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + u * gs;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gg = g[u][j] * cs;
+          mm[u][j] = b1 * mm[u][j] + (1.f - b1) * gg;
+          vv[u][j] = b2 * vv[u][j] + (1.f - b2) * gg * gg;
+          const float upd = (mm[u][j] * ibc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[u][j] * ibc2) + eps);
+          pp[u][j] = pp[u][j] - lr * (upd + wd * pp[u][j]);
+        }
+        st_out(reinterpret_cast<f32x4*>(master + i), f32x4{pp[u][0], pp[u][1], pp[u][2], pp[u][3]});
+        st_out(reinterpret_cast<f32x4*>(master + i + 4), f32x4{pp[u][4], pp[u][5], pp[u][6], pp[u][7]});
+        st_out(reinterpret_cast<f32x4*>(m + i), f32x4{mm[u][0], mm[u][1], mm[u][2], mm[u][3]});
+        st_out(reinterpret_cast<f32x4*>(m + i + 4), f32x4{mm[u][4], mm[u][5], mm[u][6], mm[u][7]});
+        st_out(reinterpret_cast<f32x4*>(v + i), f32x4{vv[u][0], vv[u][1], vv[u][2], vv[u][3]});
+        st_out(reinterpret_cast<f32x4*>(v + i + 4), f32x4{vv[u][4], vv[u][5], vv[u][6], vv[u][7]});
+        st_out(reinterpret_cast<u32x4*>(param + i), pack8(pp[u]));
+      }
     } else {
-      for (int64_t k = i; k < n; ++k) {
-        const float gg = bf2f(grad[k]) * cs;
-        m[k] = b1 * m[k] + (1.f - b1) * gg;
-        v[k] = b2 * v[k] + (1.f - b2) * gg * gg;
-        const float upd = (m[k] / bc1) / (sqrtf(v[k] / bc2) + eps);
-        master[k] = master[k] - lr * (upd + wd * master[k]);
-        param[k] = f2bf(master[k]);
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + u * gs;
+        if (i >= n) break;
+        if (i + 8 <= n) {  // a whole group: the vector path's arithmetic
+          float g[8], pp[8], mm[8], vv[8];
+          unpack8(ld_stream(reinterpret_cast<const u32x4*>(grad + i)), g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pp[j] = master[i + j];
+            mm[j] = m[i + j];
+            vv[j] = v[i + j];
+            const float gg = g[j] * cs;
+            mm[j] = b1 * mm[j] + (1.f - b1) * gg;
+            vv[j] = b2 * vv[j] + (1.f - b2) * gg * gg;
+            const float upd = (mm[j] * ibc1) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv[j] * ibc2) + eps);
+            pp[j] = pp[j] - lr * (upd + wd * pp[j]);
+            master[i + j] = pp[j];
+            m[i + j] = mm[j];
+            v[i + j] = vv[j];
+          }
+          *reinterpret_cast<u32x4*>(param + i) = pack8(pp);
+        } else {
+          for (int64_t k = i; k < n; ++k) adamw_scalar(k, master, param, grad, m, v, lr, b1, b2, eps, wd, bc1, bc2, cs);
+        }
       }
     }
   }
@@ -578,8 +633,11 @@ extern "C" int svla_adamw(int64_t n, float* master, void* param_bf16, const void
                           const float* clip_scale, void* stream) {
   SVLA_CHECK_ARG(n > 0 && master && param_bf16 && grad_bf16 && m && v, "adamw: args");
   SVLA_CHECK_ARG(al16(master) && al16(param_bf16) && al16(grad_bf16) && al16(m) && al16(v), "adamw: alignment");
-  unsigned g = nblk(n, 256 * 8);
-  if (g > 256 * 64) g = 256 * 64;
+#ifndef ADAMW_GRID
+#define ADAMW_GRID (256 * 64)  // block cap (diagnostic A/B)
+#endif
+  unsigned g = nblk(n, 256 * 8 * ADAMW_U);
+  if (g > ADAMW_GRID) g = ADAMW_GRID;
   hipLaunchKernelGGL(adamw_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, n, master, (bf16_t*)param_bf16,
                      (const bf16_t*)grad_bf16, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, clip_scale);
   return svla::check_launch("adamw");

@@ -466,6 +466,57 @@ def test_softcap_rows_every_bf16_logit(cuda):
                                   f"{got[0][~same[0]][:5].tolist()} vs {ref[~same[0]][:5].tolist()}")
 
 
+def test_softcap_rows_stats_special_values(cuda):
+    """svla_softcap_ce_rows statistics where the full-range-table path hands a lane to the per-element path: NaN
+    logits, groups whose maximum is +-0 (the max's sign follows the scan order), tied maxima (first index wins),
+    +-inf and huge logits (saturate to +-cap), a ragged row end.  Softcapped values bit-exact against the reference's
+    op-by-op bf16 softcap; per 128-column group max and first argmax exact, sum exp to 1e-5 (NaN where the group
+    holds a NaN, as the in-order scan propagates it)."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(5)
+    M, V = 48, 2048 + 5
+    ldv = Kn.round_up(V, 64)
+    raw = (torch.randn(M, V) * 8).to(BF)
+    nan, inf = float("nan"), float("inf")
+    raw[0, 5] = nan                                     # NaN in a chunk
+    raw[1, 128:256] = -(torch.rand(128) * 4).to(BF)     # group max = 0 from both signs of zero
+    raw[1, 130], raw[1, 200], raw[1, 131] = 0.0, -0.0, 0.0
+    raw[2, 256:384] = -(torch.rand(128) * 4 + 1).to(BF)
+    raw[2, 300], raw[2, 260] = -0.0, -0.0               # max -0 only
+    raw[3, :128] = 2.5                                  # every value tied
+    raw[4, 0:8] = torch.tensor([1.0, 7.0, 7.0, 3.0, 7.0, 0.5, 7.0, 2.0])  # ties inside one lane's chunk
+    raw[4, 9], raw[4, 700] = 7.0, inf                   # tie in another lane; +inf saturates to cap
+    raw[5, 3], raw[5, 4] = -inf, 1e30                   # -inf; huge -> cap
+    raw[6, 512:640] = -inf                              # a whole group at -cap
+    raw[7, V - 3] = nan                                 # NaN in the ragged end
+    raw[8, V - 2] = 300.0                               # max in the ragged end
+    buf = torch.zeros(M, ldv, dtype=BF, device=cuda)
+    buf[:, :V] = raw.to(cuda)
+    ntn = Kn.ceil_div(V, 128)
+    stats = torch.empty(M, ntn, 3, dtype=torch.float32, device=cuda)
+    Kn.softcap_ce_rows(buf, V, stats, 30.0)
+    x = raw.double()
+    y = ((x / 30.0).to(BF).double().tanh().to(BF).double() * 30.0).to(BF)
+    got = buf[:, :V].cpu()
+    same = (got.view(torch.int16) == y.view(torch.int16)) | (torch.isnan(got.float()) & torch.isnan(y.float()))
+    assert bool(same.all()), f"{int((~same).sum())} softcap mismatches"
+    st = stats.cpu()
+    yf = y.float()
+    for m in range(M):
+        for g in range(ntn):
+            seg = yf[m, g * 128:min(V, g * 128 + 128)]
+            ok = ~torch.isnan(seg)
+            mx = seg[ok].max()
+            first = int(torch.nonzero(ok & (seg == mx))[0]) + g * 128
+            se = float("nan") if not bool(ok.all()) else float(torch.exp(seg.double() - float(mx)).sum())
+            assert float(st[m, g, 0]) == float(mx), (m, g, float(st[m, g, 0]), float(mx))
+            assert int(st[m, g, 2].view(torch.int32)) == first, (m, g, int(st[m, g, 2].view(torch.int32)), first)
+            if se != se:
+                assert float(st[m, g, 1]) != float(st[m, g, 1]), (m, g)
+            else:
+                assert abs(float(st[m, g, 1]) - se) <= 1e-5 * se, (m, g, float(st[m, g, 1]), se)
+
+
 @pytest.mark.parametrize("M,H,V,every", [(300, 256, 1000, 7), (9984 // 8, 2304, 4099, 24), (64, 128, 300, 0)])
 def test_lm_head_ce_fn_label_rows(cuda, M, H, V, every):
     """LMHeadCEFn's backward runs the softmax gradient and both lm_head GEMMs over the labelled rows only;

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Variant build of libsvla.so: tools/build_variant.sh NAME "EXTRA flags" src1.hip [src2.hip ...]
-# Reuses the product objects for every other source; the variant library lands in diag/libsvla_NAME.so.
+# Diagnostic A/B builds: recompile ONE source of libsvla with extra -D flags and link it with the main build's other
+# objects: tools/build_variant.sh <source.hip> <out.so> -DKNOB=VALUE ...
 set -e
-NAME=$1; FLAGS=$2; shift 2
+src=$1; out=$2; shift 2
 R=$(cd "$(dirname "$0")/.." && pwd)
-OBJ=$R/build/obj_$NAME
-mkdir -p $OBJ $R/diag
-cp -p $R/build/obj/*.o $OBJ/
-for s in "$@"; do rm -f $OBJ/${s%.hip}.o; done
-make -s -C $R/spatialvla_amd/csrc -j8 OUT=$R/diag/libsvla_$NAME.so OBJDIR=$OBJ EXTRA="$FLAGS"
-echo built diag/libsvla_$NAME.so
+C=$R/spatialvla_amd/csrc
+tmp=$(mktemp -d)
+/opt/rocm/bin/hipcc "$@" -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-variable \
+  -munsafe-fp-atomics -ffp-contract=fast -c "$C/$src" -o "$tmp/${src%.hip}.o"
+objs=$(ls "$R"/build/obj/*.o | grep -v "/${src%.hip}.o$")
+/opt/rocm/bin/hipcc -shared -fPIC -Wl,-Bsymbolic --offload-arch=gfx950 $objs "$tmp/${src%.hip}.o" -o "$out"
+rm -rf "$tmp"

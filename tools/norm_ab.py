@@ -27,6 +27,16 @@ logits = torch.empty(R, LDV, dtype=BF, device=dev)
 logits.view(-1)[:].copy_((torch.randn(R * LDV // 64, device=dev) * 8).repeat_interleave(64).to(BF))  # 5.3 GB
 stats = torch.empty(R, (V + 127) // 128, 3, device=dev)
 small = (torch.randn(512, LDV, device=dev) * 8).to(BF)
+# the special values that send a lane to the softcap pass's per-element path: NaN, a +-0 group max, ties, +-inf
+small[0, 5] = float("nan")
+small[1, 128:256] = -small[1, 128:256].abs()
+small[1, 130], small[1, 200], small[1, 131] = 0.0, -0.0, 0.0
+small[2, 256:384] = -small[2, 256:384].abs() - 1
+small[2, 300] = -0.0
+small[3, :128] = 2.5
+small[4, 9], small[4, 700], small[5, 3], small[5, 4] = 7.0, float("inf"), float("-inf"), 1e30
+small[6, 512:640] = float("-inf")
+small[7, V - 3] = float("nan")
 gsig = r(8192, 4304)
 part = torch.randn(624, 2304, device=dev)
 cs1, cs2, cs3 = (torch.empty(n, dtype=BF, device=dev) for n in (4304, 1152, 2304))
@@ -76,6 +86,7 @@ for rnd in range(5):
                 outs[(name, tag)] = [t.clone() for t in res_t] if res_t is not None else list(softcap_small())
 ta, tb = libs[0][0], libs[1][0]
 for name in cases():
-    same = all(torch.equal(a, b) for a, b in zip(outs[(name, ta)], outs[(name, tb)]))
+    same = all(torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8))  # bitwise, NaN incl.
+               for a, b in zip(outs[(name, ta)], outs[(name, tb)]))
     print(f"{name:20s} {ta}: {best[(name, ta)]:7.1f} us  {tb}: {best[(name, tb)]:7.1f} us  "
           f"ratio {best[(name, ta)] / best[(name, tb)]:.3f}  bitwise_equal={same}", flush=True)
