@@ -210,26 +210,88 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, co
 // GELU as an HBM pass after a plain-store / bias GEMM (svla_gelu_rows): the VALU-heavy GELU epilogues ran slower
 // inside the GEMM than as a separate read-once / write-once pass.  The rounding points of the fused epilogues:
 // mode 0 y = bf16(gelu_tanh(x)), 1 y = bf16(gelu_erf(x)), 2 y = bf16(x * gelu_tanh'(pre)) (x = bf16 dL/dy).
+// Modes 0 and 1: persistent blocks, gr_u<MODE>() 16-B chunks per thread loaded before any arithmetic, dense rows
+// (ld == N everywhere) indexed linearly; mode 0 reads the gelu table from an LDS copy made once per block (from
+// global memory every lookup was a scattered 2-B load): SigLIP fc1 38.1 -> 23.5 us isolated (profiles/r6i_gelu_ab.txt).
+// Mode 2 keeps one chunk per thread, non-persistent (measured faster for it).
+#ifndef GR_OLD
+#define GR_OLD 0  // diagnostic builds: 1 = every mode one chunk per thread, non-persistent, global-memory table
+#endif
+template <int MODE>
+constexpr bool gr_simple() { return GR_OLD || MODE == 2; }
+template <int MODE>
+constexpr int gr_u() { return MODE == 0 ? 1 : 2; }
 template <int MODE>
 __global__ __launch_bounds__(256) void gelu_rows_kernel(int64_t M, int64_t N, const bf16_t* x, int64_t ldx,
                                                         const bf16_t* __restrict__ pre, int64_t ldp, bf16_t* y,
                                                         int64_t ldy) {
   const int64_t cpr = N / 8;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= M * cpr) return;
-  const int64_t m = idx / cpr, c = (idx % cpr) * 8;
-  float v[8], o[8];
-  unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + c), v);
-  if constexpr (MODE == 2) {
-    float p[8];
-    unpack8(*reinterpret_cast<const u32x4*>(pre + m * ldp + c), p);
+  if constexpr (gr_simple<MODE>()) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= M * cpr) return;
+    const int64_t m = idx / cpr, c = (idx % cpr) * 8;
+    float v[8], o[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + m * ldx + c), v);
+    if constexpr (MODE == 2) {
+      float p[8];
+      unpack8(*reinterpret_cast<const u32x4*>(pre + m * ldp + c), p);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = v[j] * gelu_tanh_grad(p[j]);
+      for (int j = 0; j < 8; ++j) o[j] = v[j] * gelu_tanh_grad(p[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = MODE == 0 ? gelu_bf16(v[j]) : gelu_erf(v[j]);
+    }
+    *reinterpret_cast<u32x4*>(y + m * ldy + c) = pack8(o);
+    return;
   } else {
+    __shared__ __attribute__((aligned(16))) unsigned short ltab[MODE == 0 ? 2 * SVLA_GELU_TAB_N : 8];
+    if constexpr (MODE == 0) {
+      constexpr int NCH = (int)(sizeof(svla_gelu_bf16_tab) / 16);
+      for (int t = threadIdx.x; t < NCH; t += 256)
+        reinterpret_cast<u32x4*>(ltab)[t] = reinterpret_cast<const u32x4*>(svla_gelu_bf16_tab)[t];
+      __syncthreads();
+    }
+    const int64_t total = M * cpr;
+    const bool dense = ldx == N && ldy == N && (MODE != 2 || ldp == N);
+    auto off = [&](int64_t idx, int64_t ld) -> int64_t {
+      if (dense) return idx * 8;
+      const int64_t m = idx / cpr;
+      return m * ld + (idx - m * cpr) * 8;
+    };
+    constexpr int U = gr_u<MODE>();
+    const int64_t step = (int64_t)gridDim.x * 256 * U;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x; base < total; base += step) {
+      u32x4 xv[U], pv[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = MODE == 0 ? gelu_bf16(v[j]) : gelu_erf(v[j]);
+      for (int k = 0; k < U; ++k) {
+        const int64_t idx = base + k * 256;
+        if (idx < total) {
+          xv[k] = *reinterpret_cast<const u32x4*>(x + off(idx, ldx));
+          if constexpr (MODE == 2) pv[k] = *reinterpret_cast<const u32x4*>(pre + off(idx, ldp));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const int64_t idx = base + k * 256;
+        if (idx >= total) break;
+        float v[8], o[8];
+        unpack8(xv[k], v);
+        if constexpr (MODE == 2) {
+          float p[8];
+          unpack8(pv[k], p);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = v[j] * gelu_tanh_grad(p[j]);
+        } else if constexpr (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = gelu_bf16_lut(__float_as_uint(v[j]) >> 16, v[j], ltab);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = gelu_erf(v[j]);
+        }
+        *reinterpret_cast<u32x4*>(y + off(idx, ldy)) = pack8(o);
+      }
+    }
   }
-  *reinterpret_cast<u32x4*>(y + m * ldy + c) = pack8(o);
 }
 
 __global__ void add_kernel(int64_t n, const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
@@ -662,17 +724,22 @@ extern "C" int svla_gelu_rows(int64_t M, int64_t N, int32_t mode, const void* x,
                  "gelu_rows: M, N (multiple of 8), mode 0..2, pointers");
   SVLA_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && (mode != 2 || ldp % 8 == 0) && al16(x) && al16(y) &&
                      (mode != 2 || al16(pre)), "gelu_rows: rows must be 16-B aligned");
-  const dim3 g(nblk(M * (N / 8), 256)), b(256);
+  const int64_t chunks = M * (N / 8);
+  auto grid = [&](bool simple, int u) {
+    return dim3(simple ? nblk(chunks, 256)
+                       : (unsigned)std::min<int64_t>(nblk(chunks, 256 * u), (int64_t)svla::num_cus() * 8));
+  };
+  const dim3 b(256);
   hipStream_t s = (hipStream_t)stream;
   if (mode == 0)
-    hipLaunchKernelGGL(gelu_rows_kernel<0>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
-                       (bf16_t*)y, ldy);
+    hipLaunchKernelGGL(gelu_rows_kernel<0>, grid(gr_simple<0>(), gr_u<0>()), b, 0, s, M, N, (const bf16_t*)x, ldx,
+                       (const bf16_t*)pre, ldp, (bf16_t*)y, ldy);
   else if (mode == 1)
-    hipLaunchKernelGGL(gelu_rows_kernel<1>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
-                       (bf16_t*)y, ldy);
+    hipLaunchKernelGGL(gelu_rows_kernel<1>, grid(gr_simple<1>(), gr_u<1>()), b, 0, s, M, N, (const bf16_t*)x, ldx,
+                       (const bf16_t*)pre, ldp, (bf16_t*)y, ldy);
   else
-    hipLaunchKernelGGL(gelu_rows_kernel<2>, g, b, 0, s, M, N, (const bf16_t*)x, ldx, (const bf16_t*)pre, ldp,
-                       (bf16_t*)y, ldy);
+    hipLaunchKernelGGL(gelu_rows_kernel<2>, grid(gr_simple<2>(), gr_u<2>()), b, 0, s, M, N, (const bf16_t*)x, ldx,
+                       (const bf16_t*)pre, ldp, (bf16_t*)y, ldy);
   return svla::check_launch("gelu_rows");
 }
 
