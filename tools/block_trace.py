@@ -19,5 +19,21 @@ for r in it:
     dd = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     tot += dd
     n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", ""))[:70]
-    print(f"{dd:9.1f} us  grid={int(r['Grid_Size_X']):>9} wg={r['Workgroup_Size_X']:>4}  {n}")
-print(f"iteration: {P} kernels, wall {(t1 - t0) / 1e3:.1f} us, kernel sum {tot:.1f} us")
+    st = (int(r["Start_Timestamp"]) - t0) / 1e3
+    print(f"{dd:9.1f} us  @{st:8.1f}  grid={int(r['Grid_Size_X']):>9} wg={r['Workgroup_Size_X']:>4}  {n}")
+# union of the kernels' intervals: wall time with at least one kernel running; the rest is idle GPU (launch gaps,
+# host waits)
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in it)
+busy, cs, ce = 0, iv[0][0], iv[0][1]
+gaps = []
+for a, b in iv[1:]:
+    if a > ce:
+        busy += ce - cs
+        gaps.append(((cs - t0) / 1e3, (a - ce) / 1e3))
+        cs, ce = a, b
+    else:
+        ce = max(ce, b)
+busy += ce - cs
+print(f"iteration: {P} kernels, wall {(t1 - t0) / 1e3:.1f} us, kernel sum {tot:.1f} us, busy (union) {busy / 1e3:.1f} us, "
+      f"idle {(t1 - t0 - busy) / 1e3:.1f} us in {len(gaps)} gaps; largest: "
+      + ", ".join(f"{g:.1f} us after @{s:.0f}" for s, g in sorted(gaps, key=lambda x: -x[1])[:6]))
