@@ -58,6 +58,23 @@ def trace(d, out):
         tot = sum(v[0] for v in agg.values())
         lines.append(f"steady-state step: wall {(t1 - t0) / 1e6:.2f} ms, sum of kernel time {tot / 1e6:.2f} ms, "
                      f"{len(seg)} launches")
+        # GPU idle inside the step: the union of the kernels' intervals against the wall time, and the largest gaps
+        # with the kernel that ended before each one
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), _key(r["Kernel_Name"])) for r in seg)
+        busy, cs, ce, last = 0, iv[0][0], iv[0][1], iv[0][2]
+        gaps = []
+        for a, b, nm in iv[1:]:
+            if a > ce:
+                busy += ce - cs
+                gaps.append((a - ce, (ce - t0) / 1e6, last, nm))
+                cs, ce = a, b
+            if b >= ce:
+                ce, last = b, nm
+        busy += ce - cs
+        lines.append(f"GPU busy (union of kernel intervals) {busy / 1e6:.2f} ms, idle {(t1 - t0 - busy) / 1e6:.2f} ms in "
+                     f"{len(gaps)} gaps")
+        for g, at, before, after in sorted(gaps, reverse=True)[:12]:
+            lines.append(f"   gap {g / 1e3:8.1f} us at {at:8.2f} ms  after {before[:50]}  before {after[:50]}")
         for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0]):
             lines.append(f"{v[0] / 1e6:9.3f} ms {100 * v[0] / tot:5.1f}% n={v[1]:5d} avg={v[0] / v[1] / 1e3:9.1f} us  {k}")
     open(out + "_step_breakdown.txt", "w").write("\n".join(lines) + "\n")
@@ -68,7 +85,7 @@ def trace(d, out):
                    "launches": len(durs), "mean_ns": (sum(durs) / len(durs)) if durs else None,
                    "mean_ns_last_26": (sum(durs[-26:]) / len(durs[-26:])) if durs else None,
                    "durations_ns": durs}, f, indent=1)
-    print("\n".join(lines[:25]))
+    print("\n".join(lines[:40]))
     print(f"dominant kernel: {len(durs)} launches, mean {sum(durs) / max(1, len(durs)) / 1e3:.1f} us")
 
 
