@@ -357,6 +357,17 @@ int svla_gelu_rows(int64_t M, int64_t N, int32_t mode, const void* x, int64_t ld
 int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* res, const void* y, int64_t ldx, const void* w1,
                        const void* w2, float eps1, float eps2, void* h_out, const svla_operand* B, void* c,
                        int64_t ldc, const svla_epilogue* epi, void* stream);
+/* Decode step (M <= 8 token rows), the whole Gemma2 MLP with the norm pair before it in ONE persistent launch
+ * (modeling_gemma2.py:91-92, :487-490): h_out = bf16(res + bf16(rms(y; w1))), x = rms(h_out; w2),
+ * act = bf16(gelu_tanh(x Wg^T) * (x Wu^T)) [M][I] (caller scratch, row stride ldact), out = act Wd^T [M][H] --
+ * bitwise svla_gemv_rmsnorm2 (GEGLU) followed by svla_gemm_bf16's small-M down GEMV.  H <= 2560, I <= 10240, all
+ * multiples of 8; w_gate / w_up [I][H] share ldw, w_down [H][I].  `sync` points at svla_decode_mlp_sync_bytes()
+ * zeroed bytes, reused by every later call on that stream (the grid barrier's counter returns to zero). */
+size_t svla_decode_mlp_sync_bytes(void);
+int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, const void* y, int64_t ldx, const void* w1,
+                    const void* w2, float eps1, float eps2, void* h_out, const void* w_gate, const void* w_up,
+                    int64_t ldw, const void* w_down, int64_t ldd, void* act, int64_t ldact, void* out, int64_t ldo,
+                    unsigned* sync, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Softcapped lm_head cross-entropy (modeling_gemma2.py:993-997 + modeling_spatialvla.py:415-430,

@@ -1,0 +1,302 @@
+// Persistent decode-step Gemma2 MLP (svla_decode_mlp): the gate|up GEMV with the post-attention + pre-feedforward
+// norm pair in its prologue and the down GEMV in ONE launch, the weights of both streamed without a kernel
+// boundary (reference: Gemma2MLP.forward and the decoder layer's sandwich norms, modeling_gemma2.py:91-92,
+// :487-490).  Bitwise the two-launch path (svla_gemv_rmsnorm2 with the GEGLU epilogue, then the long-K split GEMV
+// of the down projection):
+//  * phase A (gemv_norm2_kernel's arithmetic): every block forms h = bf16(res + rms(y; w1)) and x = rms(h; w2) in
+//    LDS (block 0 stores h); each wave then walks gate|up row pairs r = wave, wave + waves, ... with the next pair's
+//    weights loaded while the current pair's dot products run, and stores act[m][r] = bf16(gelu(g) * u);
+//  * a grid barrier: act is stored write-through, each wave drains its stores, thread 0 of each block arrives on a
+//    counter and waits for the last arrival's generation bump, then one acquire fence per block;
+//  * phase C (gemv_splitk_kernel's arithmetic): each block walks down-projection rows n = block, block + blocks, ...
+//    (four waves split the row's K range, partial dots summed through LDS in wave order), next row prefetched.
+// The grid is DM_BPC blocks per CU, sized so every block is resident; the barrier wait is bounded (a missed
+// barrier would give wrong numbers, never a hung GPU) and the sync words return to {0, generation} after every
+// launch, so a zeroed buffer serves every later call and graph replay.
+#include "svla_common.h"
+
+#include <algorithm>
+
+namespace {
+
+#ifndef DM_BPC
+#define DM_BPC 2  // blocks per CU (all resident: registers and LDS allow it), i.e. the loads in flight per CU
+#endif
+constexpr int DM_MAXM = 8;
+constexpr int DM_KCH = 5;   // 16-B chunks per lane of a gate / up row: H <= 2560
+constexpr int DM_NC = 2;    // norm chunks per thread: H <= 4096
+constexpr int DM_DCH = 5;   // 16-B chunks per thread of a down row: I <= 10240
+
+// act is stored write-through (agent-scope relaxed atomic stores, sc1), so a wave only drains its own stores before
+// the block arrives; the arrival and the generation are relaxed agent-scope atomics, and one agent-scope acquire
+// fence per block after the wait (an L1 / L2 invalidate, not one per thread) keeps phase C from reading a stale act.
+__device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned gen = __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned arrived = __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == nblocks - 1) {
+      __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (unsigned spin = 0; spin < (1u << 22); ++spin) {  // bounded: ~seconds at most, never a hang
+        if (__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // agent scope (the default for this builtin on the device)
+  }
+  __syncthreads();
+}
+
+template <int MR>
+__global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, int I, const bf16_t* __restrict__ res,
+                                                            const bf16_t* __restrict__ y, int64_t ldx,
+                                                            const bf16_t* __restrict__ w1,
+                                                            const bf16_t* __restrict__ w2, float eps1, float eps2,
+                                                            bf16_t* __restrict__ h_out, const bf16_t* __restrict__ wg,
+                                                            const bf16_t* __restrict__ wu, int64_t ldw,
+                                                            const bf16_t* __restrict__ wd, int64_t ldd,
+                                                            bf16_t* act, int64_t ldact, bf16_t* __restrict__ out,
+                                                            int64_t ldo, unsigned* sync) {
+  extern __shared__ __attribute__((aligned(16))) char dm_smem[];  // [M][H] bf16 x, reduction slots, down partials
+  bf16_t* const xs = reinterpret_cast<bf16_t*>(dm_smem);
+  float (*red)[4] = reinterpret_cast<float (*)[4]>(dm_smem + (size_t)M * H * 2);
+  float (*part)[DM_MAXM] = reinterpret_cast<float (*)[DM_MAXM]>(dm_smem + (size_t)M * H * 2 + 2 * 4 * sizeof(float));
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int nch = H >> 3;
+  const int64_t K = H;
+
+  // ---------------- phase A prologue: norm inputs, then the first gate|up row pair (gemv_norm2_kernel's order)
+  u32x4 yv[MR][DM_NC], rv[MR][DM_NC], w1v[DM_NC], w2v[DM_NC];
+#pragma unroll
+  for (int cI = 0; cI < DM_NC; ++cI) {
+    const int ch = t + cI * 256;
+    w1v[cI] = w2v[cI] = u32x4{0u, 0u, 0u, 0u};
+    if (ch < nch) {
+      w1v[cI] = *reinterpret_cast<const u32x4*>(w1 + ch * 8);
+      w2v[cI] = *reinterpret_cast<const u32x4*>(w2 + ch * 8);
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      yv[m][cI] = rv[m][cI] = u32x4{0u, 0u, 0u, 0u};
+      if (m < M && ch < nch) {
+        yv[m][cI] = *reinterpret_cast<const u32x4*>(y + m * ldx + ch * 8);
+        rv[m][cI] = *reinterpret_cast<const u32x4*>(res + m * ldx + ch * 8);
+      }
+    }
+  }
+  const int64_t wstep = (int64_t)gridDim.x * 4;
+  int64_t r = (int64_t)blockIdx.x * 4 + wv;
+  u32x4 wa[2][DM_KCH], wb[2][DM_KCH];  // two buffers of [gate, up][chunk] (static indices: no scratch)
+  auto load_pair = [&](int64_t row, u32x4 (&dst)[2][DM_KCH]) {
+    const int64_t n = row < I ? row : I - 1;
+    const bf16_t* wr[2] = {wg + n * ldw, wu + n * ldw};
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < DM_KCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        // branch-free (a chunk past K re-reads the last one; the dot products skip it), so the waits are exact
+        dst[q][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + (k < K ? k : K - 8)));
+      }
+  };
+  load_pair(r, wa);
+
+  // ---------------- the norm pair (block_sum's order: wave butterfly, then the four waves in order)
+  auto bsum = [&](float v, int slot) {
+    v = wave_sum(v);
+    if (lane == 0) red[slot][wv] = v;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    return ((red[slot][0] + red[slot][1]) + red[slot][2]) + red[slot][3];
+  };
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    if (m < M) {
+      float v[DM_NC][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int cI = 0; cI < DM_NC; ++cI)
+        if (t + cI * 256 < nch) {
+          unpack8(yv[m][cI], v[cI]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += v[cI][j] * v[cI][j];
+        }
+      const float rstd1 = rsqrtf(bsum(ss, 0) / (float)K + eps1);
+      float ss2 = 0.f;
+#pragma unroll
+      for (int cI = 0; cI < DM_NC; ++cI) {
+        const int ch = t + cI * 256;
+        if (ch < nch) {
+          float wf[8], rr[8];
+          unpack8(w1v[cI], wf);
+          unpack8(rv[m][cI], rr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[cI][j] = round_bf(rr[j] + round_bf((v[cI][j] * rstd1) * (1.0f + wf[j])));
+            ss2 += v[cI][j] * v[cI][j];
+          }
+          if (blockIdx.x == 0) *reinterpret_cast<u32x4*>(h_out + m * ldx + ch * 8) = pack8(v[cI]);
+        }
+      }
+      const float rstd2 = rsqrtf(bsum(ss2, 1) / (float)K + eps2);
+#pragma unroll
+      for (int cI = 0; cI < DM_NC; ++cI) {
+        const int ch = t + cI * 256;
+        if (ch < nch) {
+          float wf[8], o[8];
+          unpack8(w2v[cI], wf);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (v[cI][j] * rstd2) * (1.0f + wf[j]);
+          *reinterpret_cast<u32x4*>(xs + m * H + ch * 8) = pack8(o);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ---------------- phase A: gate|up row pairs of this wave, the next pair's weights in flight
+  auto pair = [&](const u32x4 (&wcur)[2][DM_KCH], u32x4 (&wnext)[2][DM_KCH]) {
+    load_pair(r + wstep, wnext);  // unconditional (clamped row): the compiler can then wait for this pair only
+    float acc[2][MR];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int m = 0; m < MR; ++m) acc[q][m] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DM_KCH; ++i) {
+      const int64_t k = (int64_t)lane * 8 + i * 512;
+      if (k < K) {
+        float wf[2][8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) unpack8(wcur[q][i], wf[q]);
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (m < M) {
+            float xf[8];
+            unpack8(*reinterpret_cast<const u32x4*>(xs + m * H + k), xf);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[q][m] = fmaf(wf[q][j], xf[j], acc[q][m]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      if (m < M) {
+        const float g = round_bf(wave_sum(acc[0][m])), u = round_bf(wave_sum(acc[1][m]));
+        if (lane == 0)  // write-through: read by other CUs / XCDs after the grid barrier
+          __hip_atomic_store(reinterpret_cast<unsigned short*>(act + m * ldact + r),
+                             (unsigned short)f2bf(gelu_bf16(g) * u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    r += wstep;
+  };
+  while (r < I) {
+    pair(wa, wb);
+    if (r >= I) break;
+    pair(wb, wa);
+  }
+
+  grid_barrier(sync, gridDim.x);
+
+  // ---------------- phase C: down rows of this block, four waves split each row's K range
+  u32x4 da[DM_DCH], db[DM_DCH];
+  auto load_down = [&](int64_t row, u32x4 (&dst)[DM_DCH]) {
+    const bf16_t* wr = wd + row * ldd;
+#pragma unroll
+    for (int i = 0; i < DM_DCH; ++i) {
+      const int64_t k = (int64_t)t * 8 + i * 2048;
+      dst[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + (k < I ? k : I - 8)));
+    }
+  };
+  int64_t n = blockIdx.x;
+  load_down(n < H ? n : H - 1, da);
+  // one token row (the batch-1 decode step): the thread's act chunks, the same for every down row, in registers
+  u32x4 av[DM_DCH];
+  if constexpr (MR == 1) {
+#pragma unroll
+    for (int i = 0; i < DM_DCH; ++i) {
+      const int64_t k = (int64_t)t * 8 + i * 2048;
+      av[i] = k < I ? *reinterpret_cast<const u32x4*>(act + k) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  auto row = [&](const u32x4 (&dcur)[DM_DCH], u32x4 (&dnext)[DM_DCH]) {
+    load_down(n + gridDim.x < H ? n + gridDim.x : H - 1, dnext);  // unconditional: see phase A
+    float acc[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DM_DCH; ++i) {
+      const int64_t k = (int64_t)t * 8 + i * 2048;
+      if (k < I) {
+        float wf[8];
+        unpack8(dcur[i], wf);
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+          if (m < M) {
+            float xf[8];
+            if constexpr (MR == 1) unpack8(av[i], xf);
+            else unpack8(*reinterpret_cast<const u32x4*>(act + m * ldact + k), xf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      if (m < M) {
+        const float v = wave_sum(acc[m]);
+        if (lane == 0) part[wv][m] = v;
+      }
+    }
+    __syncthreads();
+    if (t < M) out[t * ldo + n] = f2bf(((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
+    __syncthreads();  // part is rewritten by the next row
+    n += gridDim.x;
+  };
+  while (n < H) {
+    row(da, db);
+    if (n >= H) break;
+    row(db, da);
+  }
+}
+
+}  // namespace
+
+extern "C" size_t svla_decode_mlp_sync_bytes(void) { return 2 * sizeof(unsigned); }
+
+extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, const void* y, int64_t ldx,
+                               const void* w1, const void* w2, float eps1, float eps2, void* h_out, const void* w_gate,
+                               const void* w_up, int64_t ldw, const void* w_down, int64_t ldd, void* act,
+                               int64_t ldact, void* out, int64_t ldo, unsigned* sync, void* stream) {
+  SVLA_CHECK_ARG(M >= 1 && M <= DM_MAXM && H > 0 && H % 8 == 0 && H <= 512 * DM_KCH && H <= 256 * 8 * DM_NC &&
+                     I > 0 && I % 8 == 0 && I <= 2048 * DM_DCH,
+                 "decode_mlp: M in [1, %d], H a multiple of 8 <= %d, I a multiple of 8 <= %d", DM_MAXM, 512 * DM_KCH,
+                 2048 * DM_DCH);
+  SVLA_CHECK_ARG(res && y && w1 && w2 && h_out && w_gate && w_up && w_down && act && out && sync,
+                 "decode_mlp: NULL argument");
+  SVLA_CHECK_ARG(ldx % 8 == 0 && ldx >= H && ldw % 8 == 0 && ldw >= H && ldd % 8 == 0 && ldd >= I &&
+                     ldact % 8 == 0 && ldact >= I && ldo >= H,
+                 "decode_mlp: leading dimensions");
+  const unsigned blocks = (unsigned)std::min<int64_t>((int64_t)svla::num_cus() * DM_BPC, std::max<int64_t>(I / 4, 1));
+  const size_t lds = (size_t)M * H * 2 + 2 * 4 * sizeof(float) + 4 * DM_MAXM * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+#define SVLA_DM(MR)                                                                                                  \
+  hipLaunchKernelGGL((decode_mlp_kernel<MR>), dim3(blocks), dim3(256), lds, s, (int)M, (int)H, (int)I,              \
+                     (const bf16_t*)res, (const bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,   \
+                     (bf16_t*)h_out, (const bf16_t*)w_gate, (const bf16_t*)w_up, ldw, (const bf16_t*)w_down, ldd,  \
+                     (bf16_t*)act, ldact, (bf16_t*)out, ldo, sync)
+  if (M == 1) SVLA_DM(1);
+  else SVLA_DM(DM_MAXM);
+#undef SVLA_DM
+  return svla::check_launch("decode_mlp");
+}

@@ -611,6 +611,11 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     return out
 
 
+# the decode MLP as one persistent launch (svla_decode_mlp) instead of the norm-GEMV + down-GEMV pair: opt-in,
+# measured slower (2.21 vs 1.95 ms per decode token, profiles/r6v_decode_mlp_persist_ab.txt)
+DECODE_MLP_PERSIST = [os.environ.get("SVLA_DECODE_MLP_PERSIST", "0") != "0"]
+
+
 @torch.no_grad()
 def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd):
     """Decode-step Gemma2 MLP (modeling_gemma2.py:91-92) whose input is the post-attention + pre-feedforward norm pair
@@ -618,9 +623,13 @@ def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd):
     down(gelu_tanh(gate x) * up x) with x = rms(h_out; w2)."""
     M = y.shape[0]
     I = wg.shape[0]
+    out = _empty(M, wd.shape[0], like=y)
+    if DECODE_MLP_PERSIST[0] and y.shape[1] <= 2560 and I <= 10240 and wg.stride(1) == wu.stride(1) == wd.stride(1) == 1:
+        hact = _empty(M, I, like=y)
+        K.decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, hact, out)  # one persistent launch, bitwise
+        return out
     hact, g, u = (_empty(M, I, like=y) for _ in range(3))
     K.gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, [wg, wu], hact, geglu_out=(g, u))
-    out = _empty(M, wd.shape[0], like=y)
     K.linear_fwd(hact, [wd], out)
     return out
 

@@ -202,6 +202,35 @@ def gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, weights: List[torch.Tensor]
                                        _ld(out), ctypes.byref(e), _stream()), "svla_gemv_rmsnorm2")
 
 
+# svla_decode_mlp grid-barrier words: zeroed once per (device, stream) and never freed (captured decode graphs keep
+# the raw pointer; the counter is back at zero after every launch)
+_DECODE_MLP_SYNC = {}
+
+
+def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out):
+    """Decode-step Gemma2 MLP in one persistent launch (svla_decode_mlp): h_out = bf16(res + rms(y; w1)),
+    act = GeGLU(rms(h_out; w2) @ [wg; wu]^T), out = act @ wd^T -- bitwise gemv_rmsnorm2 (GEGLU) + the down GEMV."""
+    M, H = y.shape
+    I = wg.shape[0]
+    _req(M <= 8 and H % 8 == 0 and I % 8 == 0 and H <= 2560 and I <= 10240,
+         "decode_mlp: M <= 8, H <= 2560, I <= 10240, multiples of 8")
+    for t, nm in ((res, "res"), (y, "y"), (h_out, "h_out"), (w1, "w1"), (w2, "w2"), (wg, "wg"), (wu, "wu"),
+                  (wd, "wd"), (act, "act"), (out, "out")):
+        _chk_bf16(t, "decode_mlp " + nm)
+    _req(res.shape == y.shape == h_out.shape and _ld(res) == _ld(y) == _ld(h_out), "decode_mlp: res/y/h_out rows")
+    _req(wg.shape == wu.shape == (I, H) and _ld(wg) == _ld(wu) and wd.shape == (H, I), "decode_mlp: weight shapes")
+    _req(act.shape[0] >= M and act.shape[1] >= I and out.shape[0] >= M and out.shape[1] >= H, "decode_mlp: outputs")
+    key = (y.device.index, _stream())
+    sync = _DECODE_MLP_SYNC.get(key)
+    if sync is None:
+        sync = _DECODE_MLP_SYNC[key] = torch.zeros(max(16, int(L.lib().svla_decode_mlp_sync_bytes())),
+                                                   dtype=torch.uint8, device=y.device)
+    L.check(L.lib().svla_decode_mlp(M, H, I, res.data_ptr(), y.data_ptr(), _ld(y), w1.data_ptr(), w2.data_ptr(),
+                                    float(eps1), float(eps2), h_out.data_ptr(), wg.data_ptr(), wu.data_ptr(), _ld(wg),
+                                    wd.data_ptr(), _ld(wd), act.data_ptr(), _ld(act), out.data_ptr(), _ld(out),
+                                    sync.data_ptr(), _stream()), "svla_decode_mlp")
+
+
 # Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch
 # record a pair of HIP events on the stream it is launched on (the current torch stream).
 launch_timer: dict = {}

@@ -343,6 +343,54 @@ def test_gemv_rmsnorm2_bitwise(cuda, M, geglu):
     assert torch.equal(h, h_ref)
 
 
+@pytest.mark.parametrize("M,H,I", [(1, 2304, 9216), (3, 2304, 9216), (8, 2304, 9216), (2, 256, 520)])
+def test_decode_mlp_persistent_bitwise(cuda, M, H, I):
+    """svla_decode_mlp (one persistent launch: norm pair + gate|up GeGLU GEMV, grid barrier, down GEMV) == the
+    two-launch path (svla_gemv_rmsnorm2 GEGLU, then the small-M down GEMV), bit for bit: h, act and out -- over
+    repeated launches (the grid barrier's words are reused) and a ragged shape (fewer blocks than CUs)."""
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(23)
+    res, y = _r(M, H), _r(M, H, scale=3.0)
+    w1, w2 = _r(H, scale=0.3), _r(H, scale=0.3)
+    wg, wu, wd = _r(I, H, scale=0.02), _r(I, H, scale=0.02), _r(H, I, scale=0.02)
+    h_ref = torch.empty_like(res)
+    act_ref, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    Kn.gemv_rmsnorm2(res, y, w1, w2, 1e-6, 1e-6, h_ref, [wg, wu], act_ref, geglu_out=(g, u))
+    out_ref = torch.empty(M, H, dtype=BF, device=cuda)
+    Kn.linear_fwd(act_ref, [wd], out_ref)
+    for rep in range(3):
+        h, act, out = torch.full_like(res, 7.0), torch.full_like(act_ref, 7.0), torch.full_like(out_ref, 7.0)
+        Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+        assert torch.equal(h, h_ref), rep
+        assert torch.equal(act, act_ref), rep
+        assert torch.equal(out, out_ref), rep
+
+
+def test_decode_mlp_persistent_graph_tokens(cuda):
+    """predict_action (graph-replayed decode steps) gives the same tokens and logits with the persistent decode MLP
+    as with the two-launch MLP."""
+    from spatialvla_amd import functional as Fn
+    model, g = _tiny_model(cuda)
+    ids = g["in.input_ids"][:, :-13]
+    inputs = {"input_ids": ids, "pixel_values": g["in.pixel_values"], "intrinsic": g["in.intrinsic"]}
+    outs = {}
+    keep = Fn.DECODE_MLP_PERSIST[0]
+    try:
+        for persist in (False, True):
+            Fn.DECODE_MLP_PERSIST[0] = persist
+            model.clear_decode_cache()
+            with torch.no_grad():
+                o1 = model(input_ids=ids.to(cuda), pixel_values=inputs["pixel_values"].to(cuda),
+                           intrinsic=inputs["intrinsic"].to(cuda), use_cache=True)
+                o2 = model(input_ids=ids[:, -1:].to(cuda), past_key_values=o1.past_key_values)
+            outs[persist] = (o2.logits.clone(), model.predict_action(inputs, max_new_tokens=6, eos_token_id=-1))
+    finally:
+        Fn.DECODE_MLP_PERSIST[0] = keep
+        model.clear_decode_cache()
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+
+
 def test_decode_norm_fusion_bitwise(cuda):
     """A decode step with the norm pairs inside the projections' GEMVs gives the logits of the unfused loop, bit for
     bit (predict_action tokens as well)."""
