@@ -30,18 +30,37 @@ constexpr int DM_DCH = 5;   // 16-B chunks per thread of a down row: I <= 10240
 // act is stored write-through (agent-scope relaxed atomic stores, sc1), so a wave only drains its own stores before
 // the block arrives; the arrival and the generation are relaxed agent-scope atomics, and one agent-scope acquire
 // fence per block after the wait (an L1 / L2 invalidate, not one per thread) keeps phase C from reading a stale act.
+// Two-level arrival: blocks count on one of DM_GROUPS group counters (separate 256-B lines, so the same-address
+// atomics of a group serialise only among that group's blocks), the last arriver of a group counts on the top
+// counter, and the last of those bumps the generation.  sync layout (unsigned): [0] generation, [64 * (g + 1)] group
+// g's counter, [64 * (DM_GROUPS + 1)] the top counter; every counter is back at zero after the launch.
+#ifndef DM_GROUPS
+#define DM_GROUPS 8
+#endif
+constexpr int DM_SYNC_WORDS = 64 * (DM_GROUPS + 2);
 __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // vector memory retires in issue order: all but the DM_DCH down-weight loads issued after the act stores
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DM_DCH) : "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned gen = __hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned arrived = __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == nblocks - 1) {
-      __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&sync[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
+    const unsigned g = blockIdx.x % DM_GROUPS;
+    const unsigned gsize = nblocks / DM_GROUPS + (g < nblocks % DM_GROUPS ? 1u : 0u);
+    const unsigned ngroups = nblocks < DM_GROUPS ? nblocks : DM_GROUPS;
+    unsigned* const gcnt = sync + 64 * (g + 1);
+    unsigned* const top = sync + 64 * (DM_GROUPS + 1);
+    const unsigned gen = __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool last = false;
+    if (__hip_atomic_fetch_add(gcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sync[0], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = true;
+      }
+    }
+    if (!last) {
       for (unsigned spin = 0; spin < (1u << 22); ++spin) {  // bounded: ~seconds at most, never a hang
-        if (__hip_atomic_load(&sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+        if (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
         __builtin_amdgcn_s_sleep(1);
       }
     }
@@ -205,9 +224,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     pair(wb, wa);
   }
 
-  grid_barrier(sync, gridDim.x);
-
-  // ---------------- phase C: down rows of this block, four waves split each row's K range
+  // the block's first down row is independent of act: its weights stream in while the grid barrier waits
   u32x4 da[DM_DCH], db[DM_DCH];
   auto load_down = [&](int64_t row, u32x4 (&dst)[DM_DCH]) {
     const bf16_t* wr = wd + row * ldd;
@@ -219,6 +236,9 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
   };
   int64_t n = blockIdx.x;
   load_down(n < H ? n : H - 1, da);
+  grid_barrier(sync, gridDim.x);
+
+  // ---------------- phase C: down rows of this block, four waves split each row's K range
   // one token row (the batch-1 decode step): the thread's act chunks, the same for every down row, in registers
   u32x4 av[DM_DCH];
   if constexpr (MR == 1) {
@@ -272,7 +292,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
 
 }  // namespace
 
-extern "C" size_t svla_decode_mlp_sync_bytes(void) { return 2 * sizeof(unsigned); }
+extern "C" size_t svla_decode_mlp_sync_bytes(void) { return DM_SYNC_WORDS * sizeof(unsigned); }
 
 extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, const void* y, int64_t ldx,
                                const void* w1, const void* w2, float eps1, float eps2, void* h_out, const void* w_gate,

@@ -611,9 +611,9 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     return out
 
 
-# the decode MLP as one persistent launch (svla_decode_mlp) instead of the norm-GEMV + down-GEMV pair: opt-in,
-# measured slower (2.21 vs 1.95 ms per decode token, profiles/r6v_decode_mlp_persist_ab.txt)
-DECODE_MLP_PERSIST = [os.environ.get("SVLA_DECODE_MLP_PERSIST", "0") != "0"]
+# the decode MLP as one persistent launch (svla_decode_mlp) instead of the norm-GEMV + down-GEMV pair: 1.80 vs
+# 1.95 ms per decode token (profiles/r6z_decode_mlp_persist_ab.txt); SVLA_DECODE_MLP_PERSIST=0: the pair
+DECODE_MLP_PERSIST = [os.environ.get("SVLA_DECODE_MLP_PERSIST", "1") != "0"]
 
 
 @torch.no_grad()
