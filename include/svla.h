@@ -360,14 +360,17 @@ int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* res, const v
 /* Decode step (M <= 8 token rows), the whole Gemma2 MLP with the norm pair before it in ONE persistent launch
  * (modeling_gemma2.py:91-92, :487-490): h_out = bf16(res + bf16(rms(y; w1))), x = rms(h_out; w2),
  * act = bf16(gelu_tanh(x Wg^T) * (x Wu^T)) [M][I] (caller scratch, row stride ldact), out = act Wd^T [M][H] --
- * bitwise svla_gemv_rmsnorm2 (GEGLU) followed by svla_gemm_bf16's small-M down GEMV.  H <= 2560, I <= 10240, all
- * multiples of 8; w_gate / w_up [I][H] share ldw, w_down [H][I].  `sync` points at svla_decode_mlp_sync_bytes()
- * zeroed bytes, reused by every later call on that stream (the grid barrier's counter returns to zero). */
+ * bitwise svla_gemv_rmsnorm2 (GEGLU) followed by svla_gemm_bf16's small-M down GEMV.  With attn != NULL the o
+ * projection runs first in the same launch: y = attn w_o^T (w_o [H][KO], KO <= 2048; y is then an output), bitwise
+ * the small-M GEMV.  H <= 2560, I <= 10240, all multiples of 8; w_gate / w_up [I][H] share ldw, w_down [H][I].
+ * `sync` points at svla_decode_mlp_sync_bytes() zeroed bytes, reused by every later call on that stream (the grid
+ * barriers' counters return to zero). */
 size_t svla_decode_mlp_sync_bytes(void);
-int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, const void* y, int64_t ldx, const void* w1,
+int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, void* y, int64_t ldx, const void* w1,
                     const void* w2, float eps1, float eps2, void* h_out, const void* w_gate, const void* w_up,
                     int64_t ldw, const void* w_down, int64_t ldd, void* act, int64_t ldact, void* out, int64_t ldo,
-                    unsigned* sync, void* stream);
+                    const void* attn, int64_t ld_attn, int64_t KO, const void* w_o, int64_t ldwo, unsigned* sync,
+                    void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Softcapped lm_head cross-entropy (modeling_gemma2.py:993-997 + modeling_spatialvla.py:415-430,

@@ -125,7 +125,8 @@ SIGNATURES = {
                                    c_vp, c_i64, c_vp, c_vp]),
     "svla_decode_mlp_sync_bytes": (ctypes.c_size_t, []),
     "svla_decode_mlp": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
-                                c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+                                c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
+                                c_vp]),
     "svla_gelu_rows": (c_i32, [c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "svla_softcap_ce_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_f32, c_vp, c_vp]),
     "svla_ce_finalize": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -26,28 +26,31 @@ constexpr int DM_MAXM = 8;
 constexpr int DM_KCH = 5;   // 16-B chunks per lane of a gate / up row: H <= 2560
 constexpr int DM_NC = 2;    // norm chunks per thread: H <= 4096
 constexpr int DM_DCH = 5;   // 16-B chunks per thread of a down row: I <= 10240
+constexpr int DM_OCH = 4;   // 16-B chunks per lane of an o-projection row: KO <= 2048
 
 // act is stored write-through (agent-scope relaxed atomic stores, sc1), so a wave only drains its own stores before
 // the block arrives; the arrival and the generation are relaxed agent-scope atomics, and one agent-scope acquire
 // fence per block after the wait (an L1 / L2 invalidate, not one per thread) keeps phase C from reading a stale act.
 // Two-level arrival: blocks count on one of DM_GROUPS group counters (separate 256-B lines, so the same-address
 // atomics of a group serialise only among that group's blocks), the last arriver of a group counts on the top
-// counter, and the last of those bumps the generation.  sync layout (unsigned): [0] generation, [64 * (g + 1)] group
-// g's counter, [64 * (DM_GROUPS + 1)] the top counter; every counter is back at zero after the launch.
+// counter, and the last of those bumps the generation word sync[0]; every counter is back at zero after the launch.
 #ifndef DM_GROUPS
 #define DM_GROUPS 8
 #endif
-constexpr int DM_SYNC_WORDS = 64 * (DM_GROUPS + 2);
+constexpr int DM_SET = 64 * (DM_GROUPS + 1);   // one barrier's counters (groups + top), 256-B apart
+constexpr int DM_SYNC_WORDS = 64 + 2 * DM_SET;  // generation word, then the counter sets of barriers 0 and 1
+// PEND: vector-memory ops issued after the stores this barrier publishes (they retire in issue order); SET: which
+// counter set (a launch with two barriers never reuses a set, so a reset can not race a fast block's next arrival)
+template <int PEND, int SET>
 __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
-  // vector memory retires in issue order: all but the DM_DCH down-weight loads issued after the act stores
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DM_DCH) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PEND) : "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned g = blockIdx.x % DM_GROUPS;
     const unsigned gsize = nblocks / DM_GROUPS + (g < nblocks % DM_GROUPS ? 1u : 0u);
     const unsigned ngroups = nblocks < DM_GROUPS ? nblocks : DM_GROUPS;
-    unsigned* const gcnt = sync + 64 * (g + 1);
-    unsigned* const top = sync + 64 * (DM_GROUPS + 1);
+    unsigned* const gcnt = sync + 64 + SET * DM_SET + 64 * g;
+    unsigned* const top = sync + 64 + SET * DM_SET + 64 * DM_GROUPS;
     const unsigned gen = __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool last = false;
     if (__hip_atomic_fetch_add(gcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
@@ -71,14 +74,16 @@ __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
 
 template <int MR>
 __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, int I, const bf16_t* __restrict__ res,
-                                                            const bf16_t* __restrict__ y, int64_t ldx,
+                                                            bf16_t* y, int64_t ldx,
                                                             const bf16_t* __restrict__ w1,
                                                             const bf16_t* __restrict__ w2, float eps1, float eps2,
                                                             bf16_t* __restrict__ h_out, const bf16_t* __restrict__ wg,
                                                             const bf16_t* __restrict__ wu, int64_t ldw,
                                                             const bf16_t* __restrict__ wd, int64_t ldd,
                                                             bf16_t* act, int64_t ldact, bf16_t* __restrict__ out,
-                                                            int64_t ldo, unsigned* sync) {
+                                                            int64_t ldo, const bf16_t* __restrict__ attn,
+                                                            int64_t ld_attn, int KO, const bf16_t* __restrict__ wo,
+                                                            int64_t ldwo, unsigned* sync) {
   extern __shared__ __attribute__((aligned(16))) char dm_smem[];  // [M][H] bf16 x, reduction slots, down partials
   bf16_t* const xs = reinterpret_cast<bf16_t*>(dm_smem);
   float (*red)[4] = reinterpret_cast<float (*)[4]>(dm_smem + (size_t)M * H * 2);
@@ -86,6 +91,67 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int nch = H >> 3;
   const int64_t K = H;
+
+  const int64_t wstep = (int64_t)gridDim.x * 4;
+  int64_t r = (int64_t)blockIdx.x * 4 + wv;
+  u32x4 wa[2][DM_KCH], wb[2][DM_KCH];  // two buffers of [gate, up][chunk] (static indices: no scratch)
+  auto load_pair = [&](int64_t row, u32x4 (&dst)[2][DM_KCH]) {
+    const int64_t n = row < I ? row : I - 1;
+    const bf16_t* wr[2] = {wg + n * ldw, wu + n * ldw};
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < DM_KCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        // branch-free (a chunk past K re-reads the last one; the dot products skip it), so the waits are exact
+        dst[q][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + (k < K ? k : K - 8)));
+      }
+  };
+  // ---------------- phase O (attn != NULL): y = attn @ wo^T, the o projection (gemv_pf_kernel<4, 1>'s arithmetic,
+  // one wave a row), stored write-through; the first gate|up pair is then issued and a grid barrier publishes y
+  if (attn != nullptr) {
+    for (int64_t ro = r; ro < H; ro += wstep) {
+      const bf16_t* wr = wo + ro * ldwo;
+      u32x4 ov[DM_OCH];
+#pragma unroll
+      for (int i = 0; i < DM_OCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        ov[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + (k < KO ? k : KO - 8)));
+      }
+      float acc[MR];
+#pragma unroll
+      for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+#pragma unroll
+      for (int i = 0; i < DM_OCH; ++i) {
+        const int64_t k = (int64_t)lane * 8 + i * 512;
+        if (k < KO) {
+          float wf[8];
+          unpack8(ov[i], wf);
+#pragma unroll
+          for (int m = 0; m < MR; ++m) {
+            if (m < M) {
+              float xf[8];
+              unpack8(*reinterpret_cast<const u32x4*>(attn + m * ld_attn + k), xf);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[m] = fmaf(wf[j], xf[j], acc[m]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        if (m < M) {
+          const float v = wave_sum(acc[m]);
+          if (lane == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned short*>(y + m * ldx + ro), (unsigned short)f2bf(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    load_pair(r, wa);
+    grid_barrier<2 * DM_KCH, 0>(sync, gridDim.x);
+  }
 
   // ---------------- phase A prologue: norm inputs, then the first gate|up row pair (gemv_norm2_kernel's order)
   u32x4 yv[MR][DM_NC], rv[MR][DM_NC], w1v[DM_NC], w2v[DM_NC];
@@ -106,22 +172,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
       }
     }
   }
-  const int64_t wstep = (int64_t)gridDim.x * 4;
-  int64_t r = (int64_t)blockIdx.x * 4 + wv;
-  u32x4 wa[2][DM_KCH], wb[2][DM_KCH];  // two buffers of [gate, up][chunk] (static indices: no scratch)
-  auto load_pair = [&](int64_t row, u32x4 (&dst)[2][DM_KCH]) {
-    const int64_t n = row < I ? row : I - 1;
-    const bf16_t* wr[2] = {wg + n * ldw, wu + n * ldw};
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int i = 0; i < DM_KCH; ++i) {
-        const int64_t k = (int64_t)lane * 8 + i * 512;
-        // branch-free (a chunk past K re-reads the last one; the dot products skip it), so the waits are exact
-        dst[q][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + (k < K ? k : K - 8)));
-      }
-  };
-  load_pair(r, wa);
+  if (attn == nullptr) load_pair(r, wa);
 
   // ---------------- the norm pair (block_sum's order: wave butterfly, then the four waves in order)
   auto bsum = [&](float v, int slot) {
@@ -236,7 +287,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
   };
   int64_t n = blockIdx.x;
   load_down(n < H ? n : H - 1, da);
-  grid_barrier(sync, gridDim.x);
+  grid_barrier<DM_DCH, 1>(sync, gridDim.x);
 
   // ---------------- phase C: down rows of this block, four waves split each row's K range
   // one token row (the batch-1 decode step): the thread's act chunks, the same for every down row, in registers
@@ -294,10 +345,11 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
 
 extern "C" size_t svla_decode_mlp_sync_bytes(void) { return DM_SYNC_WORDS * sizeof(unsigned); }
 
-extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, const void* y, int64_t ldx,
-                               const void* w1, const void* w2, float eps1, float eps2, void* h_out, const void* w_gate,
+extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, void* y, int64_t ldx, const void* w1,
+                               const void* w2, float eps1, float eps2, void* h_out, const void* w_gate,
                                const void* w_up, int64_t ldw, const void* w_down, int64_t ldd, void* act,
-                               int64_t ldact, void* out, int64_t ldo, unsigned* sync, void* stream) {
+                               int64_t ldact, void* out, int64_t ldo, const void* attn, int64_t ld_attn, int64_t KO,
+                               const void* w_o, int64_t ldwo, unsigned* sync, void* stream) {
   SVLA_CHECK_ARG(M >= 1 && M <= DM_MAXM && H > 0 && H % 8 == 0 && H <= 512 * DM_KCH && H <= 256 * 8 * DM_NC &&
                      I > 0 && I % 8 == 0 && I <= 2048 * DM_DCH,
                  "decode_mlp: M in [1, %d], H a multiple of 8 <= %d, I a multiple of 8 <= %d", DM_MAXM, 512 * DM_KCH,
@@ -307,14 +359,19 @@ extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res,
   SVLA_CHECK_ARG(ldx % 8 == 0 && ldx >= H && ldw % 8 == 0 && ldw >= H && ldd % 8 == 0 && ldd >= I &&
                      ldact % 8 == 0 && ldact >= I && ldo >= H,
                  "decode_mlp: leading dimensions");
-  const unsigned blocks = (unsigned)std::min<int64_t>((int64_t)svla::num_cus() * DM_BPC, std::max<int64_t>(I / 4, 1));
+  SVLA_CHECK_ARG(!attn || (w_o && KO > 0 && KO % 8 == 0 && KO <= 512 * DM_OCH && ld_attn % 8 == 0 && ld_attn >= KO &&
+                           ldwo % 8 == 0 && ldwo >= KO),
+                 "decode_mlp: the o projection needs w_o, KO a multiple of 8 <= %d and 16-B rows", 512 * DM_OCH);
+  const unsigned blocks =
+      (unsigned)std::min<int64_t>((int64_t)svla::num_cus() * DM_BPC, std::max<int64_t>(I / 4, 1));
   const size_t lds = (size_t)M * H * 2 + 2 * 4 * sizeof(float) + 4 * DM_MAXM * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define SVLA_DM(MR)                                                                                                  \
   hipLaunchKernelGGL((decode_mlp_kernel<MR>), dim3(blocks), dim3(256), lds, s, (int)M, (int)H, (int)I,              \
-                     (const bf16_t*)res, (const bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,   \
+                     (const bf16_t*)res, (bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,         \
                      (bf16_t*)h_out, (const bf16_t*)w_gate, (const bf16_t*)w_up, ldw, (const bf16_t*)w_down, ldd,  \
-                     (bf16_t*)act, ldact, (bf16_t*)out, ldo, sync)
+                     (bf16_t*)act, ldact, (bf16_t*)out, ldo, (const bf16_t*)attn, ld_attn, (int)KO,                \
+                     (const bf16_t*)w_o, ldwo, sync)
   if (M == 1) SVLA_DM(1);
   else SVLA_DM(DM_MAXM);
 #undef SVLA_DM

@@ -560,7 +560,7 @@ DECODE_NORM_FUSED = [os.environ.get("SVLA_DECODE_NORM_FUSED", "1") != "0"]
 
 @torch.no_grad()
 def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_class, p0, cfg: GemmaAttnCfg,
-                           pre=None):
+                           pre=None, skip_o=False):
     """Gemma2Attention.forward with a KV cache (modeling_gemma2.py:364-413, cache update :387-395), inference
     only.  x holds the cfg.L new tokens of each of the cfg.B sequences, at absolute positions p0 .. p0+L-1;
     their rotated k and v are written into rows p0.. of k_cache/v_cache ([B, capacity, Hkv*D]).  The prefill
@@ -606,9 +606,21 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
         a = K.attn_args(B, Lq, cfg.Hq, cfg.Hkv, cfg.D, qkv[:, :qd], qkv.stride(0), qkv[:, qd:qd + kd],
                         qkv.stride(0), qkv[:, qd + kd:], qkv.stride(0), cfg.scale, cfg.softcap, cls, cfg.window)
         K.attn_fwd(a, attn, lse)
+    if skip_o:  # the caller runs the o projection (gemma_mlp_decode with o=(attn, wo): inside its launch)
+        return attn
     out = _empty(M, wo.shape[0], like=like)
     K.linear_fwd(attn, [wo], out)
     return out
+
+
+# ... with the o projection inside the same launch (a second grid barrier) instead of its own GEMV: opt-in, measured
+# slower (1.97 vs 1.84 ms per token: 2304 rows over 2048 waves leave one row in flight a wave; profiles/r7b_*)
+DECODE_O_FUSED = [os.environ.get("SVLA_DECODE_O_FUSED", "0") != "0"]
+
+
+def persist_ok(y, wg, wu, wd) -> bool:
+    return (DECODE_MLP_PERSIST[0] and y.shape[1] <= 2560 and wg.shape[0] <= 10240
+            and wg.stride(1) == wu.stride(1) == wd.stride(1) == 1)
 
 
 # the decode MLP as one persistent launch (svla_decode_mlp) instead of the norm-GEMV + down-GEMV pair: 1.80 vs
@@ -617,16 +629,22 @@ DECODE_MLP_PERSIST = [os.environ.get("SVLA_DECODE_MLP_PERSIST", "1") != "0"]
 
 
 @torch.no_grad()
-def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd):
+def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, o=None):
     """Decode-step Gemma2 MLP (modeling_gemma2.py:91-92) whose input is the post-attention + pre-feedforward norm pair
     (:487-490), formed inside the gate|up GEMV: h_out = res + rms(y; w1) (the residual stream), returns
     down(gelu_tanh(gate x) * up x) with x = rms(h_out; w2)."""
+    if o is not None:  # y = attn @ wo^T (the o projection), in the persistent launch or as its own GEMV
+        attn, wo = o
+        y = _empty(attn.shape[0], wo.shape[0], like=attn)
+        if not persist_ok(y, wg, wu, wd) or attn.shape[1] > 2048 or wo.stride(1) != 1:
+            K.linear_fwd(attn, [wo], y)
+            o = None
     M = y.shape[0]
     I = wg.shape[0]
     out = _empty(M, wd.shape[0], like=y)
-    if DECODE_MLP_PERSIST[0] and y.shape[1] <= 2560 and I <= 10240 and wg.stride(1) == wu.stride(1) == wd.stride(1) == 1:
+    if persist_ok(y, wg, wu, wd):
         hact = _empty(M, I, like=y)
-        K.decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, hact, out)  # one persistent launch, bitwise
+        K.decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, hact, out, o=o)  # one persistent launch, bitwise
         return out
     hact, g, u = (_empty(M, I, like=y) for _ in range(3))
     K.gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, [wg, wu], hact, geglu_out=(g, u))

@@ -207,9 +207,10 @@ def gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, weights: List[torch.Tensor]
 _DECODE_MLP_SYNC = {}
 
 
-def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out):
+def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out, o=None):
     """Decode-step Gemma2 MLP in one persistent launch (svla_decode_mlp): h_out = bf16(res + rms(y; w1)),
-    act = GeGLU(rms(h_out; w2) @ [wg; wu]^T), out = act @ wd^T -- bitwise gemv_rmsnorm2 (GEGLU) + the down GEMV."""
+    act = GeGLU(rms(h_out; w2) @ [wg; wu]^T), out = act @ wd^T -- bitwise gemv_rmsnorm2 (GEGLU) + the down GEMV.
+    o = (attn, wo): the o projection first, in the same launch (y = attn @ wo^T is then written, bitwise the GEMV)."""
     M, H = y.shape
     I = wg.shape[0]
     _req(M <= 8 and H % 8 == 0 and I % 8 == 0 and H <= 2560 and I <= 10240,
@@ -220,6 +221,12 @@ def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out):
     _req(res.shape == y.shape == h_out.shape and _ld(res) == _ld(y) == _ld(h_out), "decode_mlp: res/y/h_out rows")
     _req(wg.shape == wu.shape == (I, H) and _ld(wg) == _ld(wu) and wd.shape == (H, I), "decode_mlp: weight shapes")
     _req(act.shape[0] >= M and act.shape[1] >= I and out.shape[0] >= M and out.shape[1] >= H, "decode_mlp: outputs")
+    attn, wo = o if o is not None else (None, None)
+    if attn is not None:
+        _chk_bf16(attn, "decode_mlp attn")
+        _chk_bf16(wo, "decode_mlp wo")
+        _req(attn.shape[0] == M and wo.shape == (H, attn.shape[1]) and attn.shape[1] % 8 == 0 and
+             attn.shape[1] <= 2048 and attn.stride(1) == 1 and wo.stride(1) == 1, "decode_mlp: o projection shapes")
     key = (y.device.index, _stream())
     sync = _DECODE_MLP_SYNC.get(key)
     if sync is None:
@@ -228,7 +235,9 @@ def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out):
     L.check(L.lib().svla_decode_mlp(M, H, I, res.data_ptr(), y.data_ptr(), _ld(y), w1.data_ptr(), w2.data_ptr(),
                                     float(eps1), float(eps2), h_out.data_ptr(), wg.data_ptr(), wu.data_ptr(), _ld(wg),
                                     wd.data_ptr(), _ld(wd), act.data_ptr(), _ld(act), out.data_ptr(), _ld(out),
-                                    sync.data_ptr(), _stream()), "svla_decode_mlp")
+                                    _ptr(attn), _ld(attn) if attn is not None else 0,
+                                    attn.shape[1] if attn is not None else 0, _ptr(wo),
+                                    _ld(wo) if wo is not None else 0, sync.data_ptr(), _stream()), "svla_decode_mlp")
 
 
 # Optional live launch timing (bench.py's roofline): launch_timer["geglu"] = [] makes every GeGLU GEMM launch

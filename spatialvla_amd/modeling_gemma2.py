@@ -381,13 +381,16 @@ class Gemma2Model(nn.Module):
                 po = layers[i - 1].post_feedforward_layernorm
                 res = torch.empty_like(h)
                 pre = (h, m, po.weight, layer.input_layernorm.weight, po.eps, layer.input_layernorm.eps, res)
+            fuse_o = Fn.DECODE_O_FUSED[0] and Fn.DECODE_MLP_PERSIST[0]  # o projection inside the MLP's launch
             a = Fn.gemma_attention_cached(x if i == 0 else None, at.q_proj.weight, at.k_proj.weight, at.v_proj.weight,
                                           at.o_proj.weight, cos, sin, cache.key_cache[i], cache.value_cache[i],
-                                          cache.kv_class, cache.seen_tokens, at.attn_cfg(B, Lq), pre=pre)
+                                          cache.kv_class, cache.seen_tokens, at.attn_cfg(B, Lq), pre=pre,
+                                          skip_o=fuse_o)
             pa, pf = layer.post_attention_layernorm, layer.pre_feedforward_layernorm
             h = torch.empty_like(res)
-            m = Fn.gemma_mlp_decode(res, a, pa.weight, pf.weight, pa.eps, pf.eps, h, mlp.gate_proj.weight,
-                                    mlp.up_proj.weight, mlp.down_proj.weight)
+            m = Fn.gemma_mlp_decode(res, None if fuse_o else a, pa.weight, pf.weight, pa.eps, pf.eps, h,
+                                    mlp.gate_proj.weight, mlp.up_proj.weight, mlp.down_proj.weight,
+                                    o=(a, at.o_proj.weight) if fuse_o else None)
         po = layers[-1].post_feedforward_layernorm
         res, x = torch.empty_like(h), torch.empty_like(h)
         Kn.add_rmsnorm2_fwd(h, m, po.weight, self.norm.weight, po.eps, self.norm.eps, res, x)

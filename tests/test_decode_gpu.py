@@ -343,14 +343,19 @@ def test_gemv_rmsnorm2_bitwise(cuda, M, geglu):
     assert torch.equal(h, h_ref)
 
 
-@pytest.mark.parametrize("M,H,I", [(1, 2304, 9216), (3, 2304, 9216), (8, 2304, 9216), (2, 256, 520)])
-def test_decode_mlp_persistent_bitwise(cuda, M, H, I):
+@pytest.mark.parametrize("M,H,I,KO", [(1, 2304, 9216, 2048), (3, 2304, 9216, 0), (8, 2304, 9216, 2048),
+                                      (2, 256, 520, 0), (2, 256, 520, 264)])
+def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO):
     """svla_decode_mlp (one persistent launch: norm pair + gate|up GeGLU GEMV, grid barrier, down GEMV) == the
     two-launch path (svla_gemv_rmsnorm2 GEGLU, then the small-M down GEMV), bit for bit: h, act and out -- over
-    repeated launches (the grid barrier's words are reused) and a ragged shape (fewer blocks than CUs)."""
+    repeated launches (the grid barrier's words are reused) and a ragged shape (fewer blocks than CUs).  KO > 0: the
+    o projection y = attn @ wo^T inside the same launch (a second barrier), bitwise the small-M GEMV."""
     from spatialvla_amd import kernels as Kn
     torch.manual_seed(23)
     res, y = _r(M, H), _r(M, H, scale=3.0)
+    if KO:
+        attn, wo = _r(M, KO), _r(H, KO, scale=0.05)
+        Kn.linear_fwd(attn, [wo], y)
     w1, w2 = _r(H, scale=0.3), _r(H, scale=0.3)
     wg, wu, wd = _r(I, H, scale=0.02), _r(I, H, scale=0.02), _r(H, I, scale=0.02)
     h_ref = torch.empty_like(res)
@@ -360,7 +365,12 @@ def test_decode_mlp_persistent_bitwise(cuda, M, H, I):
     Kn.linear_fwd(act_ref, [wd], out_ref)
     for rep in range(3):
         h, act, out = torch.full_like(res, 7.0), torch.full_like(act_ref, 7.0), torch.full_like(out_ref, 7.0)
-        Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+        if KO:
+            y2 = torch.full_like(y, 7.0)
+            Kn.decode_mlp(res, y2, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out, o=(attn, wo))
+            assert torch.equal(y2, y), rep
+        else:
+            Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
         assert torch.equal(h, h_ref), rep
         assert torch.equal(act, act_ref), rep
         assert torch.equal(out, out_ref), rep
@@ -377,7 +387,7 @@ def test_decode_mlp_persistent_graph_tokens(cuda):
     keep = Fn.DECODE_MLP_PERSIST[0]
     try:
         for persist in (False, True):
-            Fn.DECODE_MLP_PERSIST[0] = persist
+            Fn.DECODE_MLP_PERSIST[0] = persist  # (with it, the o projection inside the launch: DECODE_O_FUSED)
             model.clear_decode_cache()
             with torch.no_grad():
                 o1 = model(input_ids=ids.to(cuda), pixel_values=inputs["pixel_values"].to(cuda),
