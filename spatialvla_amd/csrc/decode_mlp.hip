@@ -62,10 +62,14 @@ __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
       }
     }
     if (!last) {
-      for (unsigned spin = 0; spin < (1u << 22); ++spin) {  // bounded: ~seconds at most, never a hang
+      // bounded (~2 s): a block that never sees the release counts a timeout in sync[32] (svla_decode_mlp reports
+      // it through the tests) and goes on with wrong numbers instead of hanging the GPU
+      unsigned spin = 0;
+      for (; spin < (1u << 25); ++spin) {
         if (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
         __builtin_amdgcn_s_sleep(1);
       }
+      if (spin == (1u << 25)) __hip_atomic_fetch_add(&sync[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);  // agent scope (the default for this builtin on the device)
   }

@@ -207,6 +207,12 @@ def gemv_rmsnorm2(res, y, w1, w2, eps1, eps2, h_out, weights: List[torch.Tensor]
 _DECODE_MLP_SYNC = {}
 
 
+def decode_mlp_timeouts() -> int:
+    """Grid-barrier waits of svla_decode_mlp that hit their bound (word 32 of each stream's sync buffer): 0 unless a
+    launch's blocks could not all be resident at once."""
+    return sum(int(t.view(torch.int32)[32].item()) for t in _DECODE_MLP_SYNC.values())
+
+
 def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out, o=None):
     """Decode-step Gemma2 MLP in one persistent launch (svla_decode_mlp): h_out = bf16(res + rms(y; w1)),
     act = GeGLU(rms(h_out; w2) @ [wg; wu]^T), out = act @ wd^T -- bitwise gemv_rmsnorm2 (GEGLU) + the down GEMV.

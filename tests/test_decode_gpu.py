@@ -371,6 +371,7 @@ def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO):
             assert torch.equal(y2, y), rep
         else:
             Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+        assert Kn.decode_mlp_timeouts() == 0
         assert torch.equal(h, h_ref), rep
         assert torch.equal(act, act_ref), rep
         assert torch.equal(out, out_ref), rep
