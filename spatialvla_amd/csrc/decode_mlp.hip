@@ -114,14 +114,21 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
   // ---------------- phase O (attn != NULL): y = attn @ wo^T, the o projection (gemv_pf_kernel<4, 1>'s arithmetic,
   // one wave a row), stored write-through; the first gate|up pair is then issued and a grid barrier publishes y
   if (attn != nullptr) {
-    for (int64_t ro = r; ro < H; ro += wstep) {
-      const bf16_t* wr = wo + ro * ldwo;
-      u32x4 ov[DM_OCH];
+    // every o row of this wave (H <= 2 * waves: at most two) has its weight loads in flight before any dot product
+    const int64_t ro[2] = {r, r + wstep};
+    u32x4 ov[2][DM_OCH];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16_t* wr = wo + (ro[u] < H ? ro[u] : H - 1) * ldwo;
 #pragma unroll
       for (int i = 0; i < DM_OCH; ++i) {
         const int64_t k = (int64_t)lane * 8 + i * 512;
-        ov[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + (k < KO ? k : KO - 8)));
+        ov[u][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr + (k < KO ? k : KO - 8)));
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (ro[u] >= H) break;
       float acc[MR];
 #pragma unroll
       for (int m = 0; m < MR; ++m) acc[m] = 0.f;
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
         const int64_t k = (int64_t)lane * 8 + i * 512;
         if (k < KO) {
           float wf[8];
-          unpack8(ov[i], wf);
+          unpack8(ov[u][i], wf);
 #pragma unroll
           for (int m = 0; m < MR; ++m) {
             if (m < M) {
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
         if (m < M) {
           const float v = wave_sum(acc[m]);
           if (lane == 0)
-            __hip_atomic_store(reinterpret_cast<unsigned short*>(y + m * ldx + ro), (unsigned short)f2bf(v),
+            __hip_atomic_store(reinterpret_cast<unsigned short*>(y + m * ldx + ro[u]), (unsigned short)f2bf(v),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -368,6 +375,7 @@ extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res,
                  "decode_mlp: the o projection needs w_o, KO a multiple of 8 <= %d and 16-B rows", 512 * DM_OCH);
   const unsigned blocks =
       (unsigned)std::min<int64_t>((int64_t)svla::num_cus() * DM_BPC, std::max<int64_t>(I / 4, 1));
+  SVLA_CHECK_ARG(!attn || H <= 2 * 4 * (int64_t)blocks, "decode_mlp: the o phase covers at most two rows a wave");
   const size_t lds = (size_t)M * H * 2 + 2 * 4 * sizeof(float) + 4 * DM_MAXM * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define SVLA_DM(MR)                                                                                                  \
