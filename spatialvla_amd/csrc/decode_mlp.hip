@@ -4,8 +4,9 @@
 // :487-490).  Bitwise the two-launch path (svla_gemv_rmsnorm2 with the GEGLU epilogue, then the long-K split GEMV
 // of the down projection):
 //  * phase A (gemv_norm2_kernel's arithmetic): every block forms h = bf16(res + rms(y; w1)) and x = rms(h; w2) in
-//    LDS (block 0 stores h); each wave then walks gate|up row pairs r = wave, wave + waves, ... with the next pair's
-//    weights loaded while the current pair's dot products run, and stores act[m][r] = bf16(gelu(g) * u);
+//    LDS (block 0 stores h); each wave then walks gate|up row pairs r = wave, wave + waves, ... with the next
+//    DM_DEPTH - 1 pairs' weights in flight while a pair's dot products run, and stores act[m][r] =
+//    bf16(gelu(g) * u);
 //  * a grid barrier: act is stored write-through, each wave drains its stores, thread 0 of each block arrives on a
 //    counter and waits for the last arrival's generation bump, then one acquire fence per block;
 //  * phase C (gemv_splitk_kernel's arithmetic): each block walks down-projection rows n = block, block + blocks, ...
@@ -26,7 +27,10 @@ constexpr int DM_MAXM = 8;
 constexpr int DM_KCH = 5;   // 16-B chunks per lane of a gate / up row: H <= 2560
 constexpr int DM_NC = 2;    // norm chunks per thread: H <= 4096
 constexpr int DM_DCH = 5;   // 16-B chunks per thread of a down row: I <= 10240
-constexpr int DM_OCH = 4;   // 16-B chunks per lane of an o-projection row: KO <= 2048
+constexpr int DM_OCH = 4;
+#ifndef DM_DEPTH
+#define DM_DEPTH 2  // gate|up row pairs a wave has in flight in phase A (2 or 3; 3 measured slower, r7g)
+#endif   // 16-B chunks per lane of an o-projection row: KO <= 2048
 
 // act is stored write-through (agent-scope relaxed atomic stores, sc1), so a wave only drains its own stores before
 // the block arrives; the arrival and the generation are relaxed agent-scope atomics, and one agent-scope acquire
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
                                                             int64_t ldo, const bf16_t* __restrict__ attn,
                                                             int64_t ld_attn, int KO, const bf16_t* __restrict__ wo,
                                                             int64_t ldwo, unsigned* sync) {
+  constexpr int DEPTH = MR == 1 ? DM_DEPTH : 2;  // the 8-row instance keeps two (registers)
   extern __shared__ __attribute__((aligned(16))) char dm_smem[];  // [M][H] bf16 x, reduction slots, down partials
   bf16_t* const xs = reinterpret_cast<bf16_t*>(dm_smem);
   float (*red)[4] = reinterpret_cast<float (*)[4]>(dm_smem + (size_t)M * H * 2);
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
 
   const int64_t wstep = (int64_t)gridDim.x * 4;
   int64_t r = (int64_t)blockIdx.x * 4 + wv;
-  u32x4 wa[2][DM_KCH], wb[2][DM_KCH];  // two buffers of [gate, up][chunk] (static indices: no scratch)
+  u32x4 wa[2][DM_KCH], wb[2][DM_KCH], wc[2][DM_KCH];  // buffers of [gate, up][chunk] (static indices)
   auto load_pair = [&](int64_t row, u32x4 (&dst)[2][DM_KCH]) {
     const int64_t n = row < I ? row : I - 1;
     const bf16_t* wr[2] = {wg + n * ldw, wu + n * ldw};
@@ -161,7 +166,8 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     }
     asm volatile("" ::: "memory");
     load_pair(r, wa);
-    grid_barrier<2 * DM_KCH, 0>(sync, gridDim.x);
+    if (DEPTH == 3) load_pair(r + wstep, wb);
+    grid_barrier<2 * DM_KCH * (DEPTH == 3 ? 2 : 1), 0>(sync, gridDim.x);
   }
 
   // ---------------- phase A prologue: norm inputs, then the first gate|up row pair (gemv_norm2_kernel's order)
@@ -183,7 +189,10 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
       }
     }
   }
-  if (attn == nullptr) load_pair(r, wa);
+  if (attn == nullptr) {
+    load_pair(r, wa);
+    if (DEPTH == 3) load_pair(r + wstep, wb);
+  }
 
   // ---------------- the norm pair (block_sum's order: wave butterfly, then the four waves in order)
   auto bsum = [&](float v, int slot) {
@@ -243,7 +252,8 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
 
   // ---------------- phase A: gate|up row pairs of this wave, the next pair's weights in flight
   auto pair = [&](const u32x4 (&wcur)[2][DM_KCH], u32x4 (&wnext)[2][DM_KCH]) {
-    load_pair(r + wstep, wnext);  // unconditional (clamped row): the compiler can then wait for this pair only
+    // unconditional (clamped row): the compiler can then wait for the current pair only
+    load_pair(r + (DEPTH - 1) * wstep, wnext);
     float acc[2][MR];
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -280,10 +290,20 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     }
     r += wstep;
   };
-  while (r < I) {
-    pair(wa, wb);
-    if (r >= I) break;
-    pair(wb, wa);
+  if constexpr (DEPTH == 3) {
+    while (r < I) {
+      pair(wa, wc);
+      if (r >= I) break;
+      pair(wb, wa);
+      if (r >= I) break;
+      pair(wc, wb);
+    }
+  } else {
+    while (r < I) {
+      pair(wa, wb);
+      if (r >= I) break;
+      pair(wb, wa);
+    }
   }
 
   // the block's first down row is independent of act: its weights stream in while the grid barrier waits
