@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-fp8-leg", action="store_true", help="skip the configs[4] fp8 leg of the N=1 line")
+    ap.add_argument("--backend", default=os.environ.get("SVLA_BENCH_BACKEND", "nccl"), choices=["nccl", "gloo"],
+                    help="N>1 process-group backend: nccl (= RCCL, one rank per GPU; the scaling runs) or gloo (tests)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on cuda:0 (tests of the N>1 path on a one-GPU box, with --backend gloo)")
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE configs[4]: Gemma2 q|k|v, o, gate|up, down forward projections on the fp8 MFMA GEMM")
     return ap.parse_args()
@@ -328,11 +332,16 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and args.share_device and args.backend == "nccl":
+        sys.exit("bench.py: --share-device needs --backend gloo (RCCL refuses two ranks on one GPU)")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
     from spatialvla_amd import presets
     from spatialvla_amd.engine import TrainEngine
     cfgd = json.loads(json.dumps(getattr(presets, args.config)()))
@@ -377,10 +386,13 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t_start
-    dt_t = torch.tensor([dt], device=device)
+    # the slowest rank's clock: every rank's seconds gathered (the JSON line carries them), value from the MAX
+    per_rank = [dt]
     if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+        dts = [torch.zeros(1, dtype=torch.float64, device=device) for _ in range(world)]
+        dist.all_gather(dts, torch.tensor([dt], dtype=torch.float64, device=device))
+        per_rank = [float(t.item()) for t in dts]
+    dt = max(per_rank)
     final_loss = float(losses[-1].item())
     ms_step = dt / args.steps * 1e3
     eps = world * B * args.steps / dt
@@ -397,6 +409,10 @@ def main():
         "mfu_model_flops": round(eps * GFLOP_PER_EPISODE / 1e3 / (world * PEAK_BF16_TFLOPS), 4),
         "final_loss": round(final_loss, 4),
     }
+    if world > 1:
+        result["per_rank_seconds"] = [round(t, 6) for t in per_rank]
+        result["timed_seconds_max"] = round(dt, 6)
+        result["backend"] = args.backend
     if world == 1 and not args.fp8 and not args.no_fp8_leg and args.config == "spatialvla_4b":
         result["fp8"] = fp8_leg(model, engine, batches, args)
     if rank == 0:

@@ -364,8 +364,18 @@ int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* res, const v
  * projection runs first in the same launch: y = attn w_o^T (w_o [H][KO], KO <= 2048; y is then an output), bitwise
  * the small-M GEMV.  H <= 2560, I <= 10240, all multiples of 8; w_gate / w_up [I][H] share ldw, w_down [H][I].
  * `sync` points at svla_decode_mlp_sync_bytes() zeroed bytes, reused by every later call on that stream (the grid
- * barriers' counters return to zero). */
+ * barriers' counters return to zero).  The grid is svla_decode_mlp_grid(M, H, I) blocks (occupancy-capped, so an
+ * otherwise idle device holds them all at once), launched plainly, or cooperatively with SVLA_DECODE_MLP_COOP=1
+ * (dispatched only when every block can be resident; ~21 us more per launch).  A block whose barrier wait hits its
+ * bound (1 s: its grid was not co-resident) adds 1 to the 32-bit word 32 of `sync` and writes NaN where it would
+ * have written numbers -- callers read that word after a decode and raise. */
 size_t svla_decode_mlp_sync_bytes(void);
+/* Blocks svla_decode_mlp launches for these sizes (DM_BPC per CU, capped by the occupancy of the instance and its
+ * LDS and by I / 4), or 0 when no block fits on a CU: take the two-launch path then. */
+int svla_decode_mlp_grid(int64_t M, int64_t H, int64_t I);
+/* Test hook: grid_override > 0 launches that many blocks instead of svla_decode_mlp_grid's; cooperative 1 / 0 forces
+ * the launch mode (-1: the default); timeout_ms bounds each barrier wait (default 1000).  Not for production use. */
+void svla_decode_mlp_debug(int grid_override, int cooperative, int timeout_ms);
 int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, void* y, int64_t ldx, const void* w1,
                     const void* w2, float eps1, float eps2, void* h_out, const void* w_gate, const void* w_up,
                     int64_t ldw, const void* w_down, int64_t ldd, void* act, int64_t ldact, void* out, int64_t ldo,

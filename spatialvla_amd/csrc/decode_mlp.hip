@@ -46,7 +46,7 @@ constexpr int DM_SYNC_WORDS = 64 + 2 * DM_SET;  // generation word, then the cou
 // PEND: vector-memory ops issued after the stores this barrier publishes (they retire in issue order); SET: which
 // counter set (a launch with two barriers never reuses a set, so a reset can not race a fast block's next arrival)
 template <int PEND, int SET>
-__device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
+__device__ __forceinline__ bool grid_barrier(unsigned* sync, unsigned nblocks, int* flag, long long spin_ticks) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PEND) : "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -56,7 +56,10 @@ __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
     unsigned* const gcnt = sync + 64 + SET * DM_SET + 64 * g;
     unsigned* const top = sync + 64 + SET * DM_SET + 64 * DM_GROUPS;
     const unsigned gen = __hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool last = false;
+    // the generation must be read before this block's arrival is counted: the two requests target different lines
+    // and could otherwise be serviced out of order, a late read then seeing the bump this arrival completes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool last = false, timed_out = false;
     if (__hip_atomic_fetch_add(gcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
       __hip_atomic_store(gcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1) {
@@ -66,18 +69,24 @@ __device__ __forceinline__ void grid_barrier(unsigned* sync, unsigned nblocks) {
       }
     }
     if (!last) {
-      // bounded (~2 s): a block that never sees the release counts a timeout in sync[32] (svla_decode_mlp reports
-      // it through the tests) and goes on with wrong numbers instead of hanging the GPU
-      unsigned spin = 0;
-      for (; spin < (1u << 25); ++spin) {
-        if (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen) break;
+      // bounded by the constant-rate wall clock (1 s by default): a block that never sees the release (its grid was
+      // not co-resident) counts a timeout in sync[32] and poisons what it writes next with NaN (the caller raises on
+      // the counter); it never hangs the GPU
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        if (wall_clock64() - t0 > spin_ticks) {
+          __hip_atomic_fetch_add(&sync[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          timed_out = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (spin == (1u << 25)) __hip_atomic_fetch_add(&sync[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);  // agent scope (the default for this builtin on the device)
+    *flag = timed_out ? 1 : 0;
   }
   __syncthreads();
+  return *flag != 0;
 }
 
 template <int MR>
@@ -91,12 +100,14 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
                                                             bf16_t* act, int64_t ldact, bf16_t* __restrict__ out,
                                                             int64_t ldo, const bf16_t* __restrict__ attn,
                                                             int64_t ld_attn, int KO, const bf16_t* __restrict__ wo,
-                                                            int64_t ldwo, unsigned* sync) {
+                                                            int64_t ldwo, unsigned* sync, long long spin_ticks) {
   constexpr int DEPTH = MR == 1 ? DM_DEPTH : 2;  // the 8-row instance keeps two (registers)
   extern __shared__ __attribute__((aligned(16))) char dm_smem[];  // [M][H] bf16 x, reduction slots, down partials
   bf16_t* const xs = reinterpret_cast<bf16_t*>(dm_smem);
   float (*red)[4] = reinterpret_cast<float (*)[4]>(dm_smem + (size_t)M * H * 2);
   float (*part)[DM_MAXM] = reinterpret_cast<float (*)[DM_MAXM]>(dm_smem + (size_t)M * H * 2 + 2 * 4 * sizeof(float));
+  int* const bflag = reinterpret_cast<int*>(dm_smem + (size_t)M * H * 2 + 2 * 4 * sizeof(float) +
+                                            4 * DM_MAXM * sizeof(float));
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int nch = H >> 3;
   const int64_t K = H;
@@ -116,6 +127,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
         dst[q][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wr[q] + (k < K ? k : K - 8)));
       }
   };
+  bool poison = false;
   // ---------------- phase O (attn != NULL): y = attn @ wo^T, the o projection (gemv_pf_kernel<4, 1>'s arithmetic,
   // one wave a row), stored write-through; the first gate|up pair is then issued and a grid barrier publishes y
   if (attn != nullptr) {
@@ -167,7 +179,9 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     asm volatile("" ::: "memory");
     load_pair(r, wa);
     if (DEPTH == 3) load_pair(r + wstep, wb);
-    grid_barrier<2 * DM_KCH * (DEPTH == 3 ? 2 : 1), 0>(sync, gridDim.x);
+    // a block that missed this barrier read a partial y: its act rows (and block 0's h) become NaN, and every
+    // down row sums all of act, so the whole output is NaN
+    poison = grid_barrier<2 * DM_KCH * (DEPTH == 3 ? 2 : 1), 0>(sync, gridDim.x, bflag, spin_ticks);
   }
 
   // ---------------- phase A prologue: norm inputs, then the first gate|up row pair (gemv_norm2_kernel's order)
@@ -229,7 +243,9 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
             v[cI][j] = round_bf(rr[j] + round_bf((v[cI][j] * rstd1) * (1.0f + wf[j])));
             ss2 += v[cI][j] * v[cI][j];
           }
-          if (blockIdx.x == 0) *reinterpret_cast<u32x4*>(h_out + m * ldx + ch * 8) = pack8(v[cI]);
+          if (blockIdx.x == 0)
+            *reinterpret_cast<u32x4*>(h_out + m * ldx + ch * 8) =
+                poison ? u32x4{0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u} : pack8(v[cI]);
         }
       }
       const float rstd2 = rsqrtf(bsum(ss2, 1) / (float)K + eps2);
@@ -285,7 +301,8 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
         const float g = round_bf(wave_sum(acc[0][m])), u = round_bf(wave_sum(acc[1][m]));
         if (lane == 0)  // write-through: read by other CUs / XCDs after the grid barrier
           __hip_atomic_store(reinterpret_cast<unsigned short*>(act + m * ldact + r),
-                             (unsigned short)f2bf(gelu_bf16(g) * u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                             poison ? (unsigned short)0x7fc0 : (unsigned short)f2bf(gelu_bf16(g) * u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     r += wstep;
@@ -318,7 +335,8 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
   };
   int64_t n = blockIdx.x;
   load_down(n < H ? n : H - 1, da);
-  grid_barrier<DM_DCH, 1>(sync, gridDim.x);
+  // a block that missed this barrier would read a partial act: it writes NaN rows instead
+  const bool late = grid_barrier<DM_DCH, 1>(sync, gridDim.x, bflag, spin_ticks);
 
   // ---------------- phase C: down rows of this block, four waves split each row's K range
   // one token row (the batch-1 decode step): the thread's act chunks, the same for every down row, in registers
@@ -361,7 +379,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
       }
     }
     __syncthreads();
-    if (t < M) out[t * ldo + n] = f2bf(((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
+    if (t < M) out[t * ldo + n] = late ? (bf16_t)0x7fc0 : f2bf(((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
     __syncthreads();  // part is rewritten by the next row
     n += gridDim.x;
   };
@@ -374,7 +392,69 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
 
 }  // namespace
 
+namespace {
+size_t dm_lds(int64_t M, int64_t H) {
+  return (size_t)M * H * 2 + 2 * 4 * sizeof(float) + 4 * DM_MAXM * sizeof(float) + 16;
+}
+
+// blocks of the persistent grid: DM_BPC per CU, capped by what the occupancy calculator says can be resident at once
+// for this instance and LDS size (so a grid barrier can complete), and by the rows there are; 0 = cannot run
+int dm_blocks(int64_t M, int64_t H, int64_t I) {
+  int per_cu = 0;
+  const size_t lds = dm_lds(M, H);
+  const hipError_t e =
+      M == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mlp_kernel<1>, 256, lds)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mlp_kernel<DM_MAXM>, 256, lds);
+  if (e != hipSuccess || per_cu <= 0) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  const int64_t resident = (int64_t)svla::num_cus() * std::min(per_cu, DM_BPC);
+  return (int)std::min<int64_t>(resident, std::max<int64_t>(I / 4, 1));
+}
+
+// SVLA_DECODE_MLP_COOP=1 launches with the cooperative attribute.  Not the default: measured 2.40-2.47 ms per
+// decode token against 1.84 with the plain launch (profiles/r8a_decode_mlp_coop_ab.txt: ~21 us more per launch, 26
+// launches a token).  The plain launch's grid is occupancy-capped (dm_blocks), and a block that still misses a
+// barrier (another process holding CUs) writes NaN and counts a timeout the callers raise on.
+bool dm_coop() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SVLA_DECODE_MLP_COOP");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// test hooks (svla_decode_mlp_debug): a grid override, the launch mode and the barrier wait bound
+int g_dm_grid_override = 0;
+int g_dm_coop_override = -1;
+int g_dm_timeout_ms = 1000;
+
+long long dm_spin_ticks() {
+  static int rate_khz = 0;  // the wall clock's rate (100 MHz on MI3xx)
+  if (rate_khz <= 0) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) != hipSuccess || v <= 0) v = 100000;
+    rate_khz = v;
+  }
+  return (long long)rate_khz * g_dm_timeout_ms;
+}
+}  // namespace
+
 extern "C" size_t svla_decode_mlp_sync_bytes(void) { return DM_SYNC_WORDS * sizeof(unsigned); }
+
+extern "C" void svla_decode_mlp_debug(int grid_override, int cooperative, int timeout_ms) {
+  g_dm_grid_override = grid_override > 0 ? grid_override : 0;
+  g_dm_coop_override = cooperative;
+  g_dm_timeout_ms = timeout_ms > 0 ? timeout_ms : 1000;
+}
+
+extern "C" int svla_decode_mlp_grid(int64_t M, int64_t H, int64_t I) {
+  if (M < 1 || M > DM_MAXM || H <= 0 || I <= 0) return 0;
+  return dm_blocks(M, H, I);
+}
 
 extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res, void* y, int64_t ldx, const void* w1,
                                const void* w2, float eps1, float eps2, void* h_out, const void* w_gate,
@@ -393,19 +473,42 @@ extern "C" int svla_decode_mlp(int64_t M, int64_t H, int64_t I, const void* res,
   SVLA_CHECK_ARG(!attn || (w_o && KO > 0 && KO % 8 == 0 && KO <= 512 * DM_OCH && ld_attn % 8 == 0 && ld_attn >= KO &&
                            ldwo % 8 == 0 && ldwo >= KO),
                  "decode_mlp: the o projection needs w_o, KO a multiple of 8 <= %d and 16-B rows", 512 * DM_OCH);
-  const unsigned blocks =
-      (unsigned)std::min<int64_t>((int64_t)svla::num_cus() * DM_BPC, std::max<int64_t>(I / 4, 1));
+  const int blocks = g_dm_grid_override > 0 ? g_dm_grid_override : dm_blocks(M, H, I);
+  const bool coop = g_dm_coop_override >= 0 ? g_dm_coop_override == 1 : dm_coop();
+  long long spin_ticks = dm_spin_ticks();
+  SVLA_CHECK_ARG(blocks > 0, "decode_mlp: no block of this instance fits on a CU (LDS %zu B); use the two-launch path",
+                 dm_lds(M, H));
   SVLA_CHECK_ARG(!attn || H <= 2 * 4 * (int64_t)blocks, "decode_mlp: the o phase covers at most two rows a wave");
-  const size_t lds = (size_t)M * H * 2 + 2 * 4 * sizeof(float) + 4 * DM_MAXM * sizeof(float);
+  const size_t lds = dm_lds(M, H);
   hipStream_t s = (hipStream_t)stream;
-#define SVLA_DM(MR)                                                                                                  \
-  hipLaunchKernelGGL((decode_mlp_kernel<MR>), dim3(blocks), dim3(256), lds, s, (int)M, (int)H, (int)I,              \
-                     (const bf16_t*)res, (bf16_t*)y, ldx, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,         \
-                     (bf16_t*)h_out, (const bf16_t*)w_gate, (const bf16_t*)w_up, ldw, (const bf16_t*)w_down, ldd,  \
-                     (bf16_t*)act, ldact, (bf16_t*)out, ldo, (const bf16_t*)attn, ld_attn, (int)KO,                \
-                     (const bf16_t*)w_o, ldwo, sync)
-  if (M == 1) SVLA_DM(1);
-  else SVLA_DM(DM_MAXM);
-#undef SVLA_DM
+  // plain launch of the occupancy-capped grid (default), or cooperative (SVLA_DECODE_MLP_COOP=1: the runtime then
+  // dispatches the grid only when every block can be resident together, or fails the launch)
+  int Mi = (int)M, Hi = (int)H, Ii = (int)I, KOi = (int)KO;
+  const bf16_t *res_ = (const bf16_t*)res, *w1_ = (const bf16_t*)w1, *w2_ = (const bf16_t*)w2,
+               *wg_ = (const bf16_t*)w_gate, *wu_ = (const bf16_t*)w_up, *wd_ = (const bf16_t*)w_down,
+               *attn_ = (const bf16_t*)attn, *wo_ = (const bf16_t*)w_o;
+  bf16_t *y_ = (bf16_t*)y, *h_ = (bf16_t*)h_out, *act_ = (bf16_t*)act, *out_ = (bf16_t*)out;
+  void* args[] = {&Mi,  &Hi,    &Ii,   &res_,  &y_,      &ldx, &w1_,  &w2_,    &eps1, &eps2, &h_,   &wg_, &wu_,  &ldw,
+                  &wd_, &ldd,   &act_, &ldact, &out_,    &ldo, &attn_, &ld_attn, &KOi, &wo_,  &ldwo, &sync,
+                  &spin_ticks};
+  hipLaunchAttribute attr[1];
+  attr[0].id = hipLaunchAttributeCooperative;
+  attr[0].val.cooperative = 1;
+  hipLaunchConfig_t cfg{};
+  cfg.gridDim = dim3((unsigned)blocks);
+  cfg.blockDim = dim3(256);
+  cfg.dynamicSmemBytes = lds;
+  cfg.stream = s;
+  cfg.attrs = attr;
+  cfg.numAttrs = coop ? 1 : 0;
+  const void* fn = M == 1 ? reinterpret_cast<const void*>(&decode_mlp_kernel<1>)
+                          : reinterpret_cast<const void*>(&decode_mlp_kernel<DM_MAXM>);
+  const hipError_t e = hipLaunchKernelExC(&cfg, fn, args);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    svla::set_error("decode_mlp: %s launch of %d blocks failed: %s", coop ? "cooperative" : "plain", blocks,
+                    hipGetErrorString(e));
+    return SVLA_ERR_HIP;
+  }
   return svla::check_launch("decode_mlp");
 }

@@ -176,17 +176,25 @@ __global__ __launch_bounds__(256) void quant_mx_rows_kernel(int64_t rows, int64_
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = 0.f;
   float amax = 0.f;
+  int nonfinite = 0;  // a NaN or +-Inf element: the block becomes NaN (scale 0xFF, OCP MX §5.3), not a finite clamp
 #pragma unroll
-  for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(f[j]));
+  for (int j = 0; j < 8; ++j) {
+    amax = fmaxf(amax, fabsf(f[j]));
+    nonfinite |= (__float_as_uint(f[j]) & 0x7f800000u) == 0x7f800000u;
+  }
   amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
   amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+  nonfinite |= __shfl_xor(nonfinite, 1, 64);
+  nonfinite |= __shfl_xor(nonfinite, 2, 64);
   const int X = mx_exponent(amax);
   const float inv = __uint_as_float((uint32_t)(127 - X) << 23);  // 2^-X exactly (X >= -127 -> exponent <= 254)
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -448.f), 448.f);
-  if (ok) *reinterpret_cast<u32x2*>(q + r * ldq + k) = u32x2{cvt4(f[0], f[1], f[2], f[3]), cvt4(f[4], f[5], f[6], f[7])};
+  u32x2 qv = u32x2{cvt4(f[0], f[1], f[2], f[3]), cvt4(f[4], f[5], f[6], f[7])};
+  if (nonfinite) qv = u32x2{0x7f7f7f7fu, 0x7f7f7f7fu};  // e4m3 NaN elements as well: NaN whatever the scale decodes to
+  if (ok) *reinterpret_cast<u32x2*>(q + r * ldq + k) = qv;
   // scale bytes of the k-tile's 4 blocks (lanes 4b of the 16-lane group) -> one dword
-  uint32_t byte = (uint32_t)(127 + X);
+  uint32_t byte = nonfinite ? 0xffu : (uint32_t)(127 + X);
   uint32_t w = byte;
   w |= (uint32_t)__shfl_down((int)byte, 4, 16) << 8;
   w |= (uint32_t)__shfl_down((int)byte, 8, 16) << 16;

@@ -351,6 +351,15 @@ FP8_DGRAD = [True]
 # scaling of the fp8 operands: "mx" = OCP MX block scales (one E8M0 scale per 32 k, applied by the MFMA; the product
 # path), "row" = one fp32 scale per row applied in the epilogue (round 2-4)
 FP8_SCALING = [os.environ.get("SVLA_FP8_SCALING", "mx")]
+# which Gemma2 projections run in fp8 when a layer has fp8 weights (configs[4]): any of "qkv", "o", "gate_up", "down"
+# (SVLA_FP8_SITES, comma-separated); the others stay on the bf16 GEMM.  tests/test_fp8_ablation_gpu.py measures each
+# site's share of the logit error and of the action-row flips.
+FP8_SITES = [set(os.environ.get("SVLA_FP8_SITES", "qkv,o,gate_up,down").split(","))]
+
+
+def _fp8_site(f8, name):
+    """f8 if projection `name` runs in fp8 (FP8_SITES), else None (the bf16 GEMM)."""
+    return f8 if f8 is not None and name in FP8_SITES[0] else None
 
 
 class FP8Weights:
@@ -452,7 +461,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
         rope = (cos, sin, cos.shape[0], cfg.D, qd + kd)
-        if f8 is not None:
+        if _fp8_site(f8, "qkv") is not None:
             _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, kind=L.EPI_ROPE, rope=rope)
         else:
             K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=rope)
@@ -464,7 +473,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         if capture is not None:  # output_attentions: the rotated q|k|v rows (no copy)
             capture["qkv"] = qkv
         out = _empty(M, wo.shape[0], like=x)
-        if f8 is not None:
+        if _fp8_site(f8, "o") is not None:
             _fp8_linear(attn, f8, "o", (wo,), out)
         else:
             K.linear_fwd(attn, [wo], out)
@@ -490,7 +499,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         dwo, acc, ret_wo = _grad_dest(wo, ctx.needs_input_grad[4])
         if dwo is not None:
             side.run(lambda: K.linear_wgrad(dout, attn, [dwo], accumulate=acc), dout, attn)
-        if f8 is not None:
+        if _fp8_site(f8, "o") is not None:
             _fp8_dgrad(dout, f8, "o", (wo,), dattn)
         else:
             K.linear_dgrad(dout, [wo], dattn)
@@ -516,7 +525,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         side.run(qkv_wgrad, dqkv, x)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            if f8 is not None:
+            if _fp8_site(f8, "qkv") is not None:
                 _fp8_dgrad(dqkv, f8, "qkv", (wq, wk, wv), dx)
             else:
                 K.linear_dgrad(dqkv, [wq, wk, wv], dx)
@@ -619,8 +628,9 @@ DECODE_O_FUSED = [os.environ.get("SVLA_DECODE_O_FUSED", "0") != "0"]
 
 
 def persist_ok(y, wg, wu, wd) -> bool:
-    return (DECODE_MLP_PERSIST[0] and y.shape[1] <= 2560 and wg.shape[0] <= 10240
-            and wg.stride(1) == wu.stride(1) == wd.stride(1) == 1)
+    return (DECODE_MLP_PERSIST[0] and y.shape[1] <= 2560 and wg.shape[0] <= 10240 and y.shape[0] <= 8
+            and wg.stride(1) == wu.stride(1) == wd.stride(1) == 1
+            and K.decode_mlp_grid(y.shape[0], y.shape[1], wg.shape[0]) > 0)
 
 
 # the decode MLP as one persistent launch (svla_decode_mlp) instead of the norm-GEMV + down-GEMV pair: 1.80 vs
@@ -636,7 +646,8 @@ def gemma_mlp_decode(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, o=None):
     if o is not None:  # y = attn @ wo^T (the o projection), in the persistent launch or as its own GEMV
         attn, wo = o
         y = _empty(attn.shape[0], wo.shape[0], like=attn)
-        if not persist_ok(y, wg, wu, wd) or attn.shape[1] > 2048 or wo.stride(1) != 1:
+        if (not persist_ok(y, wg, wu, wd) or attn.shape[1] > 2048 or wo.stride(1) != 1
+                or y.shape[1] > 8 * K.decode_mlp_grid(y.shape[0], y.shape[1], wg.shape[0])):
             K.linear_fwd(attn, [wo], y)
             o = None
     M = y.shape[0]
@@ -665,11 +676,13 @@ class GemmaMLPFn(torch.autograd.Function):
         g = _empty(M, I, like=x)
         u = _empty(M, I, like=x)
         out = _empty(M, wd.shape[0], like=x)
-        if f8 is not None:
+        if _fp8_site(f8, "gate_up") is not None:
             _fp8_linear(x, f8, "gate_up", (wg, wu), h, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u)
-            _fp8_linear(h, f8, "down", (wd,), out)
         else:
             K.linear_geglu_fwd(x, wg, wu, h, g, u)
+        if _fp8_site(f8, "down") is not None:
+            _fp8_linear(h, f8, "down", (wd,), out)
+        else:
             K.linear_fwd(h, [wd], out)
         ctx.save_for_backward(x, wg, wu, wd, g, u, h)
         ctx.f8 = f8
@@ -689,7 +702,7 @@ class GemmaMLPFn(torch.autograd.Function):
         # dH by a plain-store GEMM, then the GeGLU derivative as one HBM pass in place (in the down dgrad's epilogue
         # it cost more than the pass: +60 % on the 8-phase kernel's LDS image, +0.11 ms per layer from the 4-wave
         # kernel's accumulators with the g / u loads one row block ahead, r4)
-        if f8 is not None:
+        if _fp8_site(f8, "down") is not None:
             _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
@@ -709,7 +722,7 @@ class GemmaMLPFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            if f8 is not None:
+            if _fp8_site(f8, "gate_up") is not None:
                 _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx)
             else:
                 K.linear_dgrad(dgu, [wg, wu], dx)

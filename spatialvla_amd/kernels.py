@@ -209,8 +209,37 @@ _DECODE_MLP_SYNC = {}
 
 def decode_mlp_timeouts() -> int:
     """Grid-barrier waits of svla_decode_mlp that hit their bound (word 32 of each stream's sync buffer): 0 unless a
-    launch's blocks could not all be resident at once."""
+    launch's blocks could not all be resident at once (such a block writes NaN instead of its numbers)."""
     return sum(int(t.view(torch.int32)[32].item()) for t in _DECODE_MLP_SYNC.values())
+
+
+_DECODE_MLP_TIMEOUTS_SEEN = [0]
+
+
+def check_decode_mlp_timeouts(what: str = "decode"):
+    """Raise RuntimeError if a persistent decode-MLP launch missed a grid barrier since the last check (one small
+    device read per sync buffer; predict_action / generate call it once, after their last step)."""
+    if not _DECODE_MLP_SYNC:
+        return
+    n = decode_mlp_timeouts()
+    if n != _DECODE_MLP_TIMEOUTS_SEEN[0]:
+        new = n - _DECODE_MLP_TIMEOUTS_SEEN[0]
+        _DECODE_MLP_TIMEOUTS_SEEN[0] = n
+        raise RuntimeError(f"{what}: {new} block(s) of the persistent decode MLP (svla_decode_mlp) missed a grid "
+                           "barrier (its grid was not co-resident); their outputs are NaN and the tokens are invalid. "
+                           "Set SVLA_DECODE_MLP_PERSIST=0 for the two-launch path.")
+
+
+_DECODE_MLP_GRID = {}
+
+
+def decode_mlp_grid(M: int, H: int, I: int) -> int:
+    """Blocks svla_decode_mlp would launch (occupancy-capped), 0 if it can not run: the two-launch path then."""
+    key = (torch.cuda.current_device(), M, H, I)
+    g = _DECODE_MLP_GRID.get(key)
+    if g is None:
+        g = _DECODE_MLP_GRID[key] = int(L.lib().svla_decode_mlp_grid(M, H, I))
+    return g
 
 
 def decode_mlp(res, y, w1, w2, eps1, eps2, h_out, wg, wu, wd, act, out, o=None):

@@ -794,6 +794,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
                 cache.seen_tokens = p0 + 1
             steps += 1
         toks = st["toks"][:, P:P + steps + 1].clone()
+        K.check_decode_mlp_timeouts("predict_action")
         if eos is not None:  # the step-by-step loop's length: up to the token where the last row finished
             hit = toks == eos
             if bool(hit.any(1).all()):
@@ -876,6 +877,7 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
             cache_position = cache_position[-1:] + 1
             if eos is not None and bool(finished.all()):
                 break
+        K.check_decode_mlp_timeouts("generate")
         return ids
 
     @torch.no_grad()

@@ -138,7 +138,7 @@ def test_header_symbols_exported_by_library():
     """libsvla.so loads (no GPU needed) and exports every entry point declared in include/svla.h."""
     from spatialvla_amd import _lib
     hdr = open(os.path.join(REPO, "include", "svla.h")).read()
-    names = set(re.findall(r"^\s*(?:const char\*|int|size_t)\s+(svla_\w+)\s*\(", hdr, re.M))
+    names = set(re.findall(r"^\s*(?:const char\*|int|size_t|void)\s+(svla_\w+)\s*\(", hdr, re.M))
     assert len(names) >= 20
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for n in names:
@@ -146,7 +146,7 @@ def test_header_symbols_exported_by_library():
     assert names == set(_lib.SIGNATURES), "python binding must cover exactly the header"
     # the binding's argument count equals the prototype's (a wrong count only fails at the first GPU call)
     body = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    for m in re.finditer(r"(?:const char\*|int|size_t)\s+(svla_\w+)\s*\(([^)]*)\)\s*;", body):
+    for m in re.finditer(r"(?:const char\*|int|size_t|void)\s+(svla_\w+)\s*\(([^)]*)\)\s*;", body):
         params = [p for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
         assert len(params) == len(_lib.SIGNATURES[m.group(1)][1]), (m.group(1), len(params))
     _lib.load()

@@ -343,9 +343,18 @@ def test_gemv_rmsnorm2_bitwise(cuda, M, geglu):
     assert torch.equal(h, h_ref)
 
 
+@pytest.fixture(params=["coop", "plain"])
+def dm_launch_mode(request):
+    """svla_decode_mlp launched cooperatively (the default) or with a plain launch (SVLA_DECODE_MLP_COOP=0)."""
+    from spatialvla_amd import _lib as L
+    L.lib().svla_decode_mlp_debug(0, 1 if request.param == "coop" else 0, 1000)
+    yield request.param
+    L.lib().svla_decode_mlp_debug(0, -1, 1000)
+
+
 @pytest.mark.parametrize("M,H,I,KO", [(1, 2304, 9216, 2048), (3, 2304, 9216, 0), (8, 2304, 9216, 2048),
                                       (2, 256, 520, 0), (2, 256, 520, 264)])
-def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO):
+def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO, dm_launch_mode):
     """svla_decode_mlp (one persistent launch: norm pair + gate|up GeGLU GEMV, grid barrier, down GEMV) == the
     two-launch path (svla_gemv_rmsnorm2 GEGLU, then the small-M down GEMV), bit for bit: h, act and out -- over
     repeated launches (the grid barrier's words are reused) and a ragged shape (fewer blocks than CUs).  KO > 0: the
@@ -363,6 +372,7 @@ def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO):
     Kn.gemv_rmsnorm2(res, y, w1, w2, 1e-6, 1e-6, h_ref, [wg, wu], act_ref, geglu_out=(g, u))
     out_ref = torch.empty(M, H, dtype=BF, device=cuda)
     Kn.linear_fwd(act_ref, [wd], out_ref)
+    t0 = Kn.decode_mlp_timeouts()
     for rep in range(3):
         h, act, out = torch.full_like(res, 7.0), torch.full_like(act_ref, 7.0), torch.full_like(out_ref, 7.0)
         if KO:
@@ -371,10 +381,64 @@ def test_decode_mlp_persistent_bitwise(cuda, M, H, I, KO):
             assert torch.equal(y2, y), rep
         else:
             Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
-        assert Kn.decode_mlp_timeouts() == 0
+        assert Kn.decode_mlp_timeouts() == t0
         assert torch.equal(h, h_ref), rep
         assert torch.equal(act, act_ref), rep
         assert torch.equal(out, out_ref), rep
+
+
+def test_decode_mlp_grid_is_occupancy_capped(cuda):
+    """The persistent grid never exceeds what can be resident at once: DM_BPC (2) blocks per CU at most, fewer when the
+    instance's LDS (M x H bf16) or registers allow fewer, and I / 4 for small layers."""
+    from spatialvla_amd import kernels as Kn
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    g = Kn.decode_mlp_grid(1, 2304, 9216)
+    assert 0 < g <= 2 * cus
+    assert Kn.decode_mlp_grid(8, 2304, 9216) <= 2 * cus
+    assert Kn.decode_mlp_grid(2, 256, 520) == 130
+
+
+def test_decode_mlp_oversubscribed_grid_fails_loudly(cuda):
+    """A grid that can not be co-resident never yields silent numbers: launched cooperatively the runtime
+    refuses it (an error, nothing runs); launched plainly, the blocks that miss the grid barrier count a timeout after
+    their bounded wait (50 ms here) and write NaN, check_decode_mlp_timeouts() raises, and the barrier words are back at
+    zero so the next launch is bitwise the two-launch path again."""
+    from spatialvla_amd import _lib as L
+    from spatialvla_amd import kernels as Kn
+    torch.manual_seed(29)
+    M, H, I = 1, 256, 520
+    res, y = _r(M, H), _r(M, H, scale=3.0)
+    w1, w2 = _r(H, scale=0.3), _r(H, scale=0.3)
+    wg, wu, wd = _r(I, H, scale=0.02), _r(I, H, scale=0.02), _r(H, I, scale=0.02)
+    h_ref = torch.empty_like(res)
+    act_ref, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+    Kn.gemv_rmsnorm2(res, y, w1, w2, 1e-6, 1e-6, h_ref, [wg, wu], act_ref, geglu_out=(g, u))
+    out_ref = torch.empty(M, H, dtype=BF, device=cuda)
+    Kn.linear_fwd(act_ref, [wd], out_ref)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    big = 32 * cus  # 8192 blocks of 256 threads: more than 32 waves per CU can hold
+    Kn.check_decode_mlp_timeouts()  # earlier launches: nothing pending
+    lib = L.lib()
+    try:
+        lib.svla_decode_mlp_debug(big, 1, 50)
+        h, act, out = torch.empty_like(res), torch.empty_like(act_ref), torch.empty_like(out_ref)
+        with pytest.raises(L.SvlaError):
+            Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+        torch.cuda.synchronize()
+        lib.svla_decode_mlp_debug(big, 0, 50)
+        out.fill_(7.0)
+        Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+        torch.cuda.synchronize()
+        assert Kn.decode_mlp_timeouts() > 0
+        assert torch.isnan(out.float()).any()
+        with pytest.raises(RuntimeError, match="missed a grid barrier"):
+            Kn.check_decode_mlp_timeouts()
+    finally:
+        lib.svla_decode_mlp_debug(0, -1, 1000)
+    h, act, out = torch.empty_like(res), torch.empty_like(act_ref), torch.empty_like(out_ref)
+    Kn.decode_mlp(res, y, w1, w2, 1e-6, 1e-6, h, wg, wu, wd, act, out)
+    Kn.check_decode_mlp_timeouts()
+    assert torch.equal(out, out_ref) and torch.equal(act, act_ref) and torch.equal(h, h_ref)
 
 
 def test_decode_mlp_persistent_graph_tokens(cuda):

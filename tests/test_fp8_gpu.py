@@ -226,6 +226,41 @@ def test_quant_mx_rows_bitexact(cuda, rows, k):
     assert torch.equal(q.view(torch.uint8).cpu(), qr.view(torch.uint8))
 
 
+def test_quant_mx_rows_nonfinite_blocks_are_nan(cuda):
+    """A NaN or +-Inf element makes its whole 32-k MX block NaN -- scale byte 0xFF (OCP MX v1.0 §5.3) and e4m3 NaN
+    elements (0x7F) -- instead of a finite clamp that would hide a diverging activation or dY; every other block is
+    the finite quantisation; the MX GEMM then returns NaN on exactly the rows that hold such a block."""
+    g = torch.Generator(device=cuda).manual_seed(77)
+    rows, k = 256, 512
+    x = _mx_data(rows, k, g, cuda)
+    x[3, 40] = float("nan")
+    x[7, 33 * 5 + 1] = float("inf")
+    x[9, 300] = float("-inf")
+    bad = {(3, 40 // 32), (7, (33 * 5 + 1) // 32), (9, 300 // 32)}
+    q, sc = K.quant_mx_rows(x)
+    X = sc.exponents().cpu()
+    qb = q.view(torch.uint8).cpu().view(rows, k // 32, 32)
+    xc = x.clone()
+    for r, b in bad:
+        xc[r, 32 * b:32 * b + 32] = 0.0
+    qr, Xr = ref_quant_mx(xc)
+    qrb = qr.view(torch.uint8).view(rows, k // 32, 32)
+    for r in range(rows):
+        for b in range(k // 32):
+            if (r, b) in bad:
+                assert X[r, b] == 0xFF - 127 and bool((qb[r, b] == 0x7F).all()), (r, b)
+            elif r in (3, 7, 9):
+                assert X[r, b] == Xr[r, b] and torch.equal(qb[r, b], qrb[r, b]), (r, b)
+    others = [r for r in range(rows) if r not in (3, 7, 9)]
+    assert torch.equal(X[others], Xr[others]) and torch.equal(qb[others], qrb[others])
+    w = (_mx_data(384, k, g, cuda).float() * 0.02).to(BF)
+    wq, ws = K.quant_mx_rows(w)
+    out = torch.zeros(rows, 384, dtype=BF, device=cuda)
+    K.gemm_mxfp8(q, sc, wq, ws, out)
+    nanrows = torch.isnan(out.float()).all(1).cpu()
+    assert nanrows[[3, 7, 9]].all() and not nanrows[others].any()
+
+
 def _dequant_mx(q, sc):
     X = sc.exponents()
     rows, k = q.shape
