@@ -138,6 +138,7 @@ def fp8_leg(model, engine, batches, args):
     step with the Gemma2 q|k|v, o, gate|up and down projections on the fp8 (e4m3, OCP MX block-scaled) MFMA GEMM, forward and
     dgrad, weight copies re-quantised after every optimizer step; timed like the main line (barrier-free: one rank).
     roofline: the fp8 gate/up GeGLU launches inside the timed steps vs the dense fp8 peak (5 PFLOP/s)."""
+    from spatialvla_amd import functional as Fn
     from spatialvla_amd import kernels as K
     model.enable_fp8_projections(True)
     try:
@@ -146,19 +147,22 @@ def fp8_leg(model, engine, batches, args):
             engine.train_step(batches[s % n])
         torch.cuda.synchronize()
         ev = K.launch_timer["geglu_fp8"] = []
+        ev_bf = K.launch_timer["geglu"] = []  # gate|up left on bf16 (SVLA_FP8_SITES without gate_up)
         t0 = time.perf_counter()
         for s in range(args.steps):
             loss = engine.train_step(batches[s % n])
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         K.launch_timer.pop("geglu_fp8")
+        K.launch_timer.pop("geglu")
     finally:
         model.enable_fp8_projections(False)
     B = args.batch
     return {"what": "BASELINE configs[4] at N=1: fwd+bwd+AdamW with fp8 Gemma2 projections (fwd + dgrad), B=%d" % B,
             "value": round(B * args.steps / dt, 3), "unit": "episodes/s", "ms_per_step": round(dt / args.steps * 1e3, 2),
             "steps": args.steps, "final_loss": round(float(loss.item()), 4),
-            "roofline": dominant_kernel_roofline(ev, fp8=True)}
+            "fp8_sites": sorted(Fn.FP8_SITES[0]),
+            "roofline": dominant_kernel_roofline(ev, fp8=True) if ev else dominant_kernel_roofline(ev_bf)}
 
 
 def gemma2_block_roofline(model, B, L, device, iters=20):

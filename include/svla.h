@@ -132,6 +132,17 @@ int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, co
  * [rows][ldx], q bytes [rows][ldq]; K % 128 == 0. */
 int svla_quant_mx_rows(int64_t rows, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq, void* scales,
                        int64_t sld, void* stream);
+/* The same quantisation of the rows of W^T, read from W [N][ldw] bf16 without a transposed copy: q[k][n] bytes
+ * [K][ldq], blocks of 32 consecutive n, scales in svla_quant_mx_rows' layout for a [K]-row matrix (the dgrad
+ * operand of svla_gemm_mxfp8); bitwise svla_quant_mx_rows(W^T).  N % 128 == 0, K % 64 == 0, ldq % 16 == 0. */
+int svla_quant_mx_cols(int64_t N, int64_t K, const void* w, int64_t ldw, void* q, int64_t ldq, void* scales,
+                       int64_t sld, void* stream);
+/* Both MX layouts of W [R][ldw] bf16 from one read: q_rows [R][C] (blocks along C) = svla_quant_mx_rows(W) and
+ * q_cols [C][R] (blocks along R) = svla_quant_mx_rows(W^T), each with its scales in that layout (the fp8 weight
+ * copies of the forward and the dgrad GEMMs).  R % 128 == 0, C % 128 == 0, ldq_cols % 16 == 0. */
+int svla_quant_mx_both(int64_t R, int64_t C, const void* w, int64_t ldw, void* q_rows, int64_t ldq_rows, void* sc_rows,
+                       int64_t sld_rows, void* q_cols, int64_t ldq_cols, void* sc_cols, int64_t sld_cols,
+                       void* stream);
 /* C[M,N] = epilogue( sum_k 2^(Xa(m,k/32) + Xb(n,k/32)) A(m,k) B(n,k) ): A, B e4m3 KC operands as svla_gemm_fp8
  * with their MX block scales in svla_quant_mx_rows' layout (a_mx: M rows, b_mx: N rows -- GEGLU: the gate rows then
  * the up rows of one [N] scale matrix; *_ld the per-k-tile stride, *_bytes the buffer size); K and k_valid
@@ -282,6 +293,15 @@ int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* 
 int svla_add_rmsnorm2_fwd_train(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,
                                 const void* w2, float eps1, float eps2, void* h, void* x, float* rstd1, float* rstd2,
                                 void* stream);
+/* The training forwards of svla_rmsnorm_fwd and svla_add_rmsnorm2_fwd_train that also write the OCP MX e4m3 copy of
+ * the normalised output (y, resp. x): q [rows][ldq] bytes with E8M0 scales in svla_quant_mx_rows' layout (sld >= 4
+ * rows) -- bitwise svla_quant_mx_rows of the bf16 output, the fp8 q|k|v / gate|up operand without a separate
+ * pass.  N % 128 == 0. */
+int svla_rmsnorm_fwd_mx(int64_t rows, int64_t N, const void* x, const void* w, float eps, void* y, float* rstd,
+                        void* q, int64_t ldq, void* scales, int64_t sld, void* stream);
+int svla_add_rmsnorm2_fwd_train_mx(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1,
+                                   const void* w2, float eps1, float eps2, void* h, void* x, float* rstd1,
+                                   float* rstd2, void* q, int64_t ldq, void* scales, int64_t sld, void* stream);
 int svla_layernorm_fwd(int64_t rows, int64_t N, const void* x, const void* w, const void* b, float eps,
                        void* y, float* mean, float* rstd, void* stream);
 /* dwb_partial: two planes [2][ceil(rows/rows_per_block)][N] fp32 (dw partials, then db partials), reduced by
@@ -342,6 +362,13 @@ int svla_relu_bwd(int64_t n, const void* x, const void* dy, void* dx, void* stre
  * over [M, I] bf16 rows with leading dimensions (I % 8 == 0, 16-B aligned rows); dg may alias dh. */
 int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg, const void* u,
                    int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* stream);
+/* svla_geglu_bwd that also writes the MX e4m3 copy of the [dg | du] row pair -- q [M][ldq >= 2I] bytes (dg in
+ * columns 0..I-1, du in I..2I-1) with its E8M0 scales in svla_quant_mx_rows' layout (sld >= 4 M) -- bitwise
+ * svla_quant_mx_rows of the bf16 [dg | du] it stores, without reading them back (the fp8 gate|up dgrad operand).
+ * I % 128 == 0. */
+int svla_geglu_bwd_mx(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg, const void* u,
+                      int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* q, int64_t ldq, void* scales,
+                      int64_t sld, void* stream);
 int svla_add_bf16(int64_t n, const void* a, const void* b, void* out, void* stream);
 /* GELU pass over a [M][N] bf16 matrix (N % 8 == 0), the rounding points of the fused GEMM epilogues: mode 0
  * y = bf16(gelu_tanh(x)) (SigLIP MLP fc1 activation, transformers SiglipMLP gelu_pytorch_tanh), 1 y = bf16(gelu_erf(x))

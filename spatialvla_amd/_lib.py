@@ -77,6 +77,8 @@ SIGNATURES = {
     "svla_quant_fp8_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "svla_transpose_u8": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "svla_quant_mx_rows": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "svla_quant_mx_cols": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "svla_quant_mx_both": (c_i32, [c_i64, c_i64, c_vp, c_i64] + [c_vp, c_i64, c_vp, c_i64] * 2 + [c_vp]),
     "svla_gemm_mxfp8": (c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(Operand), c_vp, c_i64, c_i64,
                                 ctypes.POINTER(Operand), c_vp, c_i64, c_i64, ctypes.POINTER(c_vp),
                                 ctypes.POINTER(c_i64), c_i32, c_i64, ctypes.POINTER(Epilogue), c_vp, ctypes.c_size_t,
@@ -101,6 +103,9 @@ SIGNATURES = {
     "svla_add_rmsnorm2_fwd_train": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp,
                                             c_vp]),
     "svla_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),
+    "svla_rmsnorm_fwd_mx": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "svla_add_rmsnorm2_fwd_train_mx": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
+                                               c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "svla_rmsnorm_bwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp]),
     "svla_add_rmsnorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp]),
     "svla_layernorm_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp]),
@@ -141,6 +146,7 @@ SIGNATURES = {
                            c_vp, c_vp]),
     "svla_clip_scale": (c_i32, [c_vp, c_f32, c_vp, c_vp, c_vp]),
     "svla_geglu_bwd": (c_i32, [c_i64, c_i64] + [c_vp, c_i64] * 5 + [c_vp]),
+    "svla_geglu_bwd_mx": (c_i32, [c_i64, c_i64] + [c_vp, c_i64] * 7 + [c_vp]),
     "svla_upsample_bilinear_nhwc": (c_i32, [c_i32] * 7 + [c_f32, c_f32, c_vp, c_vp, c_vp]),
     "svla_zoe_readout_cat": (c_i32, [c_i64] * 3 + [c_vp] * 3),
     "svla_zoe_attractor": (c_i32, [c_i32] * 5 + [c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_f32, c_i32,

@@ -5,13 +5,10 @@
 // sees one bf16 read and one fp8 write per element.
 #include "svla_common.h"
 
+#include <cstdlib>
+
 namespace {
 
-__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  return (uint32_t)w;
-}
 
 template <int NCH>
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(int64_t rows, int64_t K, const bf16_t* __restrict__ x,
@@ -154,52 +151,183 @@ __global__ __launch_bounds__(256) void transpose_u8_kernel(int64_t R, int64_t C,
 // one 128-k tile's scales of 256 consecutive rows are 1 KiB contiguous (one LDS-DMA piece per operand and k-tile in
 // the MX GEMM).  Lane layout: 8 elements a lane (one 16-B load), 4 lanes a block (amax by two xor shuffles), 16
 // lanes a k-tile (the 4 scale bytes gathered into one dword store), a wave 512 k of one row.
-__device__ __forceinline__ int mx_exponent(float amax) {
-  const uint32_t u = __float_as_uint(amax);
-  const int e = (int)((u >> 23) & 0xff);            // floor(log2(amax)) + 127 for normal amax; 0: zero / subnormal
-  const int up = (u & 0x7fffffu) > 0x600000u;       // amax * 2^-(floor(log2 amax) - 8) > 448: one more power of two
-  return max(-127, min(127, e - 127 - 8 + up));     // subnormal or zero amax: clamps to -127 (byte 0)
+
+// one (row, 512-k chunk) item of quant_mx_rows: the wave's 8 elements a lane already loaded into v
+__device__ __forceinline__ void mx_item(const u32x4 v, bool ok, int64_t r, int64_t k, uint8_t* __restrict__ q,
+                                        int64_t ldq, uint8_t* __restrict__ sc, int64_t sld) {
+  float f[8];
+  if (ok) unpack8(v, f);
+  else
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  mx_store8(f, ok, q + r * ldq + k, sc + (k / 128) * sld + r * 4);
 }
 
+// U consecutive items a wave, every item's 16-B load issued before the first is converted (one item a wave left a
+// single 1 KiB load in flight per wave and ran at ~1.2 TB/s in the fp8 training step, profiles/r8b)
+template <int U>
 __global__ __launch_bounds__(256) void quant_mx_rows_kernel(int64_t rows, int64_t K, const bf16_t* __restrict__ x,
                                                             int64_t ldx, uint8_t* __restrict__ q, int64_t ldq,
                                                             uint8_t* __restrict__ sc, int64_t sld) {
   const int lane = threadIdx.x & 63;
   const int64_t chunks = (K + 511) / 512;
-  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (row, 512-k chunk)
-  if (item >= rows * chunks) return;
-  const int64_t r = item / chunks, k = (item % chunks) * 512 + 8 * lane;
-  const bool ok = k < K;  // K % 128 == 0: whole 16-lane k-tiles are in or out together
-  float f[8];
-  if (ok) unpack8(*reinterpret_cast<const u32x4*>(x + r * ldx + k), f);
-  else
+  const int64_t items = rows * chunks;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * U;  // (row, 512-k chunk) items
+  if (base >= items) return;
+  u32x4 v[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  for (int u = 0; u < U; ++u) {
+    const int64_t it = base + u < items ? base + u : items - 1;
+    const int64_t r = it / chunks, k = (it % chunks) * 512 + 8 * lane;
+    v[u] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(x + r * ldx + k)) : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t it = base + u;
+    if (it >= items) break;
+    const int64_t r = it / chunks, k = (it % chunks) * 512 + 8 * lane;
+    mx_item(v[u], k < K, r, k, q, ldq, sc, sld);  // K % 128 == 0: whole 16-lane k-tiles are in or out together
+  }
+}
+
+// MX quantisation of the columns of W [N][K] into the rows of W^T: q[k][n] = e4m3 of W[n][k] with one E8M0 scale per
+// 32 consecutive n of column k, the layout quant_mx_rows gives for W^T (rows = K, reduction dim = N), bit for bit --
+// without materialising the bf16 W^T.  A 256-thread block owns a 128 (n) x 64 (k) tile: each lane loads 16-B row
+// pieces (8 consecutive k of one n), writes them transposed into LDS, then thread (k, b) reads the 32 n of block b of
+// column k as four 16-B LDS reads, forms the block's scale in registers and stores 32 e4m3 bytes; the 4 scale bytes of
+// a 128-n tile (threads b = 0..3 of one k) leave as one dword.
+constexpr int QC_N = 128, QC_K = 64, QC_P = QC_N + 8;  // LDS row pitch (bf16): 16-B aligned rows
+__global__ __launch_bounds__(256) void quant_mx_cols_kernel(int64_t N, int64_t K, const bf16_t* __restrict__ w,
+                                                            int64_t ldw, uint8_t* __restrict__ q, int64_t ldq,
+                                                            uint8_t* __restrict__ sc, int64_t sld) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[QC_K][QC_P];
+  const int t = threadIdx.x;
+  const int64_t n0 = (int64_t)blockIdx.x * QC_N, k0 = (int64_t)blockIdx.y * QC_K;
+  u32x4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nl = (t >> 3) + 32 * i, kc = (t & 7) * 8;
+    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + (n0 + nl) * ldw + k0 + kc));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nl = (t >> 3) + 32 * i, kc = (t & 7) * 8;
+    const uint32_t e[4] = {v[i][0], v[i][1], v[i][2], v[i][3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tile[kc + 2 * j][nl] = (bf16_t)(e[j] & 0xffffu);
+      tile[kc + 2 * j + 1][nl] = (bf16_t)(e[j] >> 16);
+    }
+  }
+  __syncthreads();
+  const int kl = t >> 2, b = t & 3;
+  float f[32];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) unpack8(*reinterpret_cast<const u32x4*>(&tile[kl][32 * b + 8 * c]), f + 8 * c);
   float amax = 0.f;
-  int nonfinite = 0;  // a NaN or +-Inf element: the block becomes NaN (scale 0xFF, OCP MX §5.3), not a finite clamp
+  int nonfinite = 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < 32; ++j) {
     amax = fmaxf(amax, fabsf(f[j]));
     nonfinite |= (__float_as_uint(f[j]) & 0x7f800000u) == 0x7f800000u;
   }
-  amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-  nonfinite |= __shfl_xor(nonfinite, 1, 64);
-  nonfinite |= __shfl_xor(nonfinite, 2, 64);
   const int X = mx_exponent(amax);
-  const float inv = __uint_as_float((uint32_t)(127 - X) << 23);  // 2^-X exactly (X >= -127 -> exponent <= 254)
+  const float inv = __uint_as_float((uint32_t)(127 - X) << 23);
+  u32x4 o[2];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -448.f), 448.f);
-  u32x2 qv = u32x2{cvt4(f[0], f[1], f[2], f[3]), cvt4(f[4], f[5], f[6], f[7])};
-  if (nonfinite) qv = u32x2{0x7f7f7f7fu, 0x7f7f7f7fu};  // e4m3 NaN elements as well: NaN whatever the scale decodes to
-  if (ok) *reinterpret_cast<u32x2*>(q + r * ldq + k) = qv;
-  // scale bytes of the k-tile's 4 blocks (lanes 4b of the 16-lane group) -> one dword
-  uint32_t byte = nonfinite ? 0xffu : (uint32_t)(127 + X);
-  uint32_t w = byte;
-  w |= (uint32_t)__shfl_down((int)byte, 4, 16) << 8;
-  w |= (uint32_t)__shfl_down((int)byte, 8, 16) << 16;
-  w |= (uint32_t)__shfl_down((int)byte, 12, 16) << 24;
-  if (ok && (lane & 15) == 0) *reinterpret_cast<uint32_t*>(sc + (k / 128) * sld + r * 4) = w;
+  for (int h = 0; h < 2; ++h) {
+    uint32_t wd[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float g[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = fminf(fmaxf(f[16 * h + 4 * j + e] * inv, -448.f), 448.f);
+      wd[j] = nonfinite ? 0x7f7f7f7fu : cvt4(g[0], g[1], g[2], g[3]);
+    }
+    o[h] = u32x4{wd[0], wd[1], wd[2], wd[3]};
+  }
+  uint8_t* qr = q + (k0 + kl) * ldq + n0 + 32 * b;
+  *reinterpret_cast<u32x4*>(qr) = o[0];
+  *reinterpret_cast<u32x4*>(qr + 16) = o[1];
+  const uint32_t byte = nonfinite ? 0xffu : (uint32_t)(127 + X);
+  uint32_t wsc = byte;
+  wsc |= (uint32_t)__shfl_down((int)byte, 1, 4) << 8;
+  wsc |= (uint32_t)__shfl_down((int)byte, 2, 4) << 16;
+  wsc |= (uint32_t)__shfl_down((int)byte, 3, 4) << 24;
+  if (b == 0) *reinterpret_cast<uint32_t*>(sc + (n0 / 128) * sld + (k0 + kl) * 4) = wsc;
+}
+
+// Both MX layouts of one bf16 matrix W [R][C] from a single read (the fp8 weight copies: the forward operand W with
+// blocks along C and the dgrad operand W^T with blocks along R; bitwise quant_mx_rows(W) and quant_mx_rows(W^T)).
+// A 256-thread block owns a 128 x 128 tile: lane t loads 8 row pieces (row (t >> 4) + 16 i, columns (t & 15) * 8 ..
+// + 8), quantises them in place for the row layout (16 lanes = one row's 128-column k-tile, mx_store8), and writes
+// them transposed into LDS; then each thread quantises two 32-row blocks of a column for the W^T layout.
+constexpr int QB_T = 128, QB_P = QB_T + 8;
+__global__ __launch_bounds__(256) void quant_mx_both_kernel(int64_t R, int64_t C, const bf16_t* __restrict__ w,
+                                                            int64_t ldw, uint8_t* __restrict__ qr, int64_t ldqr,
+                                                            uint8_t* __restrict__ scr, int64_t sldr,
+                                                            uint8_t* __restrict__ qc, int64_t ldqc,
+                                                            uint8_t* __restrict__ scc, int64_t sldc) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[QB_T][QB_P];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * QB_T, c0 = (int64_t)blockIdx.y * QB_T;
+  const int kc = (t & 15) * 8;
+  u32x4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w + (r0 + (t >> 4) + 16 * i) * ldw + c0 + kc));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rl = (t >> 4) + 16 * i;
+    const uint32_t e[4] = {v[i][0], v[i][1], v[i][2], v[i][3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tile[kc + 2 * j][rl] = (bf16_t)(e[j] & 0xffffu);
+      tile[kc + 2 * j + 1][rl] = (bf16_t)(e[j] >> 16);
+    }
+    float f[8];
+    unpack8(v[i], f);
+    mx_store8(f, true, qr + (r0 + rl) * ldqr + c0 + kc, scr + ((c0 + kc) / 128) * sldr + (r0 + rl) * 4);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int cl = (t >> 2) + 64 * p, b = t & 3;
+    float f[32];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) unpack8(*reinterpret_cast<const u32x4*>(&tile[cl][32 * b + 8 * c]), f + 8 * c);
+    float amax = 0.f;
+    int nonfinite = 0;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      amax = fmaxf(amax, fabsf(f[j]));
+      nonfinite |= (__float_as_uint(f[j]) & 0x7f800000u) == 0x7f800000u;
+    }
+    const int X = mx_exponent(amax);
+    const float inv = __uint_as_float((uint32_t)(127 - X) << 23);
+    u32x4 o[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t wd[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = fminf(fmaxf(f[16 * h + 4 * j + e] * inv, -448.f), 448.f);
+        wd[j] = nonfinite ? 0x7f7f7f7fu : cvt4(g[0], g[1], g[2], g[3]);
+      }
+      o[h] = u32x4{wd[0], wd[1], wd[2], wd[3]};
+    }
+    uint8_t* q = qc + (c0 + cl) * ldqc + r0 + 32 * b;
+    *reinterpret_cast<u32x4*>(q) = o[0];
+    *reinterpret_cast<u32x4*>(q + 16) = o[1];
+    const uint32_t byte = nonfinite ? 0xffu : (uint32_t)(127 + X);
+    uint32_t wsc = byte;
+    wsc |= (uint32_t)__shfl_down((int)byte, 1, 4) << 8;
+    wsc |= (uint32_t)__shfl_down((int)byte, 2, 4) << 16;
+    wsc |= (uint32_t)__shfl_down((int)byte, 3, 4) << 24;
+    if (b == 0) *reinterpret_cast<uint32_t*>(scc + (r0 / 128) * sldc + (c0 + cl) * 4) = wsc;
+  }
 }
 
 }  // namespace
@@ -213,9 +341,36 @@ extern "C" int svla_quant_mx_rows(int64_t rows, int64_t K, const void* x, int64_
                  "quant_mx_rows: pointers / leading dimensions");
   SVLA_CHECK_ARG(sld >= 4 * rows && sld % 4 == 0, "quant_mx_rows: scale tile stride %lld < 4 * rows", (long long)sld);
   const int64_t items = rows * ((K + 511) / 512);
-  hipLaunchKernelGGL(quant_mx_rows_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, (hipStream_t)stream, rows,
-                     K, (const bf16_t*)x, ldx, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  static int U = -1;  // SVLA_QUANT_MX_ITEMS: items a wave (1, 2, 4 or 8; default 4)
+  if (U < 0) {
+    const char* e = getenv("SVLA_QUANT_MX_ITEMS");
+    U = e ? atoi(e) : 4;
+    if (U != 1 && U != 2 && U != 8) U = 4;
+  }
+  const dim3 grid((unsigned)((items + 4 * U - 1) / (4 * U)));
+  hipStream_t s = (hipStream_t)stream;
+#define SVLA_QMX(UU)                                                                                              \
+  hipLaunchKernelGGL(quant_mx_rows_kernel<UU>, grid, dim3(256), 0, s, rows, K, (const bf16_t*)x, ldx, (uint8_t*)q, \
+                     ldq, (uint8_t*)scales, sld)
+  if (U == 1) SVLA_QMX(1);
+  else if (U == 2) SVLA_QMX(2);
+  else if (U == 8) SVLA_QMX(8);
+  else SVLA_QMX(4);
+#undef SVLA_QMX
   return svla::check_launch("quant_mx_rows");
+}
+
+extern "C" int svla_quant_mx_cols(int64_t N, int64_t K, const void* w, int64_t ldw, void* q, int64_t ldq, void* scales,
+                                  int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(N > 0 && K > 0 && N % QC_N == 0 && K % QC_K == 0,
+                 "quant_mx_cols: N=%lld (a multiple of 128), K=%lld (a multiple of 64)", (long long)N, (long long)K);
+  SVLA_CHECK_ARG(w && q && scales && ldw >= K && ldq >= N && ldw % 8 == 0 && ldq % 16 == 0 &&
+                     ((uintptr_t)w & 15) == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)scales & 3) == 0,
+                 "quant_mx_cols: pointers / leading dimensions");
+  SVLA_CHECK_ARG(sld >= 4 * K && sld % 4 == 0, "quant_mx_cols: scale tile stride %lld < 4 * K", (long long)sld);
+  hipLaunchKernelGGL(quant_mx_cols_kernel, dim3((unsigned)(N / QC_N), (unsigned)(K / QC_K)), dim3(256), 0,
+                     (hipStream_t)stream, N, K, (const bf16_t*)w, ldw, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("quant_mx_cols");
 }
 
 extern "C" int svla_transpose_u8(int64_t R, int64_t C, const void* in, int64_t ldi, void* out, int64_t ldo,
@@ -249,4 +404,23 @@ extern "C" int svla_quant_fp8_rows(int64_t rows, int64_t K, const void* x, int64
     hipLaunchKernelGGL(quant_fp8_rows_stream_kernel, grid, block, 0, s, rows, K, (const bf16_t*)x, ldx, colscale,
                        (uint8_t*)q, ldq, scale);
   return svla::check_launch("quant_fp8_rows");
+}
+
+extern "C" int svla_quant_mx_both(int64_t R, int64_t C, const void* w, int64_t ldw, void* q_rows, int64_t ldq_rows,
+                                  void* sc_rows, int64_t sld_rows, void* q_cols, int64_t ldq_cols, void* sc_cols,
+                                  int64_t sld_cols, void* stream) {
+  SVLA_CHECK_ARG(R > 0 && C > 0 && R % QB_T == 0 && C % QB_T == 0, "quant_mx_both: R=%lld, C=%lld (multiples of 128)",
+                 (long long)R, (long long)C);
+  SVLA_CHECK_ARG(w && q_rows && sc_rows && q_cols && sc_cols && ldw >= C && ldw % 8 == 0 && ((uintptr_t)w & 15) == 0,
+                 "quant_mx_both: W pointer / leading dimension");
+  SVLA_CHECK_ARG(ldq_rows >= C && ldq_rows % 8 == 0 && ((uintptr_t)q_rows & 7) == 0 && sld_rows >= 4 * R &&
+                     sld_rows % 4 == 0 && ((uintptr_t)sc_rows & 3) == 0,
+                 "quant_mx_both: row-layout output");
+  SVLA_CHECK_ARG(ldq_cols >= R && ldq_cols % 16 == 0 && ((uintptr_t)q_cols & 15) == 0 && sld_cols >= 4 * C &&
+                     sld_cols % 4 == 0 && ((uintptr_t)sc_cols & 3) == 0,
+                 "quant_mx_both: column-layout output");
+  hipLaunchKernelGGL(quant_mx_both_kernel, dim3((unsigned)(R / QB_T), (unsigned)(C / QB_T)), dim3(256), 0,
+                     (hipStream_t)stream, R, C, (const bf16_t*)w, ldw, (uint8_t*)q_rows, ldq_rows, (uint8_t*)sc_rows,
+                     sld_rows, (uint8_t*)q_cols, ldq_cols, (uint8_t*)sc_cols, sld_cols);
+  return svla::check_launch("quant_mx_both");
 }

@@ -187,7 +187,9 @@ __global__ void relu_bwd_kernel(int64_t n, const bf16_t* __restrict__ x, const b
 __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, const bf16_t* dh, int64_t ldh,
                                                         const bf16_t* __restrict__ g, int64_t ldg,
                                                         const bf16_t* __restrict__ u, int64_t ldu, bf16_t* dg,
-                                                        int64_t lddg, bf16_t* __restrict__ du, int64_t lddu) {
+                                                        int64_t lddg, bf16_t* __restrict__ du, int64_t lddu,
+                                                        uint8_t* __restrict__ q, int64_t ldq, uint8_t* __restrict__ sc,
+                                                        int64_t sld) {
   const int64_t cpr = I / 8;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= M * cpr) return;
@@ -205,6 +207,15 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t M, int64_t I, co
   }
   *reinterpret_cast<u32x4*>(dg + m * lddg + c) = pack8(og);
   *reinterpret_cast<u32x4*>(du + m * lddu + c) = pack8(ou);
+  if (q != nullptr) {  // also the MX e4m3 copy of [dg | du] (the fp8 dgrad operand), from the bf16 values just stored
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      og[j] = round_bf(og[j]);
+      ou[j] = round_bf(ou[j]);
+    }
+    mx_store8(og, true, q + m * ldq + c, sc + (c / 128) * sld + m * 4);
+    mx_store8(ou, true, q + m * ldq + I + c, sc + ((I + c) / 128) * sld + m * 4);
+  }
 }
 
 // GELU as an HBM pass after a plain-store / bias GEMM (svla_gelu_rows): the VALU-heavy GELU epilogues ran slower
@@ -714,8 +725,25 @@ extern "C" int svla_geglu_bwd(int64_t M, int64_t I, const void* dh, int64_t ldh,
                  "geglu_bwd: rows must be 16-B aligned");
   hipLaunchKernelGGL(geglu_bwd_kernel, dim3(nblk(M * (I / 8), 256)), dim3(256), 0, (hipStream_t)stream, M, I,
                      (const bf16_t*)dh, ldh, (const bf16_t*)g, ldg, (const bf16_t*)u, ldu, (bf16_t*)dg, lddg,
-                     (bf16_t*)du, lddu);
+                     (bf16_t*)du, lddu, (uint8_t*)nullptr, (int64_t)0, (uint8_t*)nullptr, (int64_t)0);
   return svla::check_launch("geglu_bwd");
+}
+
+extern "C" int svla_geglu_bwd_mx(int64_t M, int64_t I, const void* dh, int64_t ldh, const void* g, int64_t ldg,
+                                 const void* u, int64_t ldu, void* dg, int64_t lddg, void* du, int64_t lddu, void* q,
+                                 int64_t ldq, void* scales, int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(M > 0 && I > 0 && I % 128 == 0 && dh && g && u && dg && du && q && scales,
+                 "geglu_bwd_mx: bad args (I a multiple of 128)");
+  SVLA_CHECK_ARG(ldh % 8 == 0 && ldg % 8 == 0 && ldu % 8 == 0 && lddg % 8 == 0 && lddu % 8 == 0 && al16(dh) &&
+                     al16(g) && al16(u) && al16(dg) && al16(du),
+                 "geglu_bwd_mx: rows must be 16-B aligned");
+  SVLA_CHECK_ARG(ldq >= 2 * I && ldq % 8 == 0 && ((uintptr_t)q & 7) == 0 && ((uintptr_t)scales & 3) == 0 &&
+                     sld >= 4 * M && sld % 4 == 0,
+                 "geglu_bwd_mx: q [M][ldq >= 2I] 8-B rows, scale tile stride >= 4 M");
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(nblk(M * (I / 8), 256)), dim3(256), 0, (hipStream_t)stream, M, I,
+                     (const bf16_t*)dh, ldh, (const bf16_t*)g, ldg, (const bf16_t*)u, ldu, (bf16_t*)dg, lddg,
+                     (bf16_t*)du, lddu, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("geglu_bwd_mx");
 }
 
 extern "C" int svla_gelu_rows(int64_t M, int64_t N, int32_t mode, const void* x, int64_t ldx, const void* pre,

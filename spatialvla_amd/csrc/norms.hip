@@ -25,10 +25,14 @@ __device__ __forceinline__ void st8(bf16_t* p, const float* f) { *reinterpret_ca
 // ------------------------------------------------------------------ RMSNorm forward
 // RES = false: y = rms(x; w)                 (Gemma2RMSNorm.forward, modeling_gemma2.py:69-74)
 // RES = true : h = bf16(res + bf16(rms(x; w)))  (decoder residual, :489-490 / :495-496)
+// q != NULL (RES = false): also the OCP MX e4m3 copy of y (the fp8 projection operand; bitwise svla_quant_mx_rows of
+// the stored bf16 y; N % 128 == 0 so every 16-lane group holds one whole 128-column k-tile)
 template <bool RES>
 __global__ __launch_bounds__(NTH) void rms_fwd_kernel(int64_t N, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ res, const bf16_t* __restrict__ w,
-                                                      float eps, bf16_t* __restrict__ y, float* __restrict__ rstd_out) {
+                                                      float eps, bf16_t* __restrict__ y, float* __restrict__ rstd_out,
+                                                      uint8_t* __restrict__ q = nullptr, int64_t ldq = 0,
+                                                      uint8_t* __restrict__ sc = nullptr, int64_t sld = 0) {
   __shared__ float red[16];
   const int64_t row = blockIdx.x;
   const int nch = (int)(N >> 3);
@@ -62,6 +66,11 @@ __global__ __launch_bounds__(NTH) void rms_fwd_kernel(int64_t N, const bf16_t* _
         for (int j = 0; j < 8; ++j) o[j] = r[j] + round_bf(o[j]);
       }
       st8(y + row * N + ch * 8, o);
+      if (!RES && q != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]);
+        mx_store8(o, true, q + row * ldq + ch * 8, sc + (ch / 16) * sld + row * 4);
+      }
     }
   }
 }
@@ -76,7 +85,9 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
                                                             const bf16_t* __restrict__ w1,
                                                             const bf16_t* __restrict__ w2, float eps1, float eps2,
                                                             bf16_t* __restrict__ h, bf16_t* __restrict__ x,
-                                                            float* __restrict__ rstd1_out, float* __restrict__ rstd2_out) {
+                                                            float* __restrict__ rstd1_out, float* __restrict__ rstd2_out,
+                                                            uint8_t* __restrict__ q = nullptr, int64_t ldq = 0,
+                                                            uint8_t* __restrict__ sc = nullptr, int64_t sld = 0) {
   __shared__ float red[16];
   const int64_t row = blockIdx.x;
   const int nch = (int)(N >> 3);
@@ -123,6 +134,11 @@ __global__ __launch_bounds__(NTH) void rms_add_norm2_kernel(int64_t N, const bf1
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[c][j] * rstd2) * (1.0f + wf[j]);
       st8(x + row * N + ch * 8, o);
+      if (q != nullptr) {  // the MX copy of x (as rms_fwd_kernel's)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]);
+        mx_store8(o, true, q + row * ldq + ch * 8, sc + (ch / 16) * sld + row * 4);
+      }
     }
   }
 }
@@ -932,4 +948,32 @@ extern "C" int svla_add_rmsnorm2_fwd_train(int64_t rows, int64_t N, const void* 
                      (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
                      (bf16_t*)h, (bf16_t*)x, rstd1, rstd2);
   return svla::check_launch("add_rmsnorm2_fwd_train");
+}
+
+extern "C" int svla_rmsnorm_fwd_mx(int64_t rows, int64_t N, const void* x, const void* w, float eps, void* y,
+                                   float* rstd, void* q, int64_t ldq, void* scales, int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 128 == 0 && N <= NTH * MAXC * 8, "rmsnorm_mx: bad N=%lld (a multiple of 128)",
+                 (long long)N);
+  SVLA_CHECK_ARG(x && w && y && q && scales && al16(x) && al16(w) && al16(y) && ldq >= N && ldq % 8 == 0 &&
+                     ((uintptr_t)q & 7) == 0 && ((uintptr_t)scales & 3) == 0 && sld >= 4 * rows && sld % 4 == 0,
+                 "rmsnorm_mx: null/misaligned pointer or bad q / scale strides");
+  hipLaunchKernelGGL((rms_fwd_kernel<false>), dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)x, (const bf16_t*)nullptr, (const bf16_t*)w, eps, (bf16_t*)y, rstd, (uint8_t*)q,
+                     ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("rmsnorm_fwd_mx");
+}
+
+extern "C" int svla_add_rmsnorm2_fwd_train_mx(int64_t rows, int64_t N, const void* res, const void* yin,
+                                              const void* w1, const void* w2, float eps1, float eps2, void* h, void* x,
+                                              float* rstd1, float* rstd2, void* q, int64_t ldq, void* scales,
+                                              int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 128 == 0 && N <= NTH * MAXC * 8, "add_rmsnorm2_mx: bad N");
+  SVLA_CHECK_ARG(res && yin && w1 && w2 && h && x && rstd1 && rstd2 && q && scales && al16(res) && al16(yin) &&
+                     al16(w1) && al16(w2) && al16(h) && al16(x) && ldq >= N && ldq % 8 == 0 && ((uintptr_t)q & 7) == 0 &&
+                     ((uintptr_t)scales & 3) == 0 && sld >= 4 * rows && sld % 4 == 0,
+                 "add_rmsnorm2_mx: null/misaligned pointer or bad q / scale strides");
+  hipLaunchKernelGGL(rms_add_norm2_kernel, dim3((unsigned)rows), dim3(NTH), 0, (hipStream_t)stream, N,
+                     (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
+                     (bf16_t*)h, (bf16_t*)x, rstd1, rstd2, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("add_rmsnorm2_fwd_train_mx");
 }

@@ -170,3 +170,51 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   void* pb = (void*)(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)SVLA_OOB, 0x00020000);
 }
+
+// ---- e4m3 / OCP MX helpers (fp8.hip's quantisers and the producers that emit MX operands: misc.hip geglu_bwd)
+// four fp32 -> four e4m3 bytes (RNE), packed in one dword
+__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+// E8M0 exponent of an MX block: X = ceil(log2(amax / 448)) (the smallest power of two that maps the block maximum
+// into e4m3's range), clamped to [-127, 127]; zero or subnormal amax -> -127 (fp8.hip quant_mx_rows documents it)
+__device__ __forceinline__ int mx_exponent(float amax) {
+  const uint32_t u = __float_as_uint(amax);
+  const int e = (int)((u >> 23) & 0xff);            // floor(log2(amax)) + 127 for normal amax; 0: zero / subnormal
+  const int up = (u & 0x7fffffu) > 0x600000u;       // amax * 2^-(floor(log2 amax) - 8) > 448: one more power of two
+  return max(-127, min(127, e - 127 - 8 + up));     // subnormal or zero amax: clamps to -127 (byte 0)
+}
+// MX quantisation of 8 consecutive elements a lane (OCP MX: 4 lanes = one 32-element block, 16 lanes = one 128-element
+// k-tile; lane groups aligned to both): block amax by two xor shuffles, e4m3(x * 2^-X) (RNE, clamped to +-448) to q8
+// (8 bytes), and the 4 E8M0 bytes of the 16-lane group gathered into the dword the group's first lane stores at sc4.
+// A NaN / +-Inf element makes its block NaN (scale 0xFF and e4m3 NaN elements).  Every lane of the 16-lane group must
+// call it (the shuffles); `ok` false: the lane stores nothing (its f must then be finite, e.g. zeros).
+__device__ __forceinline__ void mx_store8(float* f, bool ok, uint8_t* q8, uint8_t* sc4) {
+  const int lane = threadIdx.x & 63;
+  float amax = 0.f;
+  int nonfinite = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    amax = fmaxf(amax, fabsf(f[j]));
+    nonfinite |= (__float_as_uint(f[j]) & 0x7f800000u) == 0x7f800000u;
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+  nonfinite |= __shfl_xor(nonfinite, 1, 64);
+  nonfinite |= __shfl_xor(nonfinite, 2, 64);
+  const int X = mx_exponent(amax);
+  const float inv = __uint_as_float((uint32_t)(127 - X) << 23);  // 2^-X exactly (X >= -127 -> exponent <= 254)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(f[j] * inv, -448.f), 448.f);
+  u32x2 qv = u32x2{cvt4(f[0], f[1], f[2], f[3]), cvt4(f[4], f[5], f[6], f[7])};
+  if (nonfinite) qv = u32x2{0x7f7f7f7fu, 0x7f7f7f7fu};
+  if (ok) *reinterpret_cast<u32x2*>(q8) = qv;
+  const uint32_t byte = nonfinite ? 0xffu : (uint32_t)(127 + X);
+  uint32_t w = byte;
+  w |= (uint32_t)__shfl_down((int)byte, 4, 16) << 8;
+  w |= (uint32_t)__shfl_down((int)byte, 8, 16) << 16;
+  w |= (uint32_t)__shfl_down((int)byte, 12, 16) << 24;
+  if (ok && (lane & 15) == 0) *reinterpret_cast<uint32_t*>(sc4) = w;
+}

@@ -129,16 +129,44 @@ class ResidualSlot:
         return g
 
 
+class MXSlot:
+    """Hand-off of an activation's OCP MX e4m3 copy from the kernel that produced the bf16 tensor (a norm forward) to
+    the fp8 projection that reads it (configs[4]): the producer writes both in one pass, the consumer takes the copy
+    instead of quantising the tensor again.  `ptr` ties the copy to the bf16 tensor it was made from."""
+    __slots__ = ("val", "ptr")
+
+    def __init__(self):
+        self.val, self.ptr = None, None
+
+    def put(self, t, val):
+        self.val, self.ptr = val, t.data_ptr()
+
+    def take(self, t):
+        """The copy of t if this slot holds one (else None); the slot is emptied either way."""
+        v, p = self.val, self.ptr
+        self.val, self.ptr = None, None
+        return v if v is not None and p == t.data_ptr() else None
+
+
+def mx_slot_for(f8, site) -> Optional[MXSlot]:
+    """An MXSlot when projection `site` runs in fp8 with MX scales (producers then emit the copy), else None."""
+    return MXSlot() if f8 is not None and site in FP8_SITES[0] and FP8_SCALING[0] == "mx" else None
+
+
 # ------------------------------------------------------------------------------------ norms
 class RMSNormFn(torch.autograd.Function):
-    """Gemma2RMSNorm.forward (reference model/modeling_gemma2.py:69-74)."""
+    """Gemma2RMSNorm.forward (reference model/modeling_gemma2.py:69-74).  mx: an MXSlot that receives the MX e4m3
+    copy of y, made by the same launch (the fp8 q|k|v operand)."""
 
     @staticmethod
-    def forward(ctx, x, w, eps, slot=None):
+    def forward(ctx, x, w, eps, slot=None, mx=None):
         x = _c(x)
         y = torch.empty_like(x)
         rstd = _empty(x.shape[0], dtype=F32, like=x)
-        K.rmsnorm_fwd(x, w, eps, y, rstd)
+        if mx is not None and x.shape[1] % 128 == 0:
+            mx.put(y, K.rmsnorm_fwd_mx(x, w, eps, y, rstd))
+        else:
+            K.rmsnorm_fwd(x, w, eps, y, rstd)
         ctx.save_for_backward(x, w, rstd)
         ctx.slot = slot
         return y
@@ -150,7 +178,7 @@ class RMSNormFn(torch.autograd.Function):
         dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[1])
         dres = ctx.slot.take() if ctx.slot is not None else None
         K.rmsnorm_bwd(x, w, rstd, _c(dy), None if dres is None else _c(dres), dx, dw, dw_accumulate=acc)
-        return dx, ret, None, None
+        return dx, ret, None, None, None
 
 
 class AddRMSNormFn(torch.autograd.Function):
@@ -187,12 +215,15 @@ class AddRMSNorm2Fn(torch.autograd.Function):
     dh_total is the gradient of res (parked in slot_res for the pre-norm that also reads res, as AddRMSNormFn does)."""
 
     @staticmethod
-    def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None):
+    def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None, mx=None):
         res, y = _c(res), _c(y)
         h, x = torch.empty_like(y), torch.empty_like(y)
         r1 = _empty(y.shape[0], dtype=F32, like=y)
         r2 = _empty(y.shape[0], dtype=F32, like=y)
-        K.add_rmsnorm2_fwd_train(res, y, w1, w2, eps1, eps2, h, x, r1, r2)
+        if mx is not None and y.shape[1] % 128 == 0:  # + the MX copy of x (the fp8 gate|up operand)
+            mx.put(x, K.add_rmsnorm2_fwd_train_mx(res, y, w1, w2, eps1, eps2, h, x, r1, r2))
+        else:
+            K.add_rmsnorm2_fwd_train(res, y, w1, w2, eps1, eps2, h, x, r1, r2)
         ctx.save_for_backward(y, h, w1, w2, r1, r2)
         ctx.slots = (slot_res, slot_h)
         ctx.set_materialize_grads(False)  # h's residual gradient usually arrives through slot_h: no zero tensor
@@ -216,8 +247,8 @@ class AddRMSNorm2Fn(torch.autograd.Function):
         K.rmsnorm2_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), y, w1, r1, dht, dy, dw2, dw1, acc2, acc1)
         if slot_res is not None:
             slot_res.put(dht)
-            return None, dy, ret1, ret2, None, None, None, None
-        return dht, dy, ret1, ret2, None, None, None, None
+            return None, dy, ret1, ret2, None, None, None, None, None
+        return dht, dy, ret1, ret2, None, None, None, None, None
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -383,8 +414,13 @@ class FP8Weights:
         hit = self.mats.get(name)
         if hit is None or hit["key"] != key:
             w = self._rows(mats)
-            q, s = K.quant_mx_rows(w) if FP8_SCALING[0] == "mx" else K.quant_fp8_rows(w)
-            hit = self.mats[name] = {"key": key, "q": q, "s": s}
+            if FP8_SCALING[0] == "mx" and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0:
+                # both layouts from one read of the bf16 weight (the forward copy and the dgrad copy W^T)
+                (q, s), (qt, st) = K.quant_mx_both(w)
+                hit = self.mats[name] = {"key": key, "q": q, "s": s, "qt": qt, "st": st}
+            else:
+                q, s = K.quant_mx_rows(w) if FP8_SCALING[0] == "mx" else K.quant_fp8_rows(w)
+                hit = self.mats[name] = {"key": key, "q": q, "s": s}
         return hit
 
     def get(self, name, mats):
@@ -397,7 +433,7 @@ class FP8Weights:
         e = self._entry(name, mats)
         if "qt" not in e:
             if FP8_SCALING[0] == "mx":
-                e["qt"], e["st"] = K.quant_mx_rows(self._rows(mats).t().contiguous())
+                e["qt"], e["st"] = K.quant_mx_cols(self._rows(mats))  # W^T's rows, no transposed copy
             else:
                 e["qt"], e["st"] = K.transpose_u8(e["q"]), e["s"]
         return e["qt"], e["st"]
@@ -409,24 +445,26 @@ class FP8Weights:
         return o
 
 
-def _fp8_linear(x, f8, name, mats, out, **kw):
-    """out = epi(x @ cat(mats)^T) with both operands quantised to e4m3 (x per call, weights cached)."""
+def _fp8_linear(x, f8, name, mats, out, x_mx=None, **kw):
+    """out = epi(x @ cat(mats)^T) with both operands quantised to e4m3 (x per call -- or x_mx, the MX copy x's
+    producer already made -- weights cached)."""
     wq, ws = f8.get(name, mats)
     if FP8_SCALING[0] == "mx":
-        xq, xs = K.quant_mx_rows(x)
+        xq, xs = x_mx if x_mx is not None else K.quant_mx_rows(x)
         K.gemm_mxfp8(xq, xs, wq, ws, out, **kw)
     else:
         xq, xs = K.quant_fp8_rows(x)
         K.gemm_fp8(xq, xs, wq, ws, out, **kw)
 
 
-def _fp8_dgrad(dy, f8, name, mats, out):
+def _fp8_dgrad(dy, f8, name, mats, out, dy_mx=None):
     """out[M, K] = dy[M, N] @ cat(mats)[N, K] on the fp8 GEMM.  MX: dy quantised with blocks along N against the
-    MX copy of W^T.  Row scaling: the forward's e4m3 weight W ~ diag(s_w) W_q reused transposed -- dy's columns are
-    scaled by s_w before dy is quantised per row, so out = s_dy[m] * sum_n q_dy[m, n] W_q[n, k]."""
+    MX copy of W^T (dy_mx: that quantisation already made by dy's producer).  Row scaling: the forward's e4m3 weight
+    W ~ diag(s_w) W_q reused transposed -- dy's columns are scaled by s_w before dy is quantised per row, so
+    out = s_dy[m] * sum_n q_dy[m, n] W_q[n, k]."""
     wt, st = f8.get_t(name, mats)
     if FP8_SCALING[0] == "mx":
-        dq, ds = K.quant_mx_rows(dy)
+        dq, ds = dy_mx if dy_mx is not None else K.quant_mx_rows(dy)
         K.gemm_mxfp8(dq, ds, wt, st, out)
     else:
         dq, ds = K.quant_fp8_rows(dy, colscale=st)
@@ -455,14 +493,15 @@ class GemmaAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg, f8: Optional[FP8Weights] = None,
-                capture: Optional[dict] = None):
+                capture: Optional[dict] = None, mx_in: Optional[MXSlot] = None):
         x = _c(x)
+        x_mx = mx_in.take(x) if mx_in is not None else None
         M, H = x.shape
         qd, kd = cfg.Hq * cfg.D, cfg.Hkv * cfg.D
         qkv = _empty(M, qd + 2 * kd, like=x)
         rope = (cos, sin, cos.shape[0], cfg.D, qd + kd)
         if _fp8_site(f8, "qkv") is not None:
-            _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, kind=L.EPI_ROPE, rope=rope)
+            _fp8_linear(x, f8, "qkv", (wq, wk, wv), qkv, x_mx=x_mx, kind=L.EPI_ROPE, rope=rope)
         else:
             K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=rope)
         attn = _empty(M, qd, like=x)
@@ -531,7 +570,7 @@ class GemmaAttentionFn(torch.autograd.Function):
                 K.linear_dgrad(dqkv, [wq, wk, wv], dx)
         rets = [d[2] for d in dests]
         side.join(*rets, ret_wo)
-        return (dx, *rets, ret_wo, None, None, None, None, None, None)
+        return (dx, *rets, ret_wo, None, None, None, None, None, None, None)
 
 
 @torch.no_grad()
@@ -668,8 +707,9 @@ class GemmaMLPFn(torch.autograd.Function):
     GEMM with the GeGLU in its epilogue; backward: dH GEMM, then the GeGLU derivative in one elementwise pass."""
 
     @staticmethod
-    def forward(ctx, x, wg, wu, wd, f8: Optional[FP8Weights] = None):
+    def forward(ctx, x, wg, wu, wd, f8: Optional[FP8Weights] = None, mx_in: Optional[MXSlot] = None):
         x = _c(x)
+        x_mx = mx_in.take(x) if mx_in is not None else None
         M = x.shape[0]
         I = wg.shape[0]
         h = _empty(M, I, like=x)
@@ -677,7 +717,7 @@ class GemmaMLPFn(torch.autograd.Function):
         u = _empty(M, I, like=x)
         out = _empty(M, wd.shape[0], like=x)
         if _fp8_site(f8, "gate_up") is not None:
-            _fp8_linear(x, f8, "gate_up", (wg, wu), h, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u)
+            _fp8_linear(x, f8, "gate_up", (wg, wu), h, x_mx=x_mx, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u)
         else:
             K.linear_geglu_fwd(x, wg, wu, h, g, u)
         if _fp8_site(f8, "down") is not None:
@@ -706,7 +746,13 @@ class GemmaMLPFn(torch.autograd.Function):
             _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
-        K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+        f8gu = _fp8_site(f8, "gate_up")
+        dgu_mx = None
+        if f8gu is not None and FP8_SCALING[0] == "mx" and I % 128 == 0 and ctx.needs_input_grad[0]:
+            # the MX copy of [dg | du] for the fp8 dgrad comes out of the same pass (no quantisation pass over dgu)
+            dgu_mx = K.geglu_bwd_mx(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
+        else:
+            K.geglu_bwd(dgu[:, :I], g, u, dgu[:, :I], dgu[:, I:])
         dg_, accg, retg = _grad_dest(wg, ctx.needs_input_grad[1])
         du_, accu, retu = _grad_dest(wu, ctx.needs_input_grad[2])
 
@@ -722,12 +768,12 @@ class GemmaMLPFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            if _fp8_site(f8, "gate_up") is not None:
-                _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx)
+            if f8gu is not None:
+                _fp8_dgrad(dgu, f8, "gate_up", (wg, wu), dx, dy_mx=dgu_mx)
             else:
                 K.linear_dgrad(dgu, [wg, wu], dx)
         side.join(retg, retu, ret_wd)
-        return dx, retg, retu, ret_wd, None
+        return dx, retg, retu, ret_wd, None, None
 
 
 # ------------------------------------------------------------------------------------ SigLIP blocks

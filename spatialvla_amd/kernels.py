@@ -405,6 +405,35 @@ def quant_mx_rows(x: torch.Tensor, q: Optional[torch.Tensor] = None, sc: Optiona
     return q, sc
 
 
+def quant_mx_cols(w: torch.Tensor):
+    """quant_mx_rows(w.t()) without the bf16 transpose (svla_quant_mx_cols): w [N, K] bf16 -> (q [K, N] e4m3 with MX
+    blocks of 32 consecutive n, MXScales of a [K]-row matrix) -- the dgrad operand W^T of the fp8 projections."""
+    _chk_bf16(w, "quant_mx_cols")
+    N, Kd = w.shape
+    _req(N % 128 == 0 and Kd % 64 == 0, f"quant_mx_cols: [{N}, {Kd}] needs N % 128 == 0 and K % 64 == 0")
+    q = torch.empty(Kd, N, dtype=FP8, device=w.device)
+    sc = MXScales(Kd, N, w.device)
+    L.check(L.lib().svla_quant_mx_cols(N, Kd, w.data_ptr(), _ld(w), q.data_ptr(), q.stride(0), sc.buf.data_ptr(),
+                                       sc.ld, _stream()), "svla_quant_mx_cols")
+    return q, sc
+
+
+def quant_mx_both(w: torch.Tensor):
+    """(quant_mx_rows(w), quant_mx_cols(w)) from one read of w (svla_quant_mx_both; R, C multiples of 128):
+    ((q [R, C], MXScales), (qt [C, R], MXScales))."""
+    _chk_bf16(w, "quant_mx_both")
+    R, C = w.shape
+    _req(R % 128 == 0 and C % 128 == 0, f"quant_mx_both: [{R}, {C}] needs multiples of 128")
+    q = torch.empty(R, C, dtype=FP8, device=w.device)
+    sc = MXScales(R, C, w.device)
+    qt = torch.empty(C, R, dtype=FP8, device=w.device)
+    sct = MXScales(C, R, w.device)
+    L.check(L.lib().svla_quant_mx_both(R, C, w.data_ptr(), _ld(w), q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld,
+                                       qt.data_ptr(), qt.stride(0), sct.buf.data_ptr(), sct.ld, _stream()),
+            "svla_quant_mx_both")
+    return (q, sc), (qt, sct)
+
+
 def gemm_mxfp8(xq: torch.Tensor, xs: MXScales, wq: torch.Tensor, ws: MXScales, out: torch.Tensor,
                kind=L.EPI_STORE, geglu_I: int = 0, **epi_kw):
     """out = epi(sum_k 2^(Xa + Xb) xq wq^T) on the MX fp8 MFMA kernel (svla_gemm_mxfp8); wq and ws as gemm_fp8's
@@ -495,6 +524,18 @@ def rmsnorm_fwd(x, w, eps, y, rstd):
                                      _stream()), "rmsnorm_fwd")
 
 
+def rmsnorm_fwd_mx(x, w, eps, y, rstd):
+    """rmsnorm_fwd that also returns the MX e4m3 copy of y (svla_rmsnorm_fwd_mx): (q, MXScales)."""
+    rows, N = x.shape
+    _req(N % 128 == 0 and x.is_contiguous() and y.is_contiguous(), "rmsnorm_fwd_mx: N % 128 == 0, contiguous rows")
+    q = torch.empty(rows, N, dtype=FP8, device=x.device)
+    sc = MXScales(rows, N, x.device)
+    L.check(L.lib().svla_rmsnorm_fwd_mx(rows, N, x.data_ptr(), w.data_ptr(), eps, y.data_ptr(), rstd.data_ptr(),
+                                        q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld, _stream()),
+            "rmsnorm_fwd_mx")
+    return q, sc
+
+
 def add_rmsnorm_fwd(res, yin, w, eps, h, rstd):
     rows, N = yin.shape
     L.check(L.lib().svla_add_rmsnorm_fwd(rows, N, res.data_ptr(), yin.data_ptr(), w.data_ptr(), eps, h.data_ptr(),
@@ -513,6 +554,22 @@ def add_rmsnorm2_fwd_train(res, yin, w1, w2, eps1, eps2, h, x, rstd1, rstd2):
     L.check(L.lib().svla_add_rmsnorm2_fwd_train(rows, N, res.data_ptr(), yin.data_ptr(), w1.data_ptr(), w2.data_ptr(),
                                                 float(eps1), float(eps2), h.data_ptr(), x.data_ptr(),
                                                 rstd1.data_ptr(), rstd2.data_ptr(), _stream()), "add_rmsnorm2_fwd_train")
+
+
+def add_rmsnorm2_fwd_train_mx(res, yin, w1, w2, eps1, eps2, h, x, rstd1, rstd2):
+    """add_rmsnorm2_fwd_train that also returns the MX e4m3 copy of x (svla_add_rmsnorm2_fwd_train_mx)."""
+    rows, N = yin.shape
+    for t, n in ((res, "res"), (yin, "yin"), (w1, "w1"), (w2, "w2"), (h, "h"), (x, "x")):
+        _chk_bf16(t, n)
+    _req(res.shape == yin.shape == h.shape == x.shape and res.is_contiguous() and yin.is_contiguous()
+         and h.is_contiguous() and x.is_contiguous() and N % 128 == 0, "add_rmsnorm2_train_mx: shapes")
+    q = torch.empty(rows, N, dtype=FP8, device=x.device)
+    sc = MXScales(rows, N, x.device)
+    L.check(L.lib().svla_add_rmsnorm2_fwd_train_mx(rows, N, res.data_ptr(), yin.data_ptr(), w1.data_ptr(),
+                                                   w2.data_ptr(), float(eps1), float(eps2), h.data_ptr(), x.data_ptr(),
+                                                   rstd1.data_ptr(), rstd2.data_ptr(), q.data_ptr(), q.stride(0),
+                                                   sc.buf.data_ptr(), sc.ld, _stream()), "add_rmsnorm2_fwd_train_mx")
+    return q, sc
 
 
 RPB = 16  # rows per block of the norm backward kernels (norms.hip RPB): sizes the weight-gradient partial planes
@@ -1008,6 +1065,21 @@ def geglu_bwd(dh: torch.Tensor, g: torch.Tensor, u: torch.Tensor, dg: torch.Tens
     L.check(L.lib().svla_geglu_bwd(M, I, dh.data_ptr(), dh.stride(0), g.data_ptr(), g.stride(0), u.data_ptr(),
                                    u.stride(0), dg.data_ptr(), dg.stride(0), du.data_ptr(), du.stride(0), _stream()),
             "geglu_bwd")
+
+
+def geglu_bwd_mx(dh: torch.Tensor, g: torch.Tensor, u: torch.Tensor, dg: torch.Tensor, du: torch.Tensor):
+    """geglu_bwd that also returns the MX e4m3 copy of [dg | du] (svla_geglu_bwd_mx): (q [M, 2I], MXScales),
+    bitwise quant_mx_rows of the bf16 [dg | du] -- the fp8 gate|up dgrad operand without a separate pass."""
+    M, I = g.shape
+    for t in (dh, g, u, dg, du):
+        _req(t.shape == (M, I) and t.dtype == torch.bfloat16 and t.stride(1) == 1, "geglu_bwd_mx: [M, I] bf16 rows")
+    _req(I % 128 == 0, "geglu_bwd_mx: I must be a multiple of 128")
+    q = torch.empty(M, 2 * I, dtype=FP8, device=g.device)
+    sc = MXScales(M, 2 * I, g.device)
+    L.check(L.lib().svla_geglu_bwd_mx(M, I, dh.data_ptr(), dh.stride(0), g.data_ptr(), g.stride(0), u.data_ptr(),
+                                      u.stride(0), dg.data_ptr(), dg.stride(0), du.data_ptr(), du.stride(0),
+                                      q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld, _stream()), "geglu_bwd_mx")
+    return q, sc
 
 
 # ---------------------------------------------------------------------------------------- NHWC convolution

@@ -88,9 +88,9 @@ class Gemma2RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.zeros(dim))
 
-    def forward(self, x, slot=None):
+    def forward(self, x, slot=None, mx=None):
         shp = x.shape
-        return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps, slot).view(shp)
+        return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps, slot, mx).view(shp)
 
     def add_forward(self, residual, y, slot=None):
         """residual + self(y) (decoder-layer residual branches)."""
@@ -115,10 +115,10 @@ class Gemma2MLP(nn.Module):
         if act not in ("gelu_pytorch_tanh", "gelu_tanh"):
             raise ValueError(f"Gemma2MLP: activation {act!r} not supported (kernel implements gelu_pytorch_tanh)")
 
-    def forward(self, x):
+    def forward(self, x, mx_in=None):
         shp = x.shape
         out = Fn.GemmaMLPFn.apply(x.reshape(-1, shp[-1]), self.gate_proj.weight, self.up_proj.weight,
-                                  self.down_proj.weight, getattr(self, "_svla_fp8", None))
+                                  self.down_proj.weight, getattr(self, "_svla_fp8", None), mx_in)
         return out.view(*shp[:-1], self.hidden_size)
 
 
@@ -192,7 +192,7 @@ class Gemma2Attention(nn.Module):
                                float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
 
     def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None,
-                attn_sink: Optional[list] = None):
+                attn_sink: Optional[list] = None, mx_in=None):
         B, Lq, H = hidden_states.shape
         cfg = self.attn_cfg(B, Lq)
         cos, sin = rope
@@ -213,7 +213,7 @@ class Gemma2Attention(nn.Module):
         capture = {} if attn_sink is not None else None
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
-                                        cfg, getattr(self, "_svla_fp8", None), capture)
+                                        cfg, getattr(self, "_svla_fp8", None), capture, mx_in)
         if attn_sink is not None:
             attn_sink.append(Fn.gemma_attention_weights(capture["qkv"], attention_mask.kv_class, cfg))
         return out.view(B, Lq, H)
@@ -260,20 +260,23 @@ class Gemma2DecoderLayer(nn.Module):
         # each residual-stream tensor has two consumers (pre-norm, residual add): a ResidualSlot sums their
         # gradients inside the pre-norm's backward kernel instead of an autograd add
         s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
-        x = self.input_layernorm(hidden_states, s1)
-        a = self.self_attn(x, attention_mask, rope, cache, attn_sink)
+        # fp8 projections (configs[4]): the norms also emit the MX e4m3 copies of q|k|v's and gate|up's inputs
+        f8 = getattr(self.self_attn, "_svla_fp8", None) if cache is None else None
+        mx_a, mx_m = Fn.mx_slot_for(f8, "qkv"), Fn.mx_slot_for(f8, "gate_up")
+        x = self.input_layernorm(hidden_states, s1, mx_a)
+        a = self.self_attn(x, attention_mask, rope, cache, attn_sink, mx_a)
         pa, pf = self.post_attention_layernorm, self.pre_feedforward_layernorm
         if FUSED_NORM_PAIR[0]:
             # post-attention norm + residual and the pre-feedforward norm in one launch (AddRMSNorm2Fn); h's
             # residual-branch gradient arrives through s2 (post_feedforward's add parks it there)
             shp = a.shape
             h, x = Fn.AddRMSNorm2Fn.apply(hidden_states.reshape(-1, shp[-1]), a.reshape(-1, shp[-1]), pa.weight,
-                                          pf.weight, pa.eps, pf.eps, s1, s2)
+                                          pf.weight, pa.eps, pf.eps, s1, s2, mx_m)
             h, x = h.view(shp), x.view(shp)
         else:
             h = pa.add_forward(hidden_states, a, s1)
-            x = pf(h, s2)
-        m = self.mlp(x)
+            x = pf(h, s2, mx_m)
+        m = self.mlp(x, mx_m)
         return self.post_feedforward_layernorm.add_forward(h, m, s2)
 
 

@@ -11,6 +11,8 @@ Tolerances (stated here):
     on the residual update, dx and every weight gradient -- the single-GEMM error compounded over the chain
     (measured 8.7e-2 / 7.6e-2 / 9.8e-2).
 """
+import os
+
 import pytest
 import torch
 
@@ -224,6 +226,95 @@ def test_quant_mx_rows_bitexact(cuda, rows, k):
     qr, Xr = ref_quant_mx(x)
     assert torch.equal(sc.exponents().cpu(), Xr)
     assert torch.equal(q.view(torch.uint8).cpu(), qr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("n,k", [(4096, 2304), (2304, 2048), (18432, 2304), (2304, 9216), (128, 64), (384, 192)])
+def test_quant_mx_cols_equals_rows_of_transpose(cuda, n, k):
+    """svla_quant_mx_cols(W) (the dgrad operand W^T, no bf16 transpose) is bit for bit svla_quant_mx_rows(W^T): the
+    e4m3 bytes and the E8M0 scales, including zero, subnormal, NaN and Inf blocks."""
+    g = torch.Generator(device=cuda).manual_seed(n + k)
+    w = _mx_data(n, k, g, cuda)
+    w[5, 7] = float("nan")
+    w[64 + 3, k - 1] = float("inf")
+    q, sc = K.quant_mx_cols(w)
+    qr, scr = K.quant_mx_rows(w.t().contiguous())
+    assert torch.equal(sc.exponents(), scr.exponents())
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("r,c", [(4096, 2304), (2304, 2048), (18432, 2304), (2304, 9216), (128, 128), (9984, 4096)])
+def test_quant_mx_both_equals_rows_and_cols(cuda, r, c):
+    """svla_quant_mx_both (the fp8 weight copies from one read) is bit for bit quant_mx_rows(W) and quant_mx_cols(W)."""
+    g = torch.Generator(device=cuda).manual_seed(r * 3 + c)
+    w = _mx_data(r, c, g, cuda)
+    w[1, 2] = float("nan")
+    w[100, 127] = float("-inf")
+    (q, sc), (qt, sct) = K.quant_mx_both(w)
+    q0, sc0 = K.quant_mx_rows(w)
+    qt0, sct0 = K.quant_mx_cols(w)
+    assert torch.equal(sc.exponents(), sc0.exponents()) and torch.equal(q.view(torch.uint8), q0.view(torch.uint8))
+    assert torch.equal(sct.exponents(), sct0.exponents()) and torch.equal(qt.view(torch.uint8), qt0.view(torch.uint8))
+
+
+@pytest.mark.parametrize("items", ["1", "4", "8"])
+def test_quant_mx_rows_items_per_wave_bitwise(cuda, items):
+    """The items-per-wave variants of svla_quant_mx_rows (SVLA_QUANT_MX_ITEMS, read once per process: run in a child)
+    give the bytes of the CPU restatement on a ragged shape (K = 2304: a half 512-k chunk per row)."""
+    import subprocess
+    import sys
+    code = ("import torch, sys; sys.path.insert(0, %r); sys.path.insert(0, %r); import test_fp8_gpu as T; "
+            "from spatialvla_amd import kernels as K; g = torch.Generator(device='cuda').manual_seed(3); "
+            "x = T._mx_data(1001, 2304, g, 'cuda'); q, sc = K.quant_mx_rows(x); qr, Xr = T.ref_quant_mx(x); "
+            "assert torch.equal(sc.exponents().cpu(), Xr); "
+            "assert torch.equal(q.view(torch.uint8).cpu(), qr.view(torch.uint8)); print('ok')"
+            % (os.path.dirname(os.path.abspath(__file__)), os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SVLA_QUANT_MX_ITEMS=items),
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-3000:]
+
+
+def test_geglu_bwd_mx_equals_pass_then_quant(cuda):
+    """svla_geglu_bwd_mx: the bf16 dg / du of svla_geglu_bwd bit for bit, and the MX copy of [dg | du] bit for bit
+    quant_mx_rows of them (the fused producer of the fp8 gate|up dgrad operand)."""
+    torch.manual_seed(41)
+    M, I = 777, 1280
+    dh = torch.randn(M, I, device=cuda).to(BF)
+    g = (torch.randn(M, I, device=cuda) * 2).to(BF)
+    u = torch.randn(M, I, device=cuda).to(BF)
+    dh[3, 5] = float("nan")
+    ref = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+    K.geglu_bwd(dh, g, u, ref[:, :I], ref[:, I:])
+    got = torch.empty(M, 2 * I, dtype=BF, device=cuda)
+    q, sc = K.geglu_bwd_mx(dh.clone(), g, u, got[:, :I], got[:, I:])
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    qr, scr = K.quant_mx_rows(ref)
+    assert torch.equal(sc.exponents(), scr.exponents())
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8))
+
+
+def test_norms_emit_mx_copy_bitwise(cuda):
+    """svla_rmsnorm_fwd_mx / svla_add_rmsnorm2_fwd_train_mx: the bf16 outputs and rstd of the plain kernels bit for bit,
+    and the MX copy of the normalised output bit for bit quant_mx_rows of it (the fp8 q|k|v / gate|up operands)."""
+    torch.manual_seed(43)
+    M, N = 1000, 2304
+    res = torch.randn(M, N, device=cuda).to(BF)
+    y = (torch.randn(M, N, device=cuda) * 3).to(BF)
+    w1 = (torch.randn(N, device=cuda) * 0.3).to(BF)
+    w2 = (torch.randn(N, device=cuda) * 0.3).to(BF)
+    out0, out1 = torch.empty_like(y), torch.empty_like(y)
+    r0, r1 = (torch.empty(M, dtype=torch.float32, device=cuda) for _ in range(2))
+    K.rmsnorm_fwd(y, w1, 1e-6, out0, r0)
+    q, sc = K.rmsnorm_fwd_mx(y, w1, 1e-6, out1, r1)
+    assert torch.equal(out0, out1) and torch.equal(r0, r1)
+    qr, scr = K.quant_mx_rows(out0)
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8)) and torch.equal(sc.exponents(), scr.exponents())
+    h0, x0, h1, x1 = (torch.empty_like(y) for _ in range(4))
+    a0, b0, a1, b1 = (torch.empty(M, dtype=torch.float32, device=cuda) for _ in range(4))
+    K.add_rmsnorm2_fwd_train(res, y, w1, w2, 1e-6, 1e-6, h0, x0, a0, b0)
+    q, sc = K.add_rmsnorm2_fwd_train_mx(res, y, w1, w2, 1e-6, 1e-6, h1, x1, a1, b1)
+    assert torch.equal(h0, h1) and torch.equal(x0, x1) and torch.equal(a0, a1) and torch.equal(b0, b1)
+    qr, scr = K.quant_mx_rows(x0)
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8)) and torch.equal(sc.exponents(), scr.exponents())
 
 
 def test_quant_mx_rows_nonfinite_blocks_are_nan(cuda):
