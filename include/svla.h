@@ -94,6 +94,12 @@ typedef struct {
   int32_t rope_L;            /* sequence length: row m is position m % rope_L */
   int32_t rope_D;            /* head dim; the GEMM tile width must be a multiple of it */
   const void* colscale;      /* [N] bf16 (BIAS_SCALE_RESID) */
+  void* mx_q;                /* GEGLU on the fp8 GEMMs (svla_gemm_mxfp8 / svla_gemm_fp8) only, else NULL: also the
+                                OCP MX e4m3 copy of C (h) -- [M][mx_ldq] bytes, E8M0 scales in svla_quant_mx_rows'
+                                layout (mx_sld >= 4 M), bitwise svla_quant_mx_rows of the stored bf16 h; N/2 % 128 == 0 */
+  int64_t mx_ldq;
+  void* mx_scales;
+  int64_t mx_sld;
 } svla_epilogue;
 
 /* C: up to 4 row segments (c_seg_start tile-aligned to 128) — lets dW of q/k/v (or gate/up)
@@ -283,6 +289,17 @@ int svla_add_rmsnorm_fwd(int64_t rows, int64_t N, const void* res, const void* y
 int svla_rmsnorm2_bwd(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2, const void* dx,
                       const void* dres, const void* y, const void* w1, const float* rstd1, void* dh_out, void* dy_out,
                       float* dw_partial, int64_t* n_partial, void* stream);
+/* svla_rmsnorm_bwd / svla_rmsnorm2_bwd that also write the OCP MX e4m3 copy of the input gradient they store (dx,
+ * resp. dy) -- q [rows][ldq] bytes, E8M0 scales in svla_quant_mx_rows' layout (sld >= 4 rows), bitwise
+ * svla_quant_mx_rows of it: the fp8 dgrad operands of the down and o projections, without a separate pass.
+ * N % 128 == 0 (svla_rmsnorm_bwd_mx: N > 1536, the block-per-row kernel). */
+int svla_rmsnorm_bwd_mx(int64_t rows, int64_t N, const void* x, const void* w, const float* rstd, const void* dy,
+                        const void* dres, void* dx, float* dw_partial, int64_t* n_partial, void* q, int64_t ldq,
+                        void* scales, int64_t sld, void* stream);
+int svla_rmsnorm2_bwd_mx(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2, const void* dx,
+                         const void* dres, const void* y, const void* w1, const float* rstd1, void* dh_out,
+                         void* dy_out, float* dw_partial, int64_t* n_partial, void* q, int64_t ldq, void* scales,
+                         int64_t sld, void* stream);
 /* h = res + rmsnorm(yin; w1), x = rmsnorm(h; w2) in one pass (inference; bitwise the two separate calls):
  * Gemma2 post-attention + pre-feedforward norms, or post-feedforward + next input norm (modeling_gemma2.py:487-496). */
 int svla_add_rmsnorm2_fwd(int64_t rows, int64_t N, const void* res, const void* yin, const void* w1, const void* w2,

@@ -36,7 +36,8 @@ class Epilogue(ctypes.Structure):
                 ("in0", c_vp), ("ld_in0", c_i64), ("in1", c_vp), ("ld_in1", c_i64), ("out1", c_vp),
                 ("ld_out1", c_i64), ("out2", c_vp), ("ld_out2", c_i64), ("row_stats", c_vp),
                 ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_ld", c_i64), ("rope_cols", c_i64), ("rope_L", c_i32),
-                ("rope_D", c_i32), ("colscale", c_vp)]
+                ("rope_D", c_i32), ("colscale", c_vp), ("mx_q", c_vp), ("mx_ldq", c_i64), ("mx_scales", c_vp),
+                ("mx_sld", c_i64)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -113,6 +114,10 @@ SIGNATURES = {
                                    ctypes.POINTER(c_i64), c_vp]),
     "svla_colsum_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "svla_rmsnorm2_bwd": (c_i32, [c_i64, c_i64] + [c_vp] * 11 + [ctypes.POINTER(c_i64), c_vp]),
+    "svla_rmsnorm2_bwd_mx": (c_i32, [c_i64, c_i64] + [c_vp] * 11 + [ctypes.POINTER(c_i64), c_vp, c_i64, c_vp, c_i64,
+                                                                    c_vp]),
+    "svla_rmsnorm_bwd_mx": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64),
+                                    c_vp, c_i64, c_vp, c_i64, c_vp]),
     "svla_colsum2_f32": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "svla_colsum_bf16": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "svla_colsum_bf16_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),

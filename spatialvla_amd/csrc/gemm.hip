@@ -349,6 +349,14 @@ __device__ __forceinline__ void epi_pass_fast(const float* Ei, int64_t M, int64_
         store8(cbase + (m - cm0) * ldc + n, h, I - n);
         store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g[it0], I - n);
         store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u[it0], I - n);
+        if constexpr (HC == 16) {  // the MX copy of h (fp8 down operand): 16 threads = one row's 128-column k-tile
+          if (E.mx_q != nullptr) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = round_bf(h[j]);
+            mx_store8(h, true, (uint8_t*)E.mx_q + m * E.mx_ldq + n,
+                      (uint8_t*)E.mx_scales + (n / 128) * E.mx_sld + m * 4);
+          }
+        }
       }
     }
     }
@@ -596,6 +604,14 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
           store8(cbase + (m - cm0) * Cd.ld + n, h, I - n);
           store8((bf16_t*)E.out1 + m * E.ld_out1 + n, g, I - n);
           store8((bf16_t*)E.out2 + m * E.ld_out2 + n, u, I - n);
+          if constexpr (HC == 16) {  // the MX copy of h, as epi_pass_fast<GEGLU>
+            if (E.mx_q != nullptr) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) h[j] = round_bf(h[j]);
+              mx_store8(h, true, (uint8_t*)E.mx_q + m * E.mx_ldq + n,
+                        (uint8_t*)E.mx_scales + (n / 128) * E.mx_sld + m * 4);
+            }
+          }
         }
       }
     } else {
@@ -3286,6 +3302,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* stream) {
   SVLA_CHECK_ARG(variant >= 0 && variant <= 9, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
+  SVLA_CHECK_ARG(!epi || !epi->mx_q, "gemm: the MX copy of C (epi->mx_q) is an fp8-GEMM output only");
   GemmCtx ctx;
   ctx.ws = workspace;
   ctx.ws_bytes = workspace ? ws_bytes : 0;
@@ -3299,6 +3316,7 @@ extern "C" int svla_gemv_rmsnorm2(int64_t M, int64_t N, int64_t K, const void* r
   SVLA_CHECK_ARG(M >= 1 && M <= GEMV_MAXM && N > 0 && K > 0 && K % 8 == 0 && K <= 2560 && K <= 256 * 8 * GN_MAXC,
                  "gemv_rmsnorm2: M in [1, %d], K a multiple of 8 <= 2560", GEMV_MAXM);
   SVLA_CHECK_ARG(res && y && w1 && w2 && h_out && B && c && epi, "gemv_rmsnorm2: NULL argument");
+  SVLA_CHECK_ARG(!epi->mx_q, "gemv_rmsnorm2: the MX copy of C (epi->mx_q) is an fp8-GEMM output only");
   SVLA_CHECK_ARG(ldx % 8 == 0 && ldx >= K && ldc % 8 == 0, "gemv_rmsnorm2: ldx >= K and ldc multiples of 8");
   SVLA_CHECK_ARG(B->layout == SVLA_LAYOUT_KC && B->ld % 8 == 0, "gemv_rmsnorm2: B must be KC with ld % 8 == 0");
   const bool geglu = epi->kind == SVLA_EPI_GEGLU;
@@ -3520,6 +3538,7 @@ int gemm_fp8_common(int64_t M, int64_t N, int64_t K, const svla_operand* A, cons
                        : B->nseg == 1,
                  "gemm_fp8: B is one segment, or two GEGLU segments of N/2 rows (multiple of 128) with EPI_GEGLU");
   SVLA_CHECK_ARG(!epi->accumulate, "gemm_fp8: accumulate unsupported");
+  SVLA_CHECK_ARG(!epi->mx_q || epi->kind == SVLA_EPI_GEGLU, "gemm_fp8: the MX copy of C is a GEGLU output");
   switch (epi->kind) {
     case SVLA_EPI_STORE: break;
     case SVLA_EPI_BIAS: SVLA_CHECK_ARG(epi->bias && aligned16(epi->bias), "gemm_fp8: bias"); break;
@@ -3527,6 +3546,11 @@ int gemm_fp8_common(int64_t M, int64_t N, int64_t K, const svla_operand* A, cons
     case SVLA_EPI_GEGLU:
       SVLA_CHECK_ARG(epi->out1 && epi->out2 && epi->ld_out1 % 8 == 0 && epi->ld_out2 % 8 == 0,
                      "gemm_fp8: GEGLU needs out1,out2");
+      SVLA_CHECK_ARG(!epi->mx_q || (epi->mx_scales && (N / 2) % 128 == 0 && epi->mx_ldq >= N / 2 &&
+                                    epi->mx_ldq % 8 == 0 && ((uintptr_t)epi->mx_q & 7) == 0 &&
+                                    ((uintptr_t)epi->mx_scales & 3) == 0 && epi->mx_sld >= 4 * M &&
+                                    epi->mx_sld % 4 == 0),
+                     "gemm_fp8: GEGLU MX copy of h: N/2 % 128 == 0, mx_ldq >= N/2 (8-B rows), mx_sld >= 4 M");
       break;
     case SVLA_EPI_ROPE:
       SVLA_CHECK_ARG(epi->rope_cos && epi->rope_sin && epi->rope_L > 0 && epi->rope_D >= 16 && epi->rope_D % 16 == 0 &&

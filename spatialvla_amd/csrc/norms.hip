@@ -152,7 +152,9 @@ template <int MC>
 __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ w, const float* __restrict__ rstd,
                                                       const bf16_t* __restrict__ dy, const bf16_t* __restrict__ dres,
-                                                      bf16_t* __restrict__ dx, float* __restrict__ dw_partial) {
+                                                      bf16_t* __restrict__ dx, float* __restrict__ dw_partial,
+                                                      uint8_t* __restrict__ q = nullptr, int64_t ldq = 0,
+                                                      uint8_t* __restrict__ sc = nullptr, int64_t sld = 0) {
   __shared__ float red[16];
   const int nch = (int)(N >> 3);
   float wf[MC][8], dwacc[MC][8];
@@ -225,6 +227,11 @@ __global__ __launch_bounds__(NTH) void rms_bwd_kernel(int64_t rows, int64_t N, c
           for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]) + r[j];
         }
         st8(dx + row * N + ch * 8, o);
+        if (q != nullptr) {  // the MX copy of dx (an fp8 dgrad operand; N % 128 == 0: whole k-tiles per 16 lanes)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]);
+          mx_store8(o, true, q + row * ldq + ch * 8, sc + (ch / 16) * sld + row * 4);
+        }
       }
     }
   }
@@ -254,7 +261,9 @@ __global__ __launch_bounds__(NTH) void rms_bwd2_kernel(int64_t rows, int64_t N, 
                                                        const bf16_t* __restrict__ dx, const bf16_t* __restrict__ dres,
                                                        const bf16_t* __restrict__ y, const bf16_t* __restrict__ w1,
                                                        const float* __restrict__ rstd1, bf16_t* __restrict__ dh_out,
-                                                       bf16_t* __restrict__ dy_out, float* __restrict__ partial) {
+                                                       bf16_t* __restrict__ dy_out, float* __restrict__ partial,
+                                                       uint8_t* __restrict__ q = nullptr, int64_t ldq = 0,
+                                                       uint8_t* __restrict__ sc = nullptr, int64_t sld = 0) {
   __shared__ float red[16];
   const int nch = (int)(N >> 3);
   float wf2[MC][8], wf1[MC][8], acc2[MC][8], acc1[MC][8];
@@ -365,6 +374,11 @@ __global__ __launch_bounds__(NTH) void rms_bwd2_kernel(int64_t rows, int64_t N, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rs1 * (gv[c][j] - xv[c][j] * dot1);
         st8(dy_out + row * N + ch * 8, o);
+        if (q != nullptr) {  // the MX copy of dy (the fp8 o-projection dgrad operand)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = round_bf(o[j]);
+          mx_store8(o, true, q + row * ldq + ch * 8, sc + (ch / 16) * sld + row * 4);
+        }
       }
     }
   }
@@ -976,4 +990,51 @@ extern "C" int svla_add_rmsnorm2_fwd_train_mx(int64_t rows, int64_t N, const voi
                      (const bf16_t*)yin, (const bf16_t*)res, (const bf16_t*)w1, (const bf16_t*)w2, eps1, eps2,
                      (bf16_t*)h, (bf16_t*)x, rstd1, rstd2, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
   return svla::check_launch("add_rmsnorm2_fwd_train_mx");
+}
+
+extern "C" int svla_rmsnorm_bwd_mx(int64_t rows, int64_t N, const void* x, const void* w, const float* rstd,
+                                   const void* dy, const void* dres, void* dx, float* dw_partial, int64_t* n_partial,
+                                   void* q, int64_t ldq, void* scales, int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 1536 && N % 128 == 0 && N <= NTH * MAXC * 8,
+                 "rmsnorm_bwd_mx: N=%lld (a multiple of 128 in (1536, %d])", (long long)N, NTH * MAXC * 8);
+  SVLA_CHECK_ARG(x && w && rstd && dy && dx && dw_partial && q && scales && ldq >= N && ldq % 8 == 0 &&
+                     ((uintptr_t)q & 7) == 0 && ((uintptr_t)scales & 3) == 0 && sld >= 4 * rows && sld % 4 == 0,
+                 "rmsnorm_bwd_mx: null pointer or bad q / scale strides");
+  const int64_t nb = (rows + RPB - 1) / RPB;
+  if (n_partial) *n_partial = nb;
+  if (N <= NTH * 8 * 2)
+    hipLaunchKernelGGL(rms_bwd_kernel<2>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                       dw_partial, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  else
+    hipLaunchKernelGGL(rms_bwd_kernel<MAXC>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)x, (const bf16_t*)w, rstd, (const bf16_t*)dy, (const bf16_t*)dres, (bf16_t*)dx,
+                       dw_partial, (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("rmsnorm_bwd_mx");
+}
+
+extern "C" int svla_rmsnorm2_bwd_mx(int64_t rows, int64_t N, const void* h, const void* w2, const float* rstd2,
+                                    const void* dx, const void* dres, const void* y, const void* w1, const float* rstd1,
+                                    void* dh_out, void* dy_out, float* dw_partial, int64_t* n_partial, void* q,
+                                    int64_t ldq, void* scales, int64_t sld, void* stream) {
+  SVLA_CHECK_ARG(rows > 0 && N > 0 && N % 128 == 0 && N <= NTH * 8 * 4, "rmsnorm2_bwd_mx: bad N (a multiple of 128)");
+  SVLA_CHECK_ARG(h && w2 && rstd2 && dx && y && w1 && rstd1 && dh_out && dy_out && dw_partial && q && scales,
+                 "rmsnorm2_bwd_mx: null pointer");
+  SVLA_CHECK_ARG(al16(h) && al16(w2) && al16(dx) && (!dres || al16(dres)) && al16(y) && al16(w1) && al16(dh_out) &&
+                     al16(dy_out) && al16(dw_partial) && ldq >= N && ldq % 8 == 0 && ((uintptr_t)q & 7) == 0 &&
+                     ((uintptr_t)scales & 3) == 0 && sld >= 4 * rows && sld % 4 == 0,
+                 "rmsnorm2_bwd_mx: misaligned pointer or bad q / scale strides");
+  const int64_t nb = (rows + RPB2 - 1) / RPB2;
+  if (n_partial) *n_partial = nb;
+  if (N <= NTH * 8 * 2)
+    hipLaunchKernelGGL(rms_bwd2_kernel<2>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)h, (const bf16_t*)w2, rstd2, (const bf16_t*)dx, (const bf16_t*)dres,
+                       (const bf16_t*)y, (const bf16_t*)w1, rstd1, (bf16_t*)dh_out, (bf16_t*)dy_out, dw_partial,
+                       (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  else
+    hipLaunchKernelGGL(rms_bwd2_kernel<4>, dim3((unsigned)nb), dim3(NTH), 0, (hipStream_t)stream, rows, N,
+                       (const bf16_t*)h, (const bf16_t*)w2, rstd2, (const bf16_t*)dx, (const bf16_t*)dres,
+                       (const bf16_t*)y, (const bf16_t*)w1, rstd1, (bf16_t*)dh_out, (bf16_t*)dy_out, dw_partial,
+                       (uint8_t*)q, ldq, (uint8_t*)scales, sld);
+  return svla::check_launch("rmsnorm2_bwd_mx");
 }

@@ -185,13 +185,14 @@ class AddRMSNormFn(torch.autograd.Function):
     """h = res + Gemma2RMSNorm(y)  (decoder-layer sandwich norm + residual, modeling_gemma2.py:489-496)."""
 
     @staticmethod
-    def forward(ctx, res, y, w, eps, slot=None):
+    def forward(ctx, res, y, w, eps, slot=None, mx_grad=None):
         res, y = _c(res), _c(y)
         h = torch.empty_like(y)
         rstd = _empty(y.shape[0], dtype=F32, like=y)
         K.add_rmsnorm_fwd(res, y, w, eps, h, rstd)
         ctx.save_for_backward(y, w, rstd)
         ctx.slot = slot
+        ctx.mx_grad = mx_grad
         return h
 
     @staticmethod
@@ -200,11 +201,15 @@ class AddRMSNormFn(torch.autograd.Function):
         dh = _c(dh)
         dy = torch.empty_like(y)
         dw, acc, ret = _grad_dest(w, ctx.needs_input_grad[2])
-        K.rmsnorm_bwd(y, w, rstd, dh, None, dy, dw, dw_accumulate=acc)
+        N = y.shape[1]
+        mx = ctx.mx_grad is not None and N % 128 == 0 and N > 1536
+        dy_mx = K.rmsnorm_bwd(y, w, rstd, dh, None, dy, dw, dw_accumulate=acc, mx=mx)
+        if dy_mx is not None:  # the MX copy of dy for the fp8 dgrad of the projection that produced y
+            ctx.mx_grad.put(dy, dy_mx)
         if ctx.slot is not None:  # the pre-norm reading `res` adds dh in its backward kernel
             ctx.slot.put(dh)
-            return None, dy, ret, None, None
-        return dh, dy, ret, None, None
+            return None, dy, ret, None, None, None
+        return dh, dy, ret, None, None, None
 
 
 class AddRMSNorm2Fn(torch.autograd.Function):
@@ -215,7 +220,7 @@ class AddRMSNorm2Fn(torch.autograd.Function):
     dh_total is the gradient of res (parked in slot_res for the pre-norm that also reads res, as AddRMSNormFn does)."""
 
     @staticmethod
-    def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None, mx=None):
+    def forward(ctx, res, y, w1, w2, eps1, eps2, slot_res=None, slot_h=None, mx=None, mx_grad=None):
         res, y = _c(res), _c(y)
         h, x = torch.empty_like(y), torch.empty_like(y)
         r1 = _empty(y.shape[0], dtype=F32, like=y)
@@ -226,6 +231,7 @@ class AddRMSNorm2Fn(torch.autograd.Function):
             K.add_rmsnorm2_fwd_train(res, y, w1, w2, eps1, eps2, h, x, r1, r2)
         ctx.save_for_backward(y, h, w1, w2, r1, r2)
         ctx.slots = (slot_res, slot_h)
+        ctx.mx_grad = mx_grad
         ctx.set_materialize_grads(False)  # h's residual gradient usually arrives through slot_h: no zero tensor
         return h, x
 
@@ -244,11 +250,15 @@ class AddRMSNorm2Fn(torch.autograd.Function):
         if dx is None:
             dx = torch.zeros_like(h)
         # both norms' backward in one pass (bitwise the two svla_rmsnorm_bwd calls)
-        K.rmsnorm2_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), y, w1, r1, dht, dy, dw2, dw1, acc2, acc1)
+        mx = ctx.mx_grad is not None and y.shape[1] % 128 == 0
+        dy_mx = K.rmsnorm2_bwd(h, w2, r2, _c(dx), None if dh is None else _c(dh), y, w1, r1, dht, dy, dw2, dw1, acc2,
+                               acc1, mx=mx)
+        if dy_mx is not None:  # the MX copy of dy (the attention output's gradient) for the fp8 o dgrad
+            ctx.mx_grad.put(dy, dy_mx)
         if slot_res is not None:
             slot_res.put(dht)
-            return None, dy, ret1, ret2, None, None, None, None, None
-        return dht, dy, ret1, ret2, None, None, None, None, None
+            return None, dy, ret1, ret2, None, None, None, None, None, None
+        return dht, dy, ret1, ret2, None, None, None, None, None, None
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -493,7 +503,7 @@ class GemmaAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wq, wk, wv, wo, cos, sin, kv_class, cfg: GemmaAttnCfg, f8: Optional[FP8Weights] = None,
-                capture: Optional[dict] = None, mx_in: Optional[MXSlot] = None):
+                capture: Optional[dict] = None, mx_in: Optional[MXSlot] = None, mx_dout: Optional[MXSlot] = None):
         x = _c(x)
         x_mx = mx_in.take(x) if mx_in is not None else None
         M, H = x.shape
@@ -519,6 +529,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         ctx.save_for_backward(x, wq, wk, wv, wo, qkv, attn, lse, cos, sin, kv_class)
         ctx.cfg = cfg
         ctx.f8 = f8
+        ctx.mx_dout = mx_dout
         return out
 
     @staticmethod
@@ -539,7 +550,7 @@ class GemmaAttentionFn(torch.autograd.Function):
         if dwo is not None:
             side.run(lambda: K.linear_wgrad(dout, attn, [dwo], accumulate=acc), dout, attn)
         if _fp8_site(f8, "o") is not None:
-            _fp8_dgrad(dout, f8, "o", (wo,), dattn)
+            _fp8_dgrad(dout, f8, "o", (wo,), dattn, dy_mx=ctx.mx_dout.take(dout) if ctx.mx_dout is not None else None)
         else:
             K.linear_dgrad(dout, [wo], dattn)
         dqkv = torch.empty_like(qkv)
@@ -570,7 +581,7 @@ class GemmaAttentionFn(torch.autograd.Function):
                 K.linear_dgrad(dqkv, [wq, wk, wv], dx)
         rets = [d[2] for d in dests]
         side.join(*rets, ret_wo)
-        return (dx, *rets, ret_wo, None, None, None, None, None, None, None)
+        return (dx, *rets, ret_wo, None, None, None, None, None, None, None, None)
 
 
 @torch.no_grad()
@@ -707,7 +718,8 @@ class GemmaMLPFn(torch.autograd.Function):
     GEMM with the GeGLU in its epilogue; backward: dH GEMM, then the GeGLU derivative in one elementwise pass."""
 
     @staticmethod
-    def forward(ctx, x, wg, wu, wd, f8: Optional[FP8Weights] = None, mx_in: Optional[MXSlot] = None):
+    def forward(ctx, x, wg, wu, wd, f8: Optional[FP8Weights] = None, mx_in: Optional[MXSlot] = None,
+                mx_dout: Optional[MXSlot] = None):
         x = _c(x)
         x_mx = mx_in.take(x) if mx_in is not None else None
         M = x.shape[0]
@@ -716,16 +728,23 @@ class GemmaMLPFn(torch.autograd.Function):
         g = _empty(M, I, like=x)
         u = _empty(M, I, like=x)
         out = _empty(M, wd.shape[0], like=x)
+        h_mx = None
         if _fp8_site(f8, "gate_up") is not None:
-            _fp8_linear(x, f8, "gate_up", (wg, wu), h, x_mx=x_mx, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u)
+            kw = {}
+            if _fp8_site(f8, "down") is not None and FP8_SCALING[0] == "mx" and I % 128 == 0:
+                # the GeGLU epilogue also writes the MX copy of h, the fp8 down operand (no quantisation pass)
+                h_mx = (torch.empty(M, I, dtype=torch.float8_e4m3fn, device=x.device), K.MXScales(M, I, x.device))
+                kw["mx_out"] = h_mx
+            _fp8_linear(x, f8, "gate_up", (wg, wu), h, x_mx=x_mx, kind=L.EPI_GEGLU, geglu_I=I, out1=g, out2=u, **kw)
         else:
             K.linear_geglu_fwd(x, wg, wu, h, g, u)
         if _fp8_site(f8, "down") is not None:
-            _fp8_linear(h, f8, "down", (wd,), out)
+            _fp8_linear(h, f8, "down", (wd,), out, x_mx=h_mx)
         else:
             K.linear_fwd(h, [wd], out)
         ctx.save_for_backward(x, wg, wu, wd, g, u, h)
         ctx.f8 = f8
+        ctx.mx_dout = mx_dout
         return out
 
     @staticmethod
@@ -743,7 +762,8 @@ class GemmaMLPFn(torch.autograd.Function):
         # it cost more than the pass: +60 % on the 8-phase kernel's LDS image, +0.11 ms per layer from the 4-wave
         # kernel's accumulators with the g / u loads one row block ahead, r4)
         if _fp8_site(f8, "down") is not None:
-            _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I])
+            _fp8_dgrad(dout, f8, "down", (wd,), dgu[:, :I],
+                       dy_mx=ctx.mx_dout.take(dout) if ctx.mx_dout is not None else None)
         else:
             K.linear_dgrad(dout, [wd], dgu[:, :I])
         f8gu = _fp8_site(f8, "gate_up")
@@ -773,7 +793,7 @@ class GemmaMLPFn(torch.autograd.Function):
             else:
                 K.linear_dgrad(dgu, [wg, wu], dx)
         side.join(retg, retu, ret_wd)
-        return dx, retg, retu, ret_wd, None, None
+        return dx, retg, retu, ret_wd, None, None, None
 
 
 # ------------------------------------------------------------------------------------ SigLIP blocks

@@ -60,8 +60,11 @@ def _operand(mats: Sequence[torch.Tensor], layout: int, seg_dim: int = L.SEG_OUT
 
 
 def _epi(kind=L.EPI_STORE, accumulate=False, alpha=1.0, cap=0.0, bias=None, in0=None, in1=None, out1=None,
-         out2=None, row_stats=None, rope=None, colscale=None) -> L.Epilogue:
+         out2=None, row_stats=None, rope=None, colscale=None, mx_out=None) -> L.Epilogue:
     e = L.Epilogue()
+    if mx_out is not None:  # (q [M, I] e4m3, MXScales): the GEGLU epilogue's MX copy of h (fp8 GEMMs)
+        q, sc = mx_out
+        e.mx_q, e.mx_ldq, e.mx_scales, e.mx_sld = q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld
     e.colscale = _ptr(colscale)
     e.kind = kind
     e.accumulate = 1 if accumulate else 0
@@ -587,21 +590,36 @@ def add_rmsnorm2_fwd(res, yin, w1, w2, eps1, eps2, h, x):
             "add_rmsnorm2_fwd")
 
 
-def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False):
+def rmsnorm_bwd(x, w, rstd, dy, dres, dx, dw_out, dw_accumulate=False, mx=False):
+    """RMSNorm backward (svla_rmsnorm_bwd); mx=True: svla_rmsnorm_bwd_mx, also returning the MX e4m3 copy of dx
+    (q, MXScales) -- the fp8 dgrad operand -- from the same pass (N % 128 == 0, N > 1536)."""
     rows, N = x.shape
     nb = (rows + RPB - 1) // RPB
     part = torch.empty(nb, N, dtype=torch.float32, device=x.device)
     npart = ctypes.c_int64(0)
-    L.check(L.lib().svla_rmsnorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
-                                     _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart), _stream()),
-            "rmsnorm_bwd")
+    out = None
+    if mx:
+        _req(N % 128 == 0 and N > 1536 and dx.is_contiguous(), "rmsnorm_bwd_mx: N % 128 == 0, N > 1536")
+        q = torch.empty(rows, N, dtype=FP8, device=x.device)
+        sc = MXScales(rows, N, x.device)
+        L.check(L.lib().svla_rmsnorm_bwd_mx(rows, N, x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+                                            _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart),
+                                            q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld, _stream()),
+                "rmsnorm_bwd_mx")
+        out = (q, sc)
+    else:
+        L.check(L.lib().svla_rmsnorm_bwd(rows, N, x.data_ptr(), w.data_ptr(), rstd.data_ptr(), dy.data_ptr(),
+                                         _ptr(dres), dx.data_ptr(), part.data_ptr(), ctypes.byref(npart), _stream()),
+                "rmsnorm_bwd")
     if dw_out is not None:
         colsum_f32(part[:npart.value], dw_out, dw_accumulate)
+    return out
 
 
-def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1, acc2=False, acc1=False):
+def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1, acc2=False, acc1=False, mx=False):
     """Backward of add_rmsnorm2_fwd_train in one pass (svla_rmsnorm2_bwd); weight gradients dw2 / dw1 (or None) by
-    one column-sum launch over both partial planes (two when only one is wanted or the accumulate modes differ)."""
+    one column-sum launch over both partial planes (two when only one is wanted or the accumulate modes differ).
+    mx=True: svla_rmsnorm2_bwd_mx, returning the MX e4m3 copy of dy_out (q, MXScales) from the same pass."""
     rows, N = h.shape
     for t, n in ((h, "h"), (dx, "dx"), (y, "y"), (dh_out, "dh_out"), (dy_out, "dy_out")):
         _req(t.shape == (rows, N) and t.is_contiguous(), f"rmsnorm2_bwd: {n} must be contiguous [{rows}, {N}]")
@@ -609,9 +627,22 @@ def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1,
     nb = (rows + RPB2 - 1) // RPB2
     part = torch.empty(2, nb, N, dtype=torch.float32, device=h.device)
     npart = ctypes.c_int64(0)
-    L.check(L.lib().svla_rmsnorm2_bwd(rows, N, h.data_ptr(), w2.data_ptr(), rstd2.data_ptr(), dx.data_ptr(), _ptr(dres),
-                                      y.data_ptr(), w1.data_ptr(), rstd1.data_ptr(), dh_out.data_ptr(), dy_out.data_ptr(),
-                                      part.data_ptr(), ctypes.byref(npart), _stream()), "rmsnorm2_bwd")
+    out = None
+    if mx:
+        _req(N % 128 == 0, "rmsnorm2_bwd_mx: N % 128 == 0")
+        q = torch.empty(rows, N, dtype=FP8, device=h.device)
+        sc = MXScales(rows, N, h.device)
+        L.check(L.lib().svla_rmsnorm2_bwd_mx(rows, N, h.data_ptr(), w2.data_ptr(), rstd2.data_ptr(), dx.data_ptr(),
+                                             _ptr(dres), y.data_ptr(), w1.data_ptr(), rstd1.data_ptr(),
+                                             dh_out.data_ptr(), dy_out.data_ptr(), part.data_ptr(), ctypes.byref(npart),
+                                             q.data_ptr(), q.stride(0), sc.buf.data_ptr(), sc.ld, _stream()),
+                "rmsnorm2_bwd_mx")
+        out = (q, sc)
+    else:
+        L.check(L.lib().svla_rmsnorm2_bwd(rows, N, h.data_ptr(), w2.data_ptr(), rstd2.data_ptr(), dx.data_ptr(),
+                                          _ptr(dres), y.data_ptr(), w1.data_ptr(), rstd1.data_ptr(), dh_out.data_ptr(),
+                                          dy_out.data_ptr(), part.data_ptr(), ctypes.byref(npart), _stream()),
+                "rmsnorm2_bwd")
     if dw2 is not None and dw1 is not None and acc2 == acc1:
         L.check(L.lib().svla_colsum2_f32(npart.value, N, part.data_ptr(), dw2.data_ptr(), dw1.data_ptr(), int(acc2),
                                          _stream()), "colsum2_f32")
@@ -620,6 +651,7 @@ def rmsnorm2_bwd(h, w2, rstd2, dx, dres, y, w1, rstd1, dh_out, dy_out, dw2, dw1,
             colsum_f32(part[0], dw2, acc2)
         if dw1 is not None:
             colsum_f32(part[1], dw1, acc1)
+    return out
 
 
 def layernorm_fwd(x, w, b, eps, y, mean, rstd):

@@ -92,11 +92,11 @@ class Gemma2RMSNorm(nn.Module):
         shp = x.shape
         return Fn.RMSNormFn.apply(x.reshape(-1, shp[-1]), self.weight, self.eps, slot, mx).view(shp)
 
-    def add_forward(self, residual, y, slot=None):
-        """residual + self(y) (decoder-layer residual branches)."""
+    def add_forward(self, residual, y, slot=None, mx_grad=None):
+        """residual + self(y) (decoder-layer residual branches); mx_grad: an MXSlot for the MX copy of y's gradient."""
         shp = y.shape
         return Fn.AddRMSNormFn.apply(residual.reshape(-1, shp[-1]), y.reshape(-1, shp[-1]), self.weight,
-                                     self.eps, slot).view(shp)
+                                     self.eps, slot, mx_grad).view(shp)
 
     def extra_repr(self):
         return f"{tuple(self.weight.shape)}, eps={self.eps}"
@@ -115,10 +115,10 @@ class Gemma2MLP(nn.Module):
         if act not in ("gelu_pytorch_tanh", "gelu_tanh"):
             raise ValueError(f"Gemma2MLP: activation {act!r} not supported (kernel implements gelu_pytorch_tanh)")
 
-    def forward(self, x, mx_in=None):
+    def forward(self, x, mx_in=None, mx_dout=None):
         shp = x.shape
         out = Fn.GemmaMLPFn.apply(x.reshape(-1, shp[-1]), self.gate_proj.weight, self.up_proj.weight,
-                                  self.down_proj.weight, getattr(self, "_svla_fp8", None), mx_in)
+                                  self.down_proj.weight, getattr(self, "_svla_fp8", None), mx_in, mx_dout)
         return out.view(*shp[:-1], self.hidden_size)
 
 
@@ -192,7 +192,7 @@ class Gemma2Attention(nn.Module):
                                float(self.attn_logit_softcapping or 0.0), int(self.sliding_window or 0))
 
     def forward(self, hidden_states, attention_mask: KVMask, rope: tuple, cache: Optional[Gemma2KVCache] = None,
-                attn_sink: Optional[list] = None, mx_in=None):
+                attn_sink: Optional[list] = None, mx_in=None, mx_dout=None):
         B, Lq, H = hidden_states.shape
         cfg = self.attn_cfg(B, Lq)
         cos, sin = rope
@@ -213,7 +213,7 @@ class Gemma2Attention(nn.Module):
         capture = {} if attn_sink is not None else None
         out = Fn.GemmaAttentionFn.apply(hidden_states.reshape(B * Lq, H), self.q_proj.weight, self.k_proj.weight,
                                         self.v_proj.weight, self.o_proj.weight, cos, sin, attention_mask.kv_class,
-                                        cfg, getattr(self, "_svla_fp8", None), capture, mx_in)
+                                        cfg, getattr(self, "_svla_fp8", None), capture, mx_in, mx_dout)
         if attn_sink is not None:
             attn_sink.append(Fn.gemma_attention_weights(capture["qkv"], attention_mask.kv_class, cfg))
         return out.view(B, Lq, H)
@@ -262,22 +262,24 @@ class Gemma2DecoderLayer(nn.Module):
         s1, s2 = Fn.ResidualSlot(), Fn.ResidualSlot()
         # fp8 projections (configs[4]): the norms also emit the MX e4m3 copies of q|k|v's and gate|up's inputs
         f8 = getattr(self.self_attn, "_svla_fp8", None) if cache is None else None
+        # (and the backward norms those of the o and down dgrad inputs)
         mx_a, mx_m = Fn.mx_slot_for(f8, "qkv"), Fn.mx_slot_for(f8, "gate_up")
+        mx_da, mx_dm = Fn.mx_slot_for(f8, "o"), Fn.mx_slot_for(f8, "down")
         x = self.input_layernorm(hidden_states, s1, mx_a)
-        a = self.self_attn(x, attention_mask, rope, cache, attn_sink, mx_a)
+        a = self.self_attn(x, attention_mask, rope, cache, attn_sink, mx_a, mx_da)
         pa, pf = self.post_attention_layernorm, self.pre_feedforward_layernorm
         if FUSED_NORM_PAIR[0]:
             # post-attention norm + residual and the pre-feedforward norm in one launch (AddRMSNorm2Fn); h's
             # residual-branch gradient arrives through s2 (post_feedforward's add parks it there)
             shp = a.shape
             h, x = Fn.AddRMSNorm2Fn.apply(hidden_states.reshape(-1, shp[-1]), a.reshape(-1, shp[-1]), pa.weight,
-                                          pf.weight, pa.eps, pf.eps, s1, s2, mx_m)
+                                          pf.weight, pa.eps, pf.eps, s1, s2, mx_m, mx_da)
             h, x = h.view(shp), x.view(shp)
         else:
-            h = pa.add_forward(hidden_states, a, s1)
+            h = pa.add_forward(hidden_states, a, s1, mx_da)
             x = pf(h, s2, mx_m)
-        m = self.mlp(x, mx_m)
-        return self.post_feedforward_layernorm.add_forward(h, m, s2)
+        m = self.mlp(x, mx_m, mx_dm)
+        return self.post_feedforward_layernorm.add_forward(h, m, s2, mx_dm)
 
 
 class Gemma2Model(nn.Module):

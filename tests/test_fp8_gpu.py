@@ -317,6 +317,42 @@ def test_norms_emit_mx_copy_bitwise(cuda):
     assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8)) and torch.equal(sc.exponents(), scr.exponents())
 
 
+def test_norm_backwards_emit_mx_copy_bitwise(cuda):
+    """svla_rmsnorm_bwd_mx / svla_rmsnorm2_bwd_mx: every output of the plain backward kernels bit for bit, and the MX
+    copy of the stored input gradient bit for bit quant_mx_rows of it (the fp8 down / o dgrad operands)."""
+    torch.manual_seed(47)
+    M, N = 999, 2304
+    x = (torch.randn(M, N, device=cuda) * 2).to(BF)
+    y = torch.randn(M, N, device=cuda).to(BF)
+    w1 = (torch.randn(N, device=cuda) * 0.3).to(BF)
+    w2 = (torch.randn(N, device=cuda) * 0.3).to(BF)
+    dy = torch.randn(M, N, device=cuda).to(BF)
+    dres = torch.randn(M, N, device=cuda).to(BF)
+    rs = torch.rand(M, device=cuda) + 0.5
+    rs2 = torch.rand(M, device=cuda) + 0.5
+    outs = []
+    for mx in (False, True):
+        dx = torch.empty_like(x)
+        dw = torch.zeros(N, dtype=BF, device=cuda)
+        cp = K.rmsnorm_bwd(x, w1, rs, dy, dres, dx, dw, mx=mx)
+        outs.append((dx, dw, cp))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    qr, scr = K.quant_mx_rows(outs[0][0])
+    q, sc = outs[1][2]
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8)) and torch.equal(sc.exponents(), scr.exponents())
+    outs = []
+    for mx in (False, True):
+        dh, dyo = torch.empty_like(x), torch.empty_like(x)
+        dw2, dw1 = torch.zeros(N, dtype=BF, device=cuda), torch.zeros(N, dtype=BF, device=cuda)
+        cp = K.rmsnorm2_bwd(x, w2, rs2, dy, dres, y, w1, rs, dh, dyo, dw2, dw1, mx=mx)
+        outs.append((dh, dyo, dw2, dw1, cp))
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert torch.equal(a, b)
+    qr, scr = K.quant_mx_rows(outs[0][1])
+    q, sc = outs[1][4]
+    assert torch.equal(q.view(torch.uint8), qr.view(torch.uint8)) and torch.equal(sc.exponents(), scr.exponents())
+
+
 def test_quant_mx_rows_nonfinite_blocks_are_nan(cuda):
     """A NaN or +-Inf element makes its whole 32-k MX block NaN -- scale byte 0xFF (OCP MX v1.0 §5.3) and e4m3 NaN
     elements (0x7F) -- instead of a finite clamp that would hide a diverging activation or dY; every other block is
@@ -418,3 +454,12 @@ def test_gemm_mxfp8_geglu(cuda):
     he = (torch.nn.functional.gelu(ge.float(), approximate="tanh").to(BF).float() * ue.float()).to(BF)
     print(f"mxfp8 geglu: g {rel(gg, ge):.2e} u {rel(uu, ue):.2e} h {rel(h, he):.2e}")
     assert rel(gg, ge) < 4e-3 and rel(uu, ue) < 4e-3 and rel(h, he) < 6e-3
+    # the same launch with the MX copy of h from the epilogue: h, g, u bit for bit, and the copy bit for bit
+    # quant_mx_rows(h) (the fp8 down operand); M = 700 leaves a ragged last row block
+    h2, g2, u2 = (torch.empty(m, inter, dtype=BF, device=cuda) for _ in range(3))
+    hq = (torch.empty(m, inter, dtype=torch.float8_e4m3fn, device=cuda), K.MXScales(m, inter, cuda))
+    K.gemm_mxfp8(xq, xs, wq, ws, h2, kind=L.EPI_GEGLU, geglu_I=inter, out1=g2, out2=u2, mx_out=hq)
+    assert torch.equal(h2, h) and torch.equal(g2, gg) and torch.equal(u2, uu)
+    qr, scr = K.quant_mx_rows(h)
+    assert torch.equal(hq[0].view(torch.uint8), qr.view(torch.uint8))
+    assert torch.equal(hq[1].exponents(), scr.exponents())
