@@ -755,6 +755,13 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(int B, int L, int H, co
 // round32(L)..round64(L)-1 of the workspace hold whatever the allocator left there (possibly NaN patterns).  Query
 // column q of dS^T feeds only output row q of dQ (it is the A operand's row), and rows q >= L are never stored (the
 // q < L test of the epilogue), so those columns cannot reach a result; no zero-fill is needed.
+// LDS row pitch of the dS^T tile (bf16): the A-operand reads take keys 4g + j (g = lane >> 4) of 16 queries, i.e.
+// rows 4 apart; at a 64-element (128-B) pitch those four rows share one 8-bank span (4-way conflicts, 21.7 % of the
+// kernel's LDS cycles, profiles/r5b_block_pmc.txt); at 72 (144 B) rows 4g start 16g banks apart: conflict-free,
+// and rows stay 16-B aligned for the tile's b128 writes
+#ifndef SVLA_DQ_DS_PITCH
+#define SVLA_DQ_DS_PITCH 72
+#endif
 template <bool ROPE>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(svla_attn_args a, const bf16_t* __restrict__ dsT,
                                                                 bf16_t* __restrict__ dq, int64_t lddq) {
@@ -787,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(svla_attn_args a
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i = t + 256 * u, r = i >> 3, ch = i & 7;
-      *reinterpret_cast<u32x4*>(smem + TB + (r * 64 + ch * 8) * 2) = sv[u];
+      *reinterpret_cast<u32x4*>(smem + TB + (r * SVLA_DQ_DS_PITCH + ch * 8) * 2) = sv[u];
     }
     __syncthreads();
 #pragma unroll
@@ -795,8 +802,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_ds_kernel(svla_attn_args a
       float zv[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // keys 32ks + 4g + j and 32ks + 16 + 4g + j of the wave's query 16w + c
-        zv[j] = bf2f(ls[(32 * ks + 4 * g + j) * 64 + 16 * w + c]);
-        zv[4 + j] = bf2f(ls[(32 * ks + 16 + 4 * g + j) * 64 + 16 * w + c]);
+        zv[j] = bf2f(ls[(32 * ks + 4 * g + j) * SVLA_DQ_DS_PITCH + 16 * w + c]);
+        zv[4 + j] = bf2f(ls[(32 * ks + 16 + 4 * g + j) * SVLA_DQ_DS_PITCH + 16 * w + c]);
       }
       mfma_tr_sweep<RS, NDT, false>(acc, smem, 32 * ks, pack_frag(zv), lane);
     }
@@ -1006,7 +1013,7 @@ int bwd_launch(const svla_attn_args& a, const bf16_t* out, int64_t ldo, const bf
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, ROPE, CAP, true>), dim3((unsigned)(nt * a.Hkv * a.B)), dim3(256),
                          lds_kv, s, a, dout, lddo, lse, delta, dk, lddk, dv, lddv, dsT);
       if (int rc = svla::check_launch("attn_bwd_dkv")) return rc;
-      const int lds_q = tile_bytes<D>(64) + 64 * 64 * 2;
+      const int lds_q = tile_bytes<D>(64) + 64 * SVLA_DQ_DS_PITCH * 2;
       set_lds_once<attn_bwd_dq_ds_kernel<ROPE>>(lds_q);
       hipLaunchKernelGGL((attn_bwd_dq_ds_kernel<ROPE>), dim3((unsigned)(nt * a.Hq * a.B)), dim3(256), lds_q, s, a,
                          dsT, dq, lddq);

@@ -253,6 +253,7 @@ class TrainEngine:
                 p.data = view
                 p._svla_grad = self.flat_grad[o:o + p.numel()].view_as(p)
                 p._svla_accum = False
+                Fn.register_flat_param(p)
         self.exchange = ZeroExchange(self.flat_param, self.flat_grad, buckets, process_group)
         ex = self.exchange
         # ---- sharded optimizer state: fp32 master / m / v of the owned chunk of every bucket, back to back

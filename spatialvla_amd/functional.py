@@ -8,6 +8,7 @@ in which case autograd receives None for that parameter (no extra copy, no autog
 """
 import math
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -25,10 +26,23 @@ def _empty(*shape, dtype=BF16, like=None, device=None):
     return torch.empty(*shape, dtype=dtype, device=like.device if like is not None else device)
 
 
+# Parameters whose gradients go to a TrainEngine's flat buffer, by (data_ptr, shape): a Function's saved weight can
+# come back from ctx.saved_tensors as an alias without the Parameter's attributes -- torch.utils.checkpoint's
+# recompute (gradient checkpointing) returns the recomputed saved tensors -- and its gradient must still land in the
+# flat buffer, not in a fresh tensor autograd would put in .grad.
+_FLAT_PARAMS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+
+
+def register_flat_param(p: torch.Tensor):
+    _FLAT_PARAMS[(p.data_ptr(), tuple(p.shape))] = p
+
+
 def _grad_dest(p: torch.Tensor, needed: bool):
     """(buffer, accumulate, value returned to autograd) for the gradient of parameter p."""
     if not needed:
         return None, False, None
+    if not hasattr(p, "_svla_grad"):
+        p = _FLAT_PARAMS.get((p.data_ptr(), tuple(p.shape)), p)
     g = getattr(p, "_svla_grad", None)
     if g is not None:
         return g, bool(getattr(p, "_svla_accum", False)), None

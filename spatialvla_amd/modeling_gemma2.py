@@ -18,6 +18,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 import torch
+import torch.utils.checkpoint
 from torch import nn
 
 from . import functional as Fn
@@ -291,7 +292,8 @@ class Gemma2Model(nn.Module):
         self.embed_tokens = nn.Embedding(config.vocab_size, config.hidden_size, self.padding_idx)
         self.layers = nn.ModuleList([Gemma2DecoderLayer(config, i) for i in range(config.num_hidden_layers)])
         self.norm = Gemma2RMSNorm(config.hidden_size, eps=config.rms_norm_eps)
-        # reference :669 / :752-762; accepted and recorded, never recomputes (Gemma2ForCausalLM._set_gradient_checkpointing)
+        # reference :669 / :752-762: the training forward re-runs each decoder layer in the backward when set
+        # (Gemma2ForCausalLM._set_gradient_checkpointing)
         self.gradient_checkpointing = False
 
     def get_input_embeddings(self):
@@ -325,7 +327,15 @@ class Gemma2Model(nn.Module):
                 hidden_states.register_hook(lambda g, i=i: hook(i))
             if pwait is not None:
                 pwait(("gemma", i))
-            hidden_states = layer(hidden_states, attention_mask, rope, cache, attn_sink)
+            if (self.gradient_checkpointing and self.training and cache is None and attn_sink is None
+                    and torch.is_grad_enabled()):
+                # reference :752-762: the layer's activations are dropped after the forward and the layer re-runs in
+                # the backward (non-reentrant torch.utils.checkpoint: the saved tensors of the HIP autograd Functions
+                # are recomputed, bitwise, since every kernel is deterministic)
+                hidden_states = torch.utils.checkpoint.checkpoint(layer, hidden_states, attention_mask, rope,
+                                                                  use_reentrant=False)
+            else:
+                hidden_states = layer(hidden_states, attention_mask, rope, cache, attn_sink)
         if cache is not None:
             cache.seen_tokens += hidden_states.shape[1]
         if pwait is not None:
@@ -432,17 +442,12 @@ class Gemma2ForCausalLM(nn.Module):
         self.model = decoder
 
     def _set_gradient_checkpointing(self, enable: bool = True, gradient_checkpointing_func=None):
-        """The reference training script's call (train/spatialvla_pretrain.py:331-332 -> transformers'
-        _set_gradient_checkpointing, which flips `gradient_checkpointing` on the modules that have it; the reference
-        decoder then re-runs each layer in backward, modeling_gemma2.py:752-762).  Accepted as a recorded no-op: the
-        whole B=32 working set (~120 GB) stays resident in the 288 GB of HBM, so recompute would only
-        add a forward pass.  Numerically the two are the same computation.  Enabling it warns once: a caller who
-        relies on it to fit a larger batch or a smaller device gets no memory saving."""
-        if enable and not getattr(Gemma2ForCausalLM, "_svla_ckpt_warned", False):
-            Gemma2ForCausalLM._svla_ckpt_warned = True
-            warnings.warn("spatialvla_amd: gradient checkpointing is accepted but never recomputes; activations stay "
-                          "resident in HBM (about 120 GB at B=32, L=312 for SpatialVLA-4B), so it saves no memory",
-                          stacklevel=2)
+        """The reference training script's call (train/spatialvla_pretrain.py:333-334 -> transformers'
+        _set_gradient_checkpointing, which flips `gradient_checkpointing` on the modules that have it); the decoder
+        then re-runs each layer in the backward (modeling_gemma2.py:752-762, here Gemma2Model.forward with
+        torch.utils.checkpoint, non-reentrant whatever gradient_checkpointing_func says: the layer hooks of the ZeRO-1
+        exchange and the side-stream weight gradients need the non-reentrant engine).  Activation memory of the 26
+        layers drops to their inputs; one more forward per step."""
         for m in self.modules():
             if hasattr(m, "gradient_checkpointing"):
                 m.gradient_checkpointing = bool(enable)

@@ -118,8 +118,9 @@ class SpatialVLAMultiModalProjector(nn.Module):
 class SpatialVLAPreTrainedModel(PreTrainedModel):
     config_class = SpatialVLAConfig
     base_model_prefix = "model"
-    # accepted (gradient_checkpointing_enable, the training script's language_model._set_gradient_checkpointing()),
-    # never recomputes: the working set stays resident in HBM (Gemma2ForCausalLM._set_gradient_checkpointing)
+    # gradient_checkpointing_enable / the training script's language_model._set_gradient_checkpointing(): the Gemma2
+    # decoder layers re-run in the backward (Gemma2ForCausalLM._set_gradient_checkpointing); the vision tower's flag is
+    # recorded only, as in the reference (spatialvla_pretrain.py:331 sets an attribute its encoder never reads)
     supports_gradient_checkpointing = True
     _no_split_modules = ["SpatialVLAMultiModalProjector", "ZoeDepthForDepthEstimation", "Ego3DPositionEmbeddingMLP"]
 
@@ -222,8 +223,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         return None  # SpatialVLA unties lm_head (spatialvla_pretrain.py:321-325)
 
     def _set_gradient_checkpointing(self, enable: bool = True, gradient_checkpointing_func=None):
-        """gradient_checkpointing_enable() lands here: recorded on every module that carries the flag, no recompute
-        (see Gemma2ForCausalLM._set_gradient_checkpointing)."""
+        """gradient_checkpointing_enable() lands here: the Gemma2 layers recompute in the backward (see
+        Gemma2ForCausalLM._set_gradient_checkpointing); the vision tower's flag is recorded only."""
         self.language_model._set_gradient_checkpointing(enable, gradient_checkpointing_func)
         self.vision_tower.gradient_checkpointing = bool(enable)
 

@@ -2,8 +2,9 @@
   * prepare_inputs_for_generation (reference model/modeling_spatialvla.py:445-482 over modeling_gemma2.py:1015-1091):
     slicing to the uncached tokens, per-sequence positions from the attention mask + 1, pixel values only at the
     first step, intrinsic passed through;
-  * the gradient-checkpointing calls of the reference training script (train/spatialvla_pretrain.py:329-332) and
-    gradient_checkpointing_enable() are accepted;
+  * the gradient-checkpointing calls of the reference training script (train/spatialvla_pretrain.py:331-334) and
+    gradient_checkpointing_enable() set the flag the decoder's recompute path reads (tests/test_model_gpu.py
+    test_gradient_checkpointing_recomputes_bitwise runs it);
   * a grad-enabled attention forward with per-sequence RoPE tables (padded prompts) is refused up front: the
     attention backward's RoPE transpose reads table row = position in the sequence."""
 import pytest

@@ -244,6 +244,48 @@ def test_fused_norm_pair_bitwise(cuda):
             assert torch.equal(g1[n], g0[n]), n
 
 
+def test_gradient_checkpointing_recomputes_bitwise(cuda):
+    """language_model._set_gradient_checkpointing() (train/spatialvla_pretrain.py:333-334; reference decoder
+    modeling_gemma2.py:752-762): every Gemma2 layer re-runs in the backward, and the loss, logits and every gradient
+    equal the resident run's bit for bit (deterministic kernels).  Also under the TrainEngine: the losses and fp32
+    masters of two optimizer steps with ZeRO layer hooks / flat gradient buffers are identical."""
+    import warnings
+    from spatialvla_amd import presets
+    from spatialvla_amd.engine import TrainEngine
+    cfgd = H.cfg_dict("tiny")
+    b = H.batch_tensors(presets.synthetic_batch(cfgd, batch=2, seed=6), cuda)
+    depth = torch.rand(2, 1, 224, 224, generator=torch.Generator().manual_seed(4)).mul(3).add(0.5).to(cuda)
+    out, eng_out = {}, {}
+    for ck in (False, True):
+        model = H.build_hip_model(cfgd, "cuda:0")
+        model.train()  # the reference recomputes in training mode only (modeling_gemma2.py:752)
+        model.vision_zoe_model.eval()
+        if ck:
+            with warnings.catch_warnings():
+                warnings.simplefilter("error")  # no "accepted but never recomputes" warning any more
+                model.language_model._set_gradient_checkpointing()
+            assert model.language_model.model.gradient_checkpointing
+        calls = []
+        layer0 = model.language_model.model.layers[0]
+        fwd = layer0.forward  # counted by a wrapper: torch.utils.checkpoint's recompute skips module hooks
+        layer0.forward = lambda *a, **k: (calls.append(1), fwd(*a, **k))[1]
+        out[ck] = H.run_hip(model, b, depth=depth)
+        del layer0.forward
+        # the checkpointed run executes layer 0's forward twice (forward + recompute in the backward)
+        assert len(calls) == (2 if ck else 1), (ck, len(calls))
+        model.zero_grad(set_to_none=True)
+        model.predict_depth = lambda pv, _d=depth: _d
+        eng = TrainEngine(model, lr=1e-3, warmup_ratio=0.0, total_steps=10, max_grad_norm=1.0, bucket_bytes=1 << 16)
+        losses = [eng.train_step(b).clone() for _ in range(2)]
+        eng_out[ck] = (torch.stack(losses).cpu(), eng.full_master().cpu())
+    (l1, lg1, g1, _), (l0, lg0, g0, _) = out[True], out[False]
+    assert torch.equal(l1, l0) and torch.equal(lg1, lg0)
+    assert g1.keys() == g0.keys()
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n
+    assert torch.equal(eng_out[True][0], eng_out[False][0]) and torch.equal(eng_out[True][1], eng_out[False][1])
+
+
 def _layer4b_model(li, cuda):
     from spatialvla_amd import SpatialVLAConfig
     from spatialvla_amd import presets
