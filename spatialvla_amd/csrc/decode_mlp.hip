@@ -28,6 +28,12 @@ constexpr int DM_KCH = 5;   // 16-B chunks per lane of a gate / up row: H <= 256
 constexpr int DM_NC = 2;    // norm chunks per thread: H <= 4096
 constexpr int DM_DCH = 5;   // 16-B chunks per thread of a down row: I <= 10240
 constexpr int DM_OCH = 4;
+#ifndef DM_DPRE
+// down rows a block loads before the grid barrier at batch 1; 1 = only the first.  Loading all of a block's rows (5)
+// measured slower, 1.90 vs 1.85 ms per token, and 2 or 3 the same as 1 (profiles/r8j_decode_mlp_down_prefetch_ab.txt):
+// phase C is not where the launch waits
+#define DM_DPRE 1
+#endif
 #ifndef DM_DEPTH
 #define DM_DEPTH 2  // gate|up row pairs a wave has in flight in phase A (2 or 3; 3 measured slower, r7g)
 #endif   // 16-B chunks per lane of an o-projection row: KO <= 2048
@@ -323,7 +329,8 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     }
   }
 
-  // the block's first down row is independent of act: its weights stream in while the grid barrier waits
+  // the block's down rows are independent of act: their weights stream in while phase A drains and the grid barrier
+  // waits -- the first one, or at batch 1 the first DM_DPRE (all of them when H <= DM_DPRE x blocks)
   u32x4 da[DM_DCH], db[DM_DCH];
   auto load_down = [&](int64_t row, u32x4 (&dst)[DM_DCH]) {
     const bf16_t* wr = wd + row * ldd;
@@ -334,9 +341,25 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     }
   };
   int64_t n = blockIdx.x;
-  load_down(n < H ? n : H - 1, da);
-  // a block that missed this barrier would read a partial act: it writes NaN rows instead
-  const bool late = grid_barrier<DM_DCH, 1>(sync, gridDim.x, bflag, spin_ticks);
+  constexpr bool PRE_OK = MR == 1 && DM_DPRE > 1;
+  const bool pre = PRE_OK && H <= (int64_t)DM_DPRE * gridDim.x;  // grid-uniform
+  u32x4 dpre[PRE_OK ? DM_DPRE : 1][DM_DCH];
+  bool late;
+  if constexpr (PRE_OK) {
+    if (pre) {
+#pragma unroll
+      for (int q = 0; q < DM_DPRE; ++q) {
+        const int64_t rq = n + (int64_t)q * gridDim.x;
+        load_down(rq < H ? rq : H - 1, dpre[q]);
+      }
+      // a block that missed this barrier would read a partial act: it writes NaN rows instead
+      late = grid_barrier<DM_DPRE * DM_DCH, 1>(sync, gridDim.x, bflag, spin_ticks);
+    }
+  }
+  if (!pre) {
+    load_down(n < H ? n : H - 1, da);
+    late = grid_barrier<DM_DCH, 1>(sync, gridDim.x, bflag, spin_ticks);
+  }
 
   // ---------------- phase C: down rows of this block, four waves split each row's K range
   // one token row (the batch-1 decode step): the thread's act chunks, the same for every down row, in registers
@@ -348,8 +371,7 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
       av[i] = k < I ? *reinterpret_cast<const u32x4*>(act + k) : u32x4{0u, 0u, 0u, 0u};
     }
   }
-  auto row = [&](const u32x4 (&dcur)[DM_DCH], u32x4 (&dnext)[DM_DCH]) {
-    load_down(n + gridDim.x < H ? n + gridDim.x : H - 1, dnext);  // unconditional: see phase A
+  auto dot_row = [&](const u32x4 (&dcur)[DM_DCH]) {
     float acc[MR];
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc[m] = 0.f;
@@ -382,6 +404,18 @@ __global__ __launch_bounds__(256, DM_BPC) void decode_mlp_kernel(int M, int H, i
     if (t < M) out[t * ldo + n] = late ? (bf16_t)0x7fc0 : f2bf(((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
     __syncthreads();  // part is rewritten by the next row
     n += gridDim.x;
+  };
+  if constexpr (PRE_OK) {
+    if (pre) {
+#pragma unroll
+      for (int q = 0; q < DM_DPRE; ++q)
+        if (n < H) dot_row(dpre[q]);
+      return;
+    }
+  }
+  auto row = [&](const u32x4 (&dcur)[DM_DCH], u32x4 (&dnext)[DM_DCH]) {
+    load_down(n + gridDim.x < H ? n + gridDim.x : H - 1, dnext);  // unconditional: see phase A
+    dot_row(dcur);
   };
   while (n < H) {
     row(da, db);
