@@ -114,6 +114,10 @@ typedef struct {
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                    const svla_epilogue* epi, void* workspace, size_t ws_bytes, void* stream);
+/* Cap (this host thread) on the persistent grid of the stream-K GEMM schedules: the GEMMs it launches next use at
+ * most `cap` workgroups a persistent wave (0 = every CU).  Set around a GEMM queued on a side stream so the main
+ * stream's kernels find free CUs beside it; results stay deterministic (a fixed cap fixes the split). */
+void svla_gemm_set_cu_cap(int cap);
 size_t svla_gemm_workspace_bytes(void);
 /* svla_gemm_bf16 with an explicit kernel choice (tests / tuning tools, not a reference interface): 0 = auto (as
  * svla_gemm_bf16), 1 = two-barrier tiles, 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case,

@@ -135,6 +135,7 @@ SIGNATURES = {
                                    c_vp, c_i64, c_vp, c_vp]),
     "svla_decode_mlp_sync_bytes": (ctypes.c_size_t, []),
     "svla_decode_mlp_grid": (c_i32, [c_i64, c_i64, c_i64]),
+    "svla_gemm_set_cu_cap": (None, [c_i32]),
     "svla_decode_mlp_debug": (None, [c_i32, c_i32, c_i32]),
     "svla_decode_mlp": (c_i32, [c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp,
                                 c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,

@@ -3050,6 +3050,16 @@ struct GemmCtx {
 
 using svla::num_cus;
 
+// Persistent-grid cap of this host thread's GEMM launches (svla_gemm_set_cu_cap; 0 = every CU): the stream-K
+// schedules of launch4 / launch8 size their persistent grid by it, so a GEMM queued on a side stream (the weight
+// gradients beside the input-gradient chain, functional._SideWork) leaves CUs free for the main stream's kernels
+// instead of holding every CU until it is done.
+thread_local int g_cu_cap = 0;
+int grid_cus() {
+  const int g = num_cus();
+  return g_cu_cap > 0 && g_cu_cap < g ? g_cu_cap : g;
+}
+
 #ifndef G4_SKMIN
 // fewest k-tiles per block of the 4-wave kernel's stream-K share before a full wave of tiles is folded in as well:
 // 4, not 8 -- the o-projection dgrad (312 tiles, K = 2304) ran all-stream-K at 8 (every tile split, a 256 KB slab
@@ -3078,20 +3088,22 @@ int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   sk.dp_tiles = (int)tiles;
   sk.grid = (int)tiles;
   // stream-K over the tiles of the last, partial wave of the grid (persistent grid = one block per CU)
-  const int G = num_cus();
+  const int G = grid_cus();
   const int64_t rem = tiles % G;
   int64_t sk_tiles = tiles < G ? tiles : rem;
   // fewer than 8 k-tiles per block would split a tile over too many slabs: fold one more full wave into SK
   if (sk_tiles * sk.nk < 8 * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;  // last wave nearly full: nothing to balance
-  const size_t need = sk_workspace_bytes(G);
+  const size_t need = sk_workspace_bytes(num_cus());  // the chip-wide layout (counters behind num_cus() slabs)
   if (ctx.variant != 2 && sk.nk >= G8_SKMIN_NK && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 &&
       sk_tiles < 2 * G && sk_tiles * sk.nk >= 8 * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
     sk.sk_iters = sk_tiles * sk.nk;
     sk.slabs = reinterpret_cast<float*>(ctx.ws);
-    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * G * 32 * p8::NTH * 16);
+    // the workspace layout is that of the whole chip (svla_gemm_workspace_bytes): the arrival counters sit behind the
+    // slabs of num_cus() blocks whatever grid this launch uses (a capped grid must not move them onto slab memory)
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * num_cus() * 32 * p8::NTH * 16);
   }
   dim3 grid((unsigned)sk.grid), block(p8::NTH);
   const int la = A.layout, lb = B.layout;
@@ -3159,12 +3171,12 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   sk.nk = (int)((K + BK - 1) / BK);
   sk.dp_tiles = (int)tiles;
   sk.grid = (int)tiles;
-  const int G = num_cus();
+  const int G = grid_cus();
   const int64_t rem = tiles % G;
   int64_t sk_tiles = tiles < G ? tiles : rem;
   if (sk_tiles * sk.nk < G4_SKMIN * G && tiles >= rem + G) sk_tiles = rem + G;
   if (tiles > G && rem * 4 >= 3 * G) sk_tiles = 0;
-  const size_t need = sk_workspace_bytes(G);
+  const size_t need = sk_workspace_bytes(num_cus());  // the chip-wide layout (counters behind num_cus() slabs)
   // stream-K only from 64 k-tiles a tile: below that the slab hand-off costs more than the data-parallel tail round
   // it replaces (tools/gemm_ab.py, profiles/r5e_gemm_ab_nosk.txt, same box, interleaved: data-parallel rounds were
   // 3-7 % faster for q|k|v fwd, o fwd / dgrad and down dgrad at 32-36 k-tiles and 34-37 % faster for sub-wave grids
@@ -3180,7 +3192,9 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
     // 5-12 % slower that way
     sk.sk_first = sk.sk_iters >= (int64_t)G4_SKFIRST_MIN * G ? 1 : 0;
     sk.slabs = reinterpret_cast<float*>(ctx.ws);
-    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * G * 32 * p8::NTH * 16);
+    // the workspace layout is that of the whole chip (svla_gemm_workspace_bytes): the arrival counters sit behind the
+    // slabs of num_cus() blocks whatever grid this launch uses (a capped grid must not move them onto slab memory)
+    sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + (size_t)2 * num_cus() * 32 * p8::NTH * 16);
   }
   dim3 grid((unsigned)sk.grid), block(p4::NTH);
 #define SVLA_LAUNCH4(LA_, LB_)                                                                       \
@@ -3271,6 +3285,8 @@ int check_operand(const svla_operand* op, const char* name, int64_t R, int64_t K
 }  // namespace
 
 extern "C" size_t svla_gemm_workspace_bytes(void) { return sk_workspace_bytes(num_cus()); }
+
+extern "C" void svla_gemm_set_cu_cap(int cap) { g_cu_cap = cap > 0 ? cap : 0; }
 
 #if G4_STAMPS
 extern "C" int svla_diag_g4_stamps(void* host, size_t bytes) {  // diagnostic builds only (not in svla.h)

@@ -67,6 +67,12 @@ def _c(t):
 # stream at the end of the backward pass (an autograd engine callback) and wherever the engine hands gradients to
 # a collective (join_side_work, TrainEngine's bucket hooks).
 WGRAD_STREAM = [os.environ.get("SVLA_WGRAD_STREAM", "1") != "0"]
+# CUs the side-stream weight-gradient GEMMs leave to the main stream (their stream-K persistent grid is capped at
+# num_cus - reserve, svla_gemm_set_cu_cap); 0 = they may take every CU.  Without it a persistent weight-gradient grid
+# holds every CU until it is done and the main stream's next kernel (the norm-pair backward, 69 us alone) waits
+# ~600 us for a CU (profiles/r7a_block_breakdown.txt).  8: step 216.4-216.8 -> 214.3-214.4 ms, block 4.65-4.67 ->
+# 4.61 ms (16: the same within noise; profiles/r8q_side_cu_reserve_ab.txt)
+SIDE_CU_RESERVE = [int(os.environ.get("SVLA_SIDE_CU_RESERVE", "8"))]
 WGRAD_DEFER = [os.environ.get("SVLA_WGRAD_DEFER", "1") != "0"]
 _side_streams: dict = {}
 _join_queued: dict = {}  # device -> main stream the end-of-backward callback will make wait
@@ -85,6 +91,16 @@ def join_side_work():
     for dev, main in list(_join_queued.items()):
         main.wait_stream(_side_streams[dev])
         del _join_queued[dev]
+
+
+_NUM_CUS: dict = {}
+
+
+def _num_cus(device) -> int:
+    n = _NUM_CUS.get(device)
+    if n is None:
+        n = _NUM_CUS[device] = torch.cuda.get_device_properties(device).multi_processor_count
+    return n
 
 
 class _SideWork:
@@ -106,8 +122,16 @@ class _SideWork:
             return fn()
         self.side.wait_stream(self.main)
         self.reads.extend(reads)
+        res = SIDE_CU_RESERVE[0]
         with torch.cuda.stream(self.side):
-            return fn()
+            if res <= 0:
+                return fn()
+            lib = L.lib()
+            lib.svla_gemm_set_cu_cap(max(1, _num_cus(self.side.device) - res))
+            try:
+                return fn()
+            finally:
+                lib.svla_gemm_set_cu_cap(0)
 
     def join(self, *returned):
         if not self.on:

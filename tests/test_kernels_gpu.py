@@ -153,6 +153,36 @@ def test_gemm_two_streams_bitwise(cuda):
             assert torch.equal(outs[si][j], ref[j]), (si, j)
 
 
+@pytest.mark.parametrize("cap", [248, 200, 97])
+def test_gemm_cu_cap_stream_k(cuda, cap):
+    """svla_gemm_set_cu_cap (the side-stream weight-gradient GEMMs' persistent-grid cap, functional.SIDE_CU_RESERVE):
+    stream-K schedules on a capped grid -- the 4-wave kernel (long K, every wgrad), the 8-phase one (short K, the B=1
+    gate|up wgrad that once read a stale arrival counter when the cap moved the counters onto slab memory) -- give the
+    fp32 product within bf16 rounding, are deterministic run to run, and leave the uncapped launches after them right."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(31)
+    shapes = [(18432, 2304, 312), (2304, 9216, 9984), (4096, 2304, 9984), (1152, 1152, 8192)]  # wgrad: dW = dY^T X
+    lib = L.lib()
+    for M, N, Kd in shapes:
+        dy, x = _r(Kd, M, scale=0.5), _r(Kd, N, scale=0.5)
+        ref = (dy.float().t() @ x.float())
+        outs = []
+        try:
+            lib.svla_gemm_set_cu_cap(cap)
+            for _ in range(2):
+                o = torch.full((M, N), float("nan"), dtype=BF, device=cuda)
+                Kn.linear_wgrad(dy, x, [o])
+                outs.append(o)
+        finally:
+            lib.svla_gemm_set_cu_cap(0)
+        o0 = torch.full((M, N), float("nan"), dtype=BF, device=cuda)
+        Kn.linear_wgrad(dy, x, [o0])
+        assert torch.equal(outs[0], outs[1]), (M, N, Kd)
+        for o in (outs[0], o0):
+            assert torch.isfinite(o.float()).all(), (M, N, Kd)
+            assert ((o.float() - ref).norm() / ref.norm()).item() < 8e-3, (M, N, Kd)
+
+
 @pytest.mark.parametrize("M,N,K", [(2000, 16500, 200), (2304, 14336, 1000), (4100, 8200, 64), (9984, 2304, 2048),
                                    (1000, 3000, 8192)])
 @pytest.mark.parametrize("layouts", ["nt", "nn", "tn"])

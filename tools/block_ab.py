@@ -66,11 +66,14 @@ def run(use_slot, iters=10):
 if len(sys.argv) > 2 and sys.argv[1] == "flag":
     from spatialvla_amd import modeling_gemma2 as MG
     from spatialvla_amd import kernels as Kn
-    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS, "wgrad_stream": Fn.WGRAD_STREAM, "wgrad_defer": Fn.WGRAD_DEFER}[sys.argv[2]]
+    sw = {"norm_pair": MG.FUSED_NORM_PAIR, "attn_ds": Kn.ATTN_DS, "wgrad_stream": Fn.WGRAD_STREAM, "wgrad_defer": Fn.WGRAD_DEFER,
+          "side_cap": Fn.SIDE_CU_RESERVE}[sys.argv[2]]
     gs, ws = {}, {}
     for r in range(int(sys.argv[3]) if len(sys.argv) > 3 else 5):
         for mode in (0, 1):
-            sw[0] = bool(mode)
+            # side_cap: 0 vs SVLA_SIDE_CU_RESERVE_AB CUs reserved for the main stream
+            sw[0] = (int(os.environ.get("SVLA_SIDE_CU_RESERVE_AB", "32")) * mode) if sys.argv[2] == "side_cap" \
+                else bool(mode)
             (f, t), gx = run(True)
             gs[mode] = gx
             ws[mode] = flat_g.clone()
