@@ -71,8 +71,9 @@ WGRAD_STREAM = [os.environ.get("SVLA_WGRAD_STREAM", "1") != "0"]
 # num_cus - reserve, svla_gemm_set_cu_cap); 0 = they may take every CU.  Without it a persistent weight-gradient grid
 # holds every CU until it is done and the main stream's next kernel (the norm-pair backward, 69 us alone) waits
 # ~600 us for a CU (profiles/r7a_block_breakdown.txt).  8: step 216.4-216.8 -> 214.3-214.4 ms, block 4.65-4.67 ->
-# 4.61 ms (16: the same within noise; profiles/r8q_side_cu_reserve_ab.txt)
-SIDE_CU_RESERVE = [int(os.environ.get("SVLA_SIDE_CU_RESERVE", "8"))]
+# 4.61 ms (16: the same within noise); 4: 214.1-214.3 (8) -> 212.4-212.8 ms, 2: 212.9-213.0 (profiles/
+# r8q_side_cu_reserve_ab.txt); a CU reserve for the Zoe forward beside SigLIP (64, 128) measured no gain
+SIDE_CU_RESERVE = [int(os.environ.get("SVLA_SIDE_CU_RESERVE", "4"))]
 WGRAD_DEFER = [os.environ.get("SVLA_WGRAD_DEFER", "1") != "0"]
 _side_streams: dict = {}
 _join_queued: dict = {}  # device -> main stream the end-of-backward callback will make wait

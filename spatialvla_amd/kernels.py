@@ -233,6 +233,11 @@ def check_decode_mlp_timeouts(what: str = "decode"):
                            "Set SVLA_DECODE_MLP_PERSIST=0 for the two-launch path.")
 
 
+def gemm_cu_cap(cap: int):
+    """svla_gemm_set_cu_cap: cap the persistent stream-K grid of this thread's next GEMM launches (0 = off)."""
+    L.lib().svla_gemm_set_cu_cap(max(0, int(cap)))
+
+
 _DECODE_MLP_GRID = {}
 
 
