@@ -27,6 +27,9 @@ from . import zoe_fast
 
 # the Zoe depth + Ego3D encoding of the training forward on the side stream beside SigLIP (SVLA_ZOE_STREAM=0: serial)
 ZOE_STREAM = [os.environ.get("SVLA_ZOE_STREAM", "1") != "0"]
+# ... also inside the captured B=1 prefill graph (two branches of the graph): prefill + first token 15.3 -> 12.6 ms,
+# configs[1] (prompt -> 4 tokens) 20.9 -> 18.2 ms (profiles/r8y_prefill_zoe_branch_ab.txt)
+ZOE_STREAM_CAPTURE = [os.environ.get("SVLA_ZOE_STREAM_CAPTURE", "1") != "0"]
 from . import kernels as K
 from .configuration_spatialvla import SpatialVLAConfig
 from .modeling_gemma2 import Gemma2ForCausalLM, Gemma2KVCache, KVMask
@@ -290,10 +293,13 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
         K.affine(pv, 1.0 / SIGLIP_STD[0], -SIGLIP_MEAN[0], sig_in)  # TF.normalize (:309)
         B = pv.shape[0]
         enc = None
+        capturing = pv.is_cuda and torch.cuda.is_current_stream_capturing()
         if self.config.use_vision_zoe and depth is None and ZOE_STREAM[0] and pv.is_cuda and \
-                not torch.cuda.is_current_stream_capturing():
+                (not capturing or ZOE_STREAM_CAPTURE[0]) and \
+                Fn.side_stream(pv.device) != torch.cuda.current_stream(pv.device):
             # the frozen Zoe estimator and the Ego3D encoding (no autograd) on the side stream, beside the SigLIP
-            # tower: two independent networks, each filling the CUs the other's kernel tails leave idle
+            # tower: two independent networks, each filling the CUs the other's kernel tails leave idle (also inside
+            # the captured B=1 prefill graph: a fork / join of two branches)
             main = torch.cuda.current_stream(pv.device)
             side = Fn.side_stream(pv.device)
             side.wait_stream(main)
@@ -301,7 +307,8 @@ class SpatialVLAForConditionalGeneration(SpatialVLAPreTrainedModel, GenerationMi
                 enc = self.ego3d_features(intrinsic, self.predict_depth(pixel_values.to(dt)), kinv)
             feats = self.vision_tower(sig_in)                       # [B, np, Hv]
             main.wait_stream(side)
-            enc.record_stream(main)  # allocated on the side stream, read (and saved for backward) on this one
+            if not capturing:  # (a captured graph's pool keeps its buffers alive for every replay)
+                enc.record_stream(main)  # allocated on the side stream, read (and saved for backward) on this one
         else:
             feats = self.vision_tower(sig_in)                       # [B, np, Hv]
         Hv = feats.shape[-1]
