@@ -50,9 +50,12 @@ constexpr int BK = 64;
 constexpr int GROUP_M = 8;
 constexpr uint32_t OOB = 0x80000000u;  // voffset beyond num_records -> returns zeros
 
-template <int BM_, int BN_, int WGM_, int WGN_>
+// NST_: LDS stages of the k-loop.  2 = double buffering (one k-tile in flight while the other is read); more stages
+// keep NST-1 k-tiles in flight, for grids whose blocks are few and whose k-loops are latency-bound (the B = 1
+// prefill: a 64x64 tile's k-tile is ~64 MFMA cycles per wave against a ~1.3k-cycle load round trip).
+template <int BM_, int BN_, int WGM_, int WGN_, int NST_ = 2>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_;
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, NST = NST_;
   static constexpr int NW = WGM * WGN, NTH = 64 * NW;
   static constexpr int WTM = BM / WGM, WTN = BN / WGN;
   static constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -61,7 +64,8 @@ struct Cfg {
   static constexpr int IA = BM / (8 * NW), IB = BN / (8 * NW);  // LDS-DMA instructions per wave per k-tile
   static constexpr int EPI_ROWS = 64, EPI_LD = BN + 4;
   static constexpr int EPI_BYTES = EPI_ROWS * EPI_LD * 4;
-  static constexpr int LDS = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  static constexpr int LDS = (NST * STAGE > EPI_BYTES) ? NST * STAGE : EPI_BYTES;
+  static_assert(NST >= 2 && LDS <= 160 * 1024, "stages must fit the 160 KiB of LDS");
   static_assert(EPI_BYTES + TANH_TAB_BYTES <= LDS, "epilogue image + tanh table must fit");
   static_assert(IA >= 1 && IB >= 1, "tile too small for the wave count");
 };
@@ -69,6 +73,10 @@ using CfgBig = Cfg<256, 256, 2, 4>;
 using CfgMid = Cfg<256, 128, 4, 2>;
 using CfgSmall = Cfg<128, 128, 2, 2>;
 using CfgTiny = Cfg<64, 64, 2, 2>;  // sub-wave grids of the B = 1 prefill (4x the blocks of 128x128)
+// deep-pipelined small tiles for the short-M GEMMs of the B = 1 prefill (launch_deep)
+using CfgTinyD = Cfg<64, 64, 2, 2, 8>;
+using CfgNarrowD = Cfg<64, 128, 2, 2, 6>;
+using CfgSmallD = Cfg<128, 128, 2, 2, 4>;
 
 // RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
@@ -707,21 +715,56 @@ __device__ __forceinline__ void tile_epilogue(int64_t M, int64_t N, int64_t m0, 
 }
 
 
+// s_waitcnt vmcnt(NLD * later) for a wave-uniform later in [0, KMAX] (the count is an immediate)
+template <int NLD, int KMAX>
+__device__ __forceinline__ void vm_wait_upto(int later) {
+  if constexpr (KMAX == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    static_assert(NLD * KMAX <= 63, "vmcnt field");
+    if (later >= KMAX) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD * KMAX) : "memory");
+    else vm_wait_upto<NLD, KMAX - 1>(later);
+  }
+}
+
+// Split-K of the deep-pipelined instances (S > 1): block (tile, split) runs k-tiles [split*nk/S, (split+1)*nk/S) of
+// its tile, stores its fp32 accumulators to slab tile*S + split and adds one to the tile's arrival counter; the
+// block whose add completes the count sums the S slabs in split order (the same order whichever block is last)
+// and runs the epilogue.  No block waits for another.  slabs / counters: the caller's stream-K workspace
+// (counters zero between launches: the reducer resets its tile's).
+struct SplitArgs {
+  int S;
+  float* slabs;
+  int* counters;
+};
+
 template <typename C, int LA, int LB>
 __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, int64_t K, svla_operand A,
-                                                          svla_operand B, CDesc Cd, svla_epilogue E) {
+                                                          svla_operand B, CDesc Cd, svla_epilogue E, SplitArgs sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int sflag;
   constexpr int BM = C::BM, BN = C::BN, NTH = C::NTH, TM = C::TM, TN = C::TN;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
   const int total = tiles_m * tiles_n;
-  const int pid = xcd_remap(blockIdx.x, total);
-  const int group = GROUP_M * tiles_n;
-  const int first_m = (pid / group) * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (pid % group) % gsz;
-  const int tn = (pid % group) / gsz;
+  int tm, tn, split = 0;
+  if (C::NST > 2 && sp.S > 1) {
+    // the M tiles of one (split, column tile) are consecutive ids, so they share an XCD and its L2 copy of the weight
+    // slice
+    const int L = xcd_remap(blockIdx.x, total * sp.S);
+    split = L / total;
+    const int tile = L % total;
+    tm = tile % tiles_m;
+    tn = tile / tiles_m;
+  } else {
+    const int pid = xcd_remap(blockIdx.x, total);
+    const int group = GROUP_M * tiles_n;
+    const int first_m = (pid / group) * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    tm = first_m + (pid % group) % gsz;
+    tn = (pid % group) / gsz;
+  }
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
   const int wr = w / C::WGN, wc = w % C::WGN;
@@ -741,19 +784,10 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
   op_setup<LB, BN, C::IB>(B, n0, rvB, w, lane, sb);
 
   constexpr int NLD = C::IA + C::IB;  // LDS-DMA instructions per lane per k-tile
-  const int nk = (int)((K + BK - 1) / BK);
-  op_issue<LA, BM, C::IA>(A, sa, m0, 0, kvA, smem, w);
-  op_issue<LB, BN, C::IB>(B, sb, n0, 0, kvB, smem + C::A_BYTES, w);
-  if (nk > 1) {
-    op_issue<LA, BM, C::IA>(A, sa, m0, BK, kvA, smem + C::STAGE, w);
-    op_issue<LB, BN, C::IB>(B, sb, n0, BK, kvB, smem + C::STAGE + C::A_BYTES, w);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const char* la = smem + cur * C::STAGE;
+  const int nk_all = (int)((K + BK - 1) / BK);
+  const int kb = (C::NST > 2 && sp.S > 1) ? (int)((int64_t)split * nk_all / sp.S) : 0;
+  const int nk = (C::NST > 2 && sp.S > 1) ? (int)((int64_t)(split + 1) * nk_all / sp.S) - kb : nk_all;
+  auto mfma_stage = [&](const char* la) {
     const char* lb = la + C::A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -767,12 +801,94 @@ __global__ __launch_bounds__(C::NTH, 1) void gemm_kernel(int64_t M, int64_t N, i
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+  if constexpr (C::NST > 2) {
+    // ring of NST stages, NST-1 k-tiles in flight: k-tile kt waits only for itself (vmcnt counts the later stages'
+    // DMAs still allowed outstanding), one barrier a k-tile publishes every wave's DMA of kt and retires every
+    // wave's reads of kt-1, whose slot then takes k-tile kt+NST-1
+    constexpr int NST = C::NST;
+#pragma unroll
+    for (int st = 0; st < NST - 1; ++st)
+      if (st < nk) {
+        op_issue<LA, BM, C::IA>(A, sa, m0, (int64_t)(kb + st) * BK, kvA, smem + st * C::STAGE, w);
+        op_issue<LB, BN, C::IB>(B, sb, n0, (int64_t)(kb + st) * BK, kvB, smem + st * C::STAGE + C::A_BYTES, w);
+      }
+#pragma unroll 1
+    for (int kt = 0; kt < nk; ++kt) {
+      vm_wait_upto<NLD, NST - 2>(min(NST - 2, nk - 1 - kt));
+      __builtin_amdgcn_s_barrier();
+      const int kn = kt + NST - 1;
+      if (kn < nk) {
+        char* dst = smem + (kn % NST) * C::STAGE;
+        op_issue<LA, BM, C::IA>(A, sa, m0, (int64_t)(kb + kn) * BK, kvA, dst, w);
+        op_issue<LB, BN, C::IB>(B, sb, n0, (int64_t)(kb + kn) * BK, kvB, dst + C::A_BYTES, w);
+      }
+      mfma_stage(smem + (kt % NST) * C::STAGE);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the epilogue image reuses the stage memory
+    if (sp.S > 1) {
+      // hand-off as the stream-K kernels': slabs stored / loaded sc1 (write-through, L1 bypass), every wave drains
+      // vmcnt before the barrier, one lane counts the arrival (cdna_hip_programming.md G16 R1)
+      const int tile = tm + tn * tiles_m;
+      constexpr int SLAB = TM * TN * NTH * 16;  // bytes
+      const char* base = reinterpret_cast<const char*>(sp.slabs) + (int64_t)tile * sp.S * SLAB;
+      {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)split * SLAB);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                   (uint32_t)((t + (i * TN + j) * NTH) * 16), 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        int* cnt = sp.counters + tile;
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sflag = (old == sp.S - 1);
+        if (old == sp.S - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!sflag) return;  // block-uniform: another block reduces this tile
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads stay below
+#pragma unroll 1
+      for (int sg = 0; sg < sp.S; ++sg) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)sg * SLAB);
+        f32x4 x[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            x[i][j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((t + (i * TN + j) * NTH) * 16), 0, 16));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = sg == 0 ? x[i][j] : acc[i][j] + x[i][j];
+      }
+    }
+  } else {
+  op_issue<LA, BM, C::IA>(A, sa, m0, 0, kvA, smem, w);
+  op_issue<LB, BN, C::IB>(B, sb, n0, 0, kvB, smem + C::A_BYTES, w);
+  if (nk > 1) {
+    op_issue<LA, BM, C::IA>(A, sa, m0, BK, kvA, smem + C::STAGE, w);
+    op_issue<LB, BN, C::IB>(B, sb, n0, BK, kvB, smem + C::STAGE + C::A_BYTES, w);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NLD) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    mfma_stage(smem + cur * C::STAGE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + 2 < nk) {
       op_issue<LA, BM, C::IA>(A, sa, m0, (int64_t)(kt + 2) * BK, kvA, smem + cur * C::STAGE, w);
       op_issue<LB, BN, C::IB>(B, sb, n0, (int64_t)(kt + 2) * BK, kvB, smem + cur * C::STAGE + C::A_BYTES, w);
     }
+  }
   }
 
   auto wp = [&](int pass, float* Ei) {
@@ -2448,14 +2564,14 @@ void set_lds_once(int bytes) {
 
 template <typename C>
 int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
-           const svla_epilogue& E, hipStream_t s) {
+           const svla_epilogue& E, hipStream_t s, SplitArgs sp = SplitArgs{1, nullptr, nullptr}) {
   const int64_t tiles = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
-  dim3 grid((unsigned)tiles), block(C::NTH);
+  dim3 grid((unsigned)(tiles * sp.S)), block(C::NTH);
   const int la = A.layout, lb = B.layout;
 #define SVLA_LAUNCH(LA_, LB_)                                                                      \
   {                                                                                                \
     set_lds_once<gemm_kernel<C, LA_, LB_>>(C::LDS);                                                \
-    hipLaunchKernelGGL((gemm_kernel<C, LA_, LB_>), grid, block, C::LDS, s, M, N, K, A, B, Cd, E);  \
+    hipLaunchKernelGGL((gemm_kernel<C, LA_, LB_>), grid, block, C::LDS, s, M, N, K, A, B, Cd, E, sp);  \
   }
   if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_KC) SVLA_LAUNCH(0, 0)
   else if (la == SVLA_LAYOUT_KC && lb == SVLA_LAYOUT_RC) SVLA_LAUNCH(0, 1)
@@ -2463,6 +2579,26 @@ int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_op
   else SVLA_LAUNCH(1, 1)
 #undef SVLA_LAUNCH
   return svla::check_launch("gemm");
+}
+
+__global__ void rope_inplace_kernel(int64_t M, bf16_t* __restrict__ c, int64_t ldc, svla_epilogue E);
+
+// The deep-pipelined small-tile instances.  A head-wide RoPE (the partner column D/2 away in another tile) runs as
+// the plain product followed by rope_inplace_kernel, which rounds as the epilogue does (bitwise).
+template <typename C>
+int launch_deep(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
+                const svla_epilogue& E, hipStream_t s, SplitArgs sp = SplitArgs{1, nullptr, nullptr}) {
+  if (E.kind == SVLA_EPI_ROPE && E.rope_D > C::BN) {
+    svla_epilogue E0 = E;
+    E0.kind = SVLA_EPI_STORE;
+    const int rc = launch<C>(M, N, K, A, B, Cd, E0, s, sp);
+    if (rc != 0) return rc;
+    const int64_t work = M * (E.rope_cols / E.rope_D) * (E.rope_D / 16);
+    hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, M, Cd.ptr[0], Cd.ld,
+                       E);
+    return svla::check_launch("gemm (rope pass)");
+  }
+  return launch<C>(M, N, K, A, B, Cd, E, s, sp);
 }
 
 // In-place rotate_half RoPE over the first rope_cols columns of a bf16 [M][ldc] matrix (heads of rope_D
@@ -3079,6 +3215,25 @@ int grid_cus() {
 // 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
 size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }
 
+// Split-K factor of a deep-pipelined small-tile GEMM: as many splits as keep the grid within one wave of blocks
+// (G / tiles), at least 4 k-tiles a split, at most 16; the slabs and the per-tile counters must fit the stream-K
+// workspace's layout (slab region of 2G 256 KiB slabs, 2G counters behind it).  S = 1: no split.
+template <typename C>
+SplitArgs split_args(int64_t M, int64_t N, int64_t K, const GemmCtx& ctx) {
+  const int G = grid_cus();
+  const int64_t tiles = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
+  const int64_t nk = (K + BK - 1) / BK;
+  int64_t S = tiles < G ? G / tiles : 1;
+  S = std::min<int64_t>(S, std::min<int64_t>(nk / 4, 16));
+  constexpr int64_t SLAB = (int64_t)C::TM * C::TN * C::NTH * 16;
+  const int64_t slab_region = (int64_t)2 * num_cus() * 32 * p8::NTH * 16;
+  if (S < 2 || !ctx.ws || ctx.ws_bytes < sk_workspace_bytes(num_cus()) || tiles > 2 * num_cus() ||
+      tiles * S * SLAB > slab_region)
+    return SplitArgs{1, nullptr, nullptr};
+  return SplitArgs{(int)S, reinterpret_cast<float*>(ctx.ws),
+                   reinterpret_cast<int*>(reinterpret_cast<char*>(ctx.ws) + slab_region)};
+}
+
 int launch8(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
             const svla_epilogue& E, const GemmCtx& ctx, hipStream_t s) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
@@ -3316,7 +3471,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
                                  void* stream) {
-  SVLA_CHECK_ARG(variant >= 0 && variant <= 9, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 15, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   SVLA_CHECK_ARG(!epi || !epi->mx_q, "gemm: the MX copy of C (epi->mx_q) is an fp8-GEMM output only");
   GemmCtx ctx;
@@ -3500,6 +3655,48 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   const bool light_epi = ek == SVLA_EPI_STORE || ek == SVLA_EPI_BIAS || ek == SVLA_EPI_GEGLU || ek == SVLA_EPI_ROPE;
   const bool use4 = !kseg && seg_ok(256, 256) &&
                     (variant == 3 || ((variant == 0 || variant >= 5) && light_epi && K >= 384 && 4 * t256 >= num_cus()));
+  // forced deep-pipelined small tiles (tools/gemma_prefill_gemm_bench.py A/B): KC x KC, no k segments, whole
+  // 64-column GeGLU halves
+  if (variant >= 10 && A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && !kseg &&
+      ek != SVLA_EPI_SOFTCAP_CE && !(ek == SVLA_EPI_GEGLU && epi->mx_q)) {
+    const int cv = variant >= 13 ? variant - 3 : variant;
+    const bool split = variant >= 13;
+    if (cv == 10 && seg_ok(64, 64))
+      return launch_deep<CfgTinyD>(M, N, K, *A, *B, C, *epi, s, split ? split_args<CfgTinyD>(M, N, K, ctx) : SplitArgs{1, nullptr, nullptr});
+    if (cv == 11 && seg_ok(64, 128))
+      return launch_deep<CfgNarrowD>(M, N, K, *A, *B, C, *epi, s, split ? split_args<CfgNarrowD>(M, N, K, ctx) : SplitArgs{1, nullptr, nullptr});
+    if (cv == 12 && seg_ok(128, 128))
+      return launch_deep<CfgSmallD>(M, N, K, *A, *B, C, *epi, s, split ? split_args<CfgSmallD>(M, N, K, ctx) : SplitArgs{1, nullptr, nullptr});
+  }
+  // Short-M grids (the B = 1 prefill: Gemma2 at 299 prompt tokens, SigLIP at 256, BEiT at 577 patches): a block's
+  // k-loop there is bound by what one CU can pull into LDS (~50-70 GB/s a CU, MI355X_MICROARCH.md ldsdma-fill /
+  // ring-gemm), so the tile and split-K factor are the ones with the fewest bytes per block per wave of blocks:
+  // operand fill (BM + BN) x k per k-tile, plus for a split tile its slab store and the reducer's S slab reads
+  // (weighted 2x: latency-bound single-block reads).  The 256 x 256 data-parallel estimate stands for the 4-wave /
+  // 8-phase path, which keeps ties (gate|up GeGLU at 299 rows: 55.7 vs 62.3 us).  Measured per shape in
+  // profiles/r8z_prefill_split_ab.txt: Gemma2 q|k|v+RoPE 68.6 -> 26.9 us, down 68.6 -> 38.5, SigLIP fc2 34.1 ->
+  // 18.2, BEiT fc2 33.2 -> 22.0.
+  if (variant == 0 && M <= 1024 && A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && !kseg &&
+      ek != SVLA_EPI_SOFTCAP_CE && !(ek == SVLA_EPI_GEGLU && epi->mx_q)) {
+    const int G = grid_cus();
+    auto est = [&](int bm, int bn, int S) {
+      const double waves = (double)((tiles(bm, bn) * S + G - 1) / G);
+      const double fill = (double)nk / S * BK * (bm + bn) * 2;
+      return waves * (fill + (S > 1 ? (double)bm * bn * 4 * (1 + 2 * S) : 0.0));
+    };
+    const SplitArgs s64 = split_args<CfgTinyD>(M, N, K, ctx), s64n = split_args<CfgNarrowD>(M, N, K, ctx),
+                    s128 = split_args<CfgSmallD>(M, N, K, ctx);
+    const double e64 = seg_ok(64, 64) ? est(64, 64, s64.S) : 1e30;
+    const double e64n = seg_ok(64, 128) ? est(64, 128, s64n.S) : 1e30;
+    const double e128 = seg_ok(128, 128) ? est(128, 128, s128.S) : 1e30;
+    const double ebig = seg_ok(256, 256) ? est(256, 256, 1) : 1e30;
+    const double best = std::min(e64, std::min(e64n, e128));
+    if (best < ebig) {
+      if (best == e64n) return launch_deep<CfgNarrowD>(M, N, K, *A, *B, C, *epi, s, s64n);
+      if (best == e64) return launch_deep<CfgTinyD>(M, N, K, *A, *B, C, *epi, s, s64);
+      return launch_deep<CfgSmallD>(M, N, K, *A, *B, C, *epi, s, s128);
+    }
+  }
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile
     SVLA_CHECK_ARG(seg_ok(256, 256), "gemm: ROPE with head_dim > 128 needs 256-aligned segments");
     if (use4) return launch4(M, N, K, *A, *B, C, *epi, ctx, s);

@@ -38,6 +38,19 @@ def _batches(device):
 
 def _run(rank, world, device):
     from spatialvla_amd.engine import TrainEngine
+    from spatialvla_amd import kernels as Kn
+    # GEMMs without split-K / stream-K (variant 2): every output element sums k in the same order whatever the
+    # per-rank batch, so the comparison isolates the ZeRO-1 exchange; under the default dispatch the short-M split-K
+    # picks its split factor from the row count (2 vs 4 episodes), which reorders the fp32 sums of the tiny model's
+    # GEMMs and AdamW turns its noise-level gradients (layer-0 norm biases) into full steps
+    v0, Kn.gemm_variant = Kn.gemm_variant, 2
+    try:
+        return _run_fixed_k_order(rank, world, device, TrainEngine)
+    finally:
+        Kn.gemm_variant = v0
+
+
+def _run_fixed_k_order(rank, world, device, TrainEngine):
     model = H.build_hip_model(H.cfg_dict("tiny"), device)
     depth = torch.rand(B_TOTAL, 1, 224, 224, generator=torch.Generator().manual_seed(9)).mul(3).add(0.5).to(device)
     per = B_TOTAL // world

@@ -1185,3 +1185,79 @@ def test_gemm4_192_row_tiles(cuda, lay):
     big3 = torch.empty_like(big)
     Kn.gemm(M + 64, N, K, Kn._operand([a], L.LAYOUT_KC), B, [big3], [0], N, Kn._epi(L.EPI_BIAS, bias=bias))
     assert torch.equal(c3, big3[:M]) and rel_l2(c3, ref[:M] + bias.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(299, 2304, 9216), (256, 1152, 4304), (577, 1024, 4096), (37, 200, 1000),
+                                   (300, 200, 136), (299, 4304, 2304)])
+def test_gemm_deep_split(cuda, M, N, K):
+    """The deep-pipelined small tiles (variants 10-12: 64x64, 64x128, 128x128 with NST-stage LDS rings) and their
+    split-K forms (13-15: slabs + arrival counter, the last arriver sums the slabs in split order), and the short-M
+    auto dispatch (variant 0) against fp32: plain store with ragged N (the columns past N untouched), bias+residual,
+    GeGLU; the unsplit deep tiles bitwise the 128x128 data-parallel tiles (same k order); each split result
+    reproduced bitwise by a second call (deterministic reduction order, counters reset by the reducer) and after a
+    stream-K GEMM that shares the workspace's counters."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(71)
+    a, b = _r(M, K), _r(N, K, scale=0.05)
+    ref = a.float() @ b.float().T
+    A, B = Kn._operand([a], L.LAYOUT_KC), Kn._operand([b], L.LAYOUT_KC)
+    bias, res = _r(N + (-N) % 8, scale=0.5)[:N], _r(M, N + (-N) % 8)[:, :N]
+    base = torch.empty(M, N + (-N) % 8, dtype=BF, device=cuda)
+    Kn.gemm(M, N, K, A, B, [base[:, :N]], [0], base.stride(0), Kn._epi(), variant=1)
+    # a stream-K launch on the same workspace (4-wave kernel, 9984 x 2304 x 4096 k-tiles: split tiles + counters)
+    xs, ws_ = _r(2304, 4096), _r(2304, 4096, scale=0.05)
+    ys = torch.empty(2304, 2304, dtype=BF, device=cuda)
+    for v in (10, 11, 12, 13, 14, 15, 0):
+        c = torch.full((M, N + (-N) % 8), 7.0, dtype=BF, device=cuda)
+        Kn.gemm(M, N, K, A, B, [c[:, :N]], [0], c.stride(0), Kn._epi(), variant=v)
+        assert rel_l2(c[:, :N], ref) < 5e-3, v
+        assert bool((c[:, N:] == 7.0).all()), v
+        if v in (10, 11, 12):
+            assert torch.equal(c[:, :N], base[:, :N]), v
+        Kn.linear_fwd(xs, [ws_], ys)
+        c2 = torch.full_like(c, 7.0)
+        Kn.gemm(M, N, K, A, B, [c2[:, :N]], [0], c2.stride(0), Kn._epi(), variant=v)
+        assert torch.equal(c, c2), v
+        cb = torch.empty_like(c)
+        Kn.gemm(M, N, K, A, B, [cb[:, :N]], [0], cb.stride(0), Kn._epi(L.EPI_BIAS_RESID, bias=bias, in0=res),
+                variant=v)
+        assert rel_l2(cb[:, :N], ref + bias.float() + res.float()) < 5e-3, v
+    if N % 64 == 0:  # GeGLU: gate rows [0, N/2), up rows [N/2, N) of the tile halves
+        I = N // 2
+        wg, wu = b[:I], b[I:]
+        lut = _gelu_lut(cuda)
+        for v in (10, 11, 12, 13, 14, 15, 0):
+            h, g, u = (torch.empty(M, I, dtype=BF, device=cuda) for _ in range(3))
+            Kn.gemm_variant = v
+            try:
+                Kn.linear_geglu_fwd(a, wg, wu, h, g, u)
+            finally:
+                Kn.gemm_variant = 0
+            assert rel_l2(g, ref[:, :I]) < 5e-3 and rel_l2(u, ref[:, I:]) < 5e-3, v
+            assert torch.equal(h, (_apply_lut(lut, g).float() * u.float()).to(BF)), v
+
+
+def test_gemm_deep_rope_pass_bitwise(cuda):
+    """q|k|v + head_dim-256 RoPE at 299 rows on the 64x128 deep tiles (variant 11: product, then the in-place rope
+    pass) == the 4-wave kernel's RoPE epilogue (variant 3), bit for bit; split-K (14) and the auto dispatch within
+    fp32 reordering."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(73)
+    M, Kd, L_ = 299, 2304, 299
+    x = _r(M, Kd)
+    ws = [_r(2048, Kd, scale=0.05), _r(1024, Kd, scale=0.05), _r(1024, Kd, scale=0.05)]
+    pos = torch.arange(L_, device=cuda).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, 256, 2, device=cuda).float() / 256))
+    fr = pos[:, None] * inv[None]
+    cos, sin = fr.cos().to(BF).contiguous(), fr.sin().to(BF).contiguous()
+    outs = {}
+    for v in (3, 11, 14, 0):
+        o = torch.empty(M, 4096, dtype=BF, device=cuda)
+        try:
+            Kn.gemm_variant = v
+            Kn.linear_fwd(x, ws, o, kind=L.EPI_ROPE, rope=(cos, sin, L_, 256, 3072))
+        finally:
+            Kn.gemm_variant = 0
+        outs[v] = o
+    assert torch.equal(outs[3], outs[11])
+    assert rel_l2(outs[14], outs[3]) < 2e-3 and rel_l2(outs[0], outs[3]) < 2e-3
