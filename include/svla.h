@@ -107,9 +107,10 @@ typedef struct {
  * Requirements: ld of every operand and of C a multiple of 8 elements; pointers 16-B aligned; the
  * reduction extent of a KC operand (k_valid, default K) a multiple of 8 (zero-pad: e.g. the lm_head
  * dlogits rows are zero beyond V up to their padded ld). */
-/* workspace: caller-owned stream-K workspace of the 256x256 kernels (256-B aligned, zero-filled once before its
- * first use, at least svla_gemm_workspace_bytes() for the current device; the kernels leave it zeroed).  NULL =
- * every output tile runs whole.  GEMMs that run concurrently (other streams, other threads) must use distinct
+/* workspace: caller-owned stream-K / split-K workspace (fp32 partial slabs + arrival counters of the 256x256
+ * kernels' stream-K and of the short-M split-K tiles; 256-B aligned, zero-filled once before its first use, at
+ * least svla_gemm_workspace_bytes() for the current device; the kernels leave the counters zeroed).  NULL = every
+ * output tile runs whole.  GEMMs that run concurrently (other streams, other threads) must use distinct
  * workspaces; nothing else is shared between calls, so the entry point is re-entrant. */
 int svla_gemm_bf16(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                    void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
@@ -122,7 +123,9 @@ size_t svla_gemm_workspace_bytes(void);
 /* svla_gemm_bf16 with an explicit kernel choice (tests / tuning tools, not a reference interface): 0 = auto (as
  * svla_gemm_bf16), 1 = two-barrier tiles, 2 = 8-phase without stream-K, 3 = 4-wave kernel for every 256x256 case,
  * 4 = never the 4-wave kernel, 5 = auto without the small-M GEMV path, 6 = small-M GEMVs without the prefetching
- * kernel, 7 = the prefetching GEMV with two rows per wave. */
+ * kernel, 7 = the prefetching GEMV with two rows per wave, 8 = 8-phase + stream-K for every sub-wave grid, 9 = the
+ * 64x64 two-stage tiles for sub-wave grids, 10 / 11 / 12 / 16 = the deep-pipelined 64x64 / 64x128 / 128x128 /
+ * 128x256 tiles (both operands KC), 13 / 14 / 15 / 17 = the same with split-K. */
 int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_operand* A, const svla_operand* B,
                       void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                       const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant, void* stream);

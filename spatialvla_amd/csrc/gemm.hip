@@ -77,6 +77,7 @@ using CfgTiny = Cfg<64, 64, 2, 2>;  // sub-wave grids of the B = 1 prefill (4x t
 using CfgTinyD = Cfg<64, 64, 2, 2, 8>;
 using CfgNarrowD = Cfg<64, 128, 2, 2, 6>;
 using CfgSmallD = Cfg<128, 128, 2, 2, 4>;
+using CfgWideD = Cfg<128, 256, 2, 2, 3>;
 
 // RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
@@ -3215,6 +3216,13 @@ int grid_cus() {
 // 2 slabs per block + one arrival counter per stream-K tile (at most 2G - 1 of them)
 size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (size_t)2 * G * sizeof(int); }
 
+#ifndef WIDE_DEEP
+// the 128 x 256 deep tiles (3 stages) among the short-M candidates: measured no faster than the 4-wave kernel on the
+// one shape the estimate gives them (gate|up GeGLU at 299 rows: 55.0 vs 53.4 us) and far slower where forced
+// elsewhere (profiles/r8z_prefill_split_ab.txt), so off; variants 16 / 17 keep them for A/B
+#define WIDE_DEEP 0
+#endif
+
 // Split-K factor of a deep-pipelined small-tile GEMM: as many splits as keep the grid within one wave of blocks
 // (G / tiles), at least 4 k-tiles a split, at most 16; the slabs and the per-tile counters must fit the stream-K
 // workspace's layout (slab region of 2G 256 KiB slabs, 2G counters behind it).  S = 1: no split.
@@ -3471,7 +3479,7 @@ extern "C" int svla_gemm_bf16_ex(int64_t M, int64_t N, int64_t K, const svla_ope
                                  void* const* c_ptr, const int64_t* c_seg_start, int32_t c_nseg, int64_t ldc,
                                  const svla_epilogue* epi, void* workspace, size_t ws_bytes, int32_t variant,
                                  void* stream) {
-  SVLA_CHECK_ARG(variant >= 0 && variant <= 15, "gemm: variant %d", variant);
+  SVLA_CHECK_ARG(variant >= 0 && variant <= 17, "gemm: variant %d", variant);
   SVLA_CHECK_ARG(workspace == nullptr || ((uintptr_t)workspace & 255) == 0, "gemm workspace must be 256-B aligned");
   SVLA_CHECK_ARG(!epi || !epi->mx_q, "gemm: the MX copy of C (epi->mx_q) is an fp8-GEMM output only");
   GemmCtx ctx;
@@ -3659,8 +3667,10 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   // 64-column GeGLU halves
   if (variant >= 10 && A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && !kseg &&
       ek != SVLA_EPI_SOFTCAP_CE && !(ek == SVLA_EPI_GEGLU && epi->mx_q)) {
-    const int cv = variant >= 13 ? variant - 3 : variant;
-    const bool split = variant >= 13;
+    const int cv = variant == 17 ? 16 : (variant >= 13 && variant <= 15 ? variant - 3 : variant);
+    const bool split = variant >= 13 && variant != 16;
+    if (cv == 16 && seg_ok(128, 256))
+      return launch_deep<CfgWideD>(M, N, K, *A, *B, C, *epi, s, split ? split_args<CfgWideD>(M, N, K, ctx) : SplitArgs{1, nullptr, nullptr});
     if (cv == 10 && seg_ok(64, 64))
       return launch_deep<CfgTinyD>(M, N, K, *A, *B, C, *epi, s, split ? split_args<CfgTinyD>(M, N, K, ctx) : SplitArgs{1, nullptr, nullptr});
     if (cv == 11 && seg_ok(64, 128))
@@ -3685,16 +3695,18 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
       return waves * (fill + (S > 1 ? (double)bm * bn * 4 * (1 + 2 * S) : 0.0));
     };
     const SplitArgs s64 = split_args<CfgTinyD>(M, N, K, ctx), s64n = split_args<CfgNarrowD>(M, N, K, ctx),
-                    s128 = split_args<CfgSmallD>(M, N, K, ctx);
+                    s128 = split_args<CfgSmallD>(M, N, K, ctx), s128w = split_args<CfgWideD>(M, N, K, ctx);
     const double e64 = seg_ok(64, 64) ? est(64, 64, s64.S) : 1e30;
     const double e64n = seg_ok(64, 128) ? est(64, 128, s64n.S) : 1e30;
     const double e128 = seg_ok(128, 128) ? est(128, 128, s128.S) : 1e30;
+    const double e128w = (WIDE_DEEP && seg_ok(128, 256)) ? est(128, 256, s128w.S) : 1e30;
     const double ebig = seg_ok(256, 256) ? est(256, 256, 1) : 1e30;
-    const double best = std::min(e64, std::min(e64n, e128));
+    const double best = std::min(std::min(e64, e64n), std::min(e128, e128w));
     if (best < ebig) {
       if (best == e64n) return launch_deep<CfgNarrowD>(M, N, K, *A, *B, C, *epi, s, s64n);
       if (best == e64) return launch_deep<CfgTinyD>(M, N, K, *A, *B, C, *epi, s, s64);
-      return launch_deep<CfgSmallD>(M, N, K, *A, *B, C, *epi, s, s128);
+      if (best == e128) return launch_deep<CfgSmallD>(M, N, K, *A, *B, C, *epi, s, s128);
+      return launch_deep<CfgWideD>(M, N, K, *A, *B, C, *epi, s, s128w);
     }
   }
   if (epi->kind == SVLA_EPI_ROPE && epi->rope_D > 128) {  // a head must fit one 256-wide tile

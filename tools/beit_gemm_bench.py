@@ -40,7 +40,7 @@ def main():
         if kind == L.EPI_BIAS_SCALE_RESID:
             kw.update(colscale=cs, in0=res)
         row = []
-        for v in (0, 1, 3, 8):
+        for v in [int(s) for s in os.environ.get("SVLA_VARIANTS", "0,1,3,8").split(",")]:
             K.gemm_variant = v
             try:
                 ms = timed(lambda: K.linear_fwd(x, [w], out, kind=kind, **kw))
