@@ -3210,6 +3210,9 @@ int grid_cus() {
 #ifndef G4_SKMIN_NK
 #define G4_SKMIN_NK 64  // fewest k-tiles per tile for the 4-wave kernel's stream-K schedule (launch4)
 #endif
+#ifndef G4_SKMIN_NK_SUB
+#define G4_SKMIN_NK_SUB 64  // the same floor for grids under 3/4 of a wave of tiles (diagnostic A/B)
+#endif
 #ifndef G8_SKMIN_NK
 #define G8_SKMIN_NK 0  // the same for the 8-phase kernel (launch8); 0 = no floor
 #endif
@@ -3345,7 +3348,8 @@ int launch4(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_o
   // 3-7 % faster for q|k|v fwd, o fwd / dgrad and down dgrad at 32-36 k-tiles and 34-37 % faster for sub-wave grids
   // (252 tiles at K = 2048, SigLIP o fwd); stream-K stays 3-19 % ahead from 64 k-tiles up: q|k|v dgrad, down fwd,
   // gate/up dgrad / wgrad, every weight gradient)
-  if (!G4_NOSK && sk.nk >= G4_SKMIN_NK && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
+  const int skmin_nk = tiles * 4 < 3 * G ? G4_SKMIN_NK_SUB : G4_SKMIN_NK;
+  if (!G4_NOSK && sk.nk >= skmin_nk && ctx.ws && ctx.ws_bytes >= need && sk_tiles > 0 && sk_tiles < 2 * G &&
       sk_tiles * sk.nk >= G4_SKMIN * G) {
     sk.dp_tiles = (int)(tiles - sk_tiles);
     sk.grid = G;
