@@ -38,6 +38,9 @@
 #ifndef SVLA_ATT_BPF
 #define SVLA_ATT_BPF 1  // key tiles of score bias (BEiT) in flight ahead of the tile being scored: 1 or 2 (2: 245-261 us)
 #endif
+#ifndef SVLA_ATT_SUBWAVE
+#define SVLA_ATT_SUBWAVE 1  // sub-wave forward grids take the variant with twice the workgroups (svla_attn_fwd)
+#endif
 #ifndef SVLA_ATT_QW256
 #define SVLA_ATT_QW256 1  // head_dim 256 forward: 1 = head pairs (NH 2), 16 queries per wave; 2 = one head, 32 per wave
 #endif
@@ -1045,11 +1048,17 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
   const bool cap = a->softcap > 0.f;
   bf16_t* o = (bf16_t*)out;
   SVLA_CHECK_ARG(!a->bias || a->D == 64, "attn_fwd: an additive bias is only supported with head_dim 64");
+  // sub-wave grids (the B = 1 prefill: Gemma2 at 299 prompt tokens, BEiT at 577, SigLIP at 256 patches): the
+  // variant with twice the workgroups (one head per workgroup / one 16-query sub-tile per wave) when the default
+  // one would leave most CUs idle
+  const int64_t qt2 = (a->L + 127) / 128, qt1 = (a->L + 63) / 64;
+  const bool subwave = SVLA_ATT_SUBWAVE && qt1 * (a->Hq / 2) * a->B < svla::num_cus();
   if (a->D == 256) {
     if (SVLA_ATT_QW256 == 2)
       return cap ? fwd_launch<256, 1, true, false, 2>(*a, o, ldo, lse, s)
                  : fwd_launch<256, 1, false, false, 2>(*a, o, ldo, lse, s);
-    if (pair) return cap ? fwd_launch<256, 2, true>(*a, o, ldo, lse, s) : fwd_launch<256, 2, false>(*a, o, ldo, lse, s);
+    if (pair && !subwave)
+      return cap ? fwd_launch<256, 2, true>(*a, o, ldo, lse, s) : fwd_launch<256, 2, false>(*a, o, ldo, lse, s);
     return cap ? fwd_launch<256, 1, true>(*a, o, ldo, lse, s) : fwd_launch<256, 1, false>(*a, o, ldo, lse, s);
   }
   if (a->D == 64) {  // BEiT: plain MHA with the additive relative position bias, nothing else
@@ -1058,10 +1067,13 @@ extern "C" int svla_attn_fwd(const svla_attn_args* a, void* out, int64_t ldo, fl
     if (a->bias) {
       SVLA_CHECK_ARG(a->bias_ld >= (a->L + 7) / 8 * 8 && a->bias_ld % 8 == 0 && ((uintptr_t)a->bias & 15) == 0,
                      "attn_fwd: bias rows must hold round8(L) keys (ld a multiple of 8), 16-B aligned");
+      if (qt2 * a->Hq * a->B < svla::num_cus() && SVLA_ATT_SUBWAVE) return fwd_launch<64, 1, false, true, 1>(*a, o, ldo, lse, s);
       return fwd_launch<64, 1, false, true, SVLA_ATT_QW>(*a, o, ldo, lse, s);
     }
     return fwd_launch<64, 1, false, false, SVLA_ATT_QW>(*a, o, ldo, lse, s);
   }
+  if (qt2 * a->Hq * a->B < svla::num_cus() && SVLA_ATT_SUBWAVE && !cap)
+    return fwd_launch<72, 1, false, false, 1>(*a, o, ldo, lse, s);
   return cap ? fwd_launch<72, 1, true, false, SVLA_ATT_QW>(*a, o, ldo, lse, s)
              : fwd_launch<72, 1, false, false, SVLA_ATT_QW>(*a, o, ldo, lse, s);
 }
