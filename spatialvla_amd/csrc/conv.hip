@@ -20,6 +20,10 @@
 
 namespace {
 
+#ifndef CONV_SMALL
+#define CONV_SMALL 1  // 64 x 64 tiles for sub-wave grids (diagnostic A/B: 0 = always 128 x 128)
+#endif
+
 constexpr int CBK = 64;
 constexpr uint32_t COOB = 0x80000000u;
 
@@ -52,6 +56,7 @@ struct CCfg {
 using ConvBig = CCfg<256, 128, 4, 2>;   // Cout >= 128: 8 waves, 64x64 per wave
 using ConvMid = CCfg<128, 128, 2, 2>;   // 4 waves, 64x64 per wave
 using ConvNarrow = CCfg<256, 32, 4, 1>; // Cout 32: 4 waves, 64x32 per wave
+using ConvSmall = CCfg<64, 64, 2, 2>;   // sub-wave grids (the B = 1 DPT neck): 4 waves, 32x32 per wave
 
 __device__ __forceinline__ bf16x8 relu8(bf16x8 v) {
   // relu on bf16 bit patterns: a negative bf16 is a negative int16, so max(x, 0) as packed int16 is relu
@@ -338,5 +343,9 @@ extern "C" int svla_conv2d_nhwc(const svla_conv_args* a, void* stream) {
   const bool pre = (a->flags & SVLA_CONV_PRE_RELU) != 0;
   if (k.N <= 32) return launch_conv<ConvNarrow>(k, pre, s);
   if (k.M >= (int64_t)256 * 256 && k.N >= 128) return launch_conv<ConvBig>(k, pre, s);
+  // a grid of 128 x 128 tiles under one wave of CUs (B = 1 prefill: the 12x12 .. 48x48 maps of the DPT neck): 4x the
+  // workgroups on 64 x 64 tiles, each k-tile half the bytes (a small block's k-loop is bound by its CU's intake)
+  const int64_t t128 = ((k.M + 127) / 128) * ((k.N + 127) / 128);
+  if (CONV_SMALL && t128 < svla::num_cus()) return launch_conv<ConvSmall>(k, pre, s);
   return launch_conv<ConvMid>(k, pre, s);
 }
