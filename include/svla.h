@@ -262,6 +262,13 @@ int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t
                          const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache, int64_t ldk,
                          int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0, void* stream);
 
+/* The prefill's form of svla_qkv_rope_append (same arguments and rounding): q AND k rotated in place in the projection
+ * rows (where the prompt's flash attention reads them), rotated k and plain v also written to cache rows p0+t -- one
+ * launch instead of a RoPE pass and two cache copies (model/modeling_gemma2.py:123-154, :387-395). */
+int svla_qkv_rope_fill(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                       const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache, int64_t ldk,
+                       int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0, void* stream);
+
 /* dq/dk/dv use the same in-place layout convention as q/k/v (ld_dq, ld_dk, ld_dv).
  * workspace: B*Hq*L fp32 (row dot(dO, O), formed by the dQ kernel and read by the dK/dV kernel). */
 int svla_attn_bwd(const svla_attn_args* a, const void* out, int64_t ldo, const void* dout, int64_t lddo,

@@ -100,6 +100,8 @@ SIGNATURES = {
                                       ctypes.c_size_t, c_vp]),
     "svla_qkv_rope_append": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                                      c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
+    "svla_qkv_rope_fill": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                   c_i64, c_vp, c_i64, c_i64, c_i32, c_vp]),
     "svla_add_rmsnorm2_fwd": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp]),
     "svla_add_rmsnorm2_fwd_train": (c_i32, [c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp,
                                             c_vp]),

@@ -431,6 +431,9 @@ size_t fused_cnt_bytes(int64_t B, int64_t Lq, int64_t Hkv) {
 // RoPE on q (in place) and k, k written rotated and v copied into cache rows p0 + t.  Same rounding as the
 // GEMM's ROPE epilogue: out = bf16(bf16(x*cos) + bf16(rotate_half(x)*sin)) (modeling_gemma2.py:123-154).
 // One thread owns 8 columns of the low half of a head and their partners D/2 away (q/k), or 16 v columns.
+// KBACK (the prefill, svla_qkv_rope_fill): the rotated k is also written back into the projection rows, where the
+// prompt's flash attention reads it.
+template <bool KBACK>
 __global__ void qkv_rope_append_kernel(int B, int Lq, int Hq, int Hkv, int D, bf16_t* __restrict__ qkv, int64_t ld,
                                        const bf16_t* __restrict__ cos_t, const bf16_t* __restrict__ sin_t,
                                        int64_t rope_ld, bf16_t* __restrict__ kc, int64_t ldk, int64_t bsk,
@@ -458,10 +461,11 @@ __global__ void qkv_rope_append_kernel(int B, int Lq, int Hq, int Hkv, int D, bf
       ol[j] = round_bf(xl[j] * cs[j]) + round_bf(-xh[j] * sn[j]);
       oh[j] = round_bf(xh[j] * cs[j]) + round_bf(xl[j] * sn[j]);
     }
-    if (head < Hq) {  // q stays in the projection output for the attention kernel
+    if (head < Hq || KBACK) {  // q stays in the projection output for the attention kernel
       *reinterpret_cast<u32x4*>(lo) = pack8(ol);
       *reinterpret_cast<u32x4*>(hi) = pack8(oh);
-    } else {
+    }
+    if (head >= Hq) {
       bf16_t* kr = kc + (int64_t)b * bsk + (int64_t)(p0 + t) * ldk + (int64_t)(head - Hq) * D + dd;
       *reinterpret_cast<u32x4*>(kr) = pack8(ol);
       *reinterpret_cast<u32x4*>(kr + half) = pack8(oh);
@@ -557,10 +561,11 @@ extern "C" int svla_attn_decode_rope(const svla_attn_decode_args* a, const void*
   }
 }
 
-extern "C" int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
-                                    const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache,
-                                    int64_t ldk, int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0,
-                                    void* stream) {
+namespace {
+template <bool KBACK>
+int qkv_rope_append_impl(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                         const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache, int64_t ldk,
+                         int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0, void* stream) {
   SVLA_CHECK_ARG(qkv && rope_cos && rope_sin && k_cache && v_cache, "qkv_rope_append: NULL pointer");
   SVLA_CHECK_ARG(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && p0 >= 0, "qkv_rope_append: bad sizes");
   SVLA_CHECK_ARG(D % 16 == 0 && D <= 256, "qkv_rope_append: head_dim must be a multiple of 16, <= 256");
@@ -571,8 +576,25 @@ extern "C" int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t H
                    (uintptr_t)rope_sin) & 15) == 0, "qkv_rope_append: pointers must be 16-B aligned");
   const int64_t per_row = (int64_t)(Hq + Hkv) * (D / 16) + (int64_t)Hkv * D / 16;
   const int64_t work = (int64_t)B * Lq * per_row;
-  hipLaunchKernelGGL(qkv_rope_append_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     B, Lq, Hq, Hkv, D, (bf16_t*)qkv, ld, (const bf16_t*)rope_cos, (const bf16_t*)rope_sin, rope_ld,
-                     (bf16_t*)k_cache, ldk, bsk, (bf16_t*)v_cache, ldv, bsv, p0);
+  hipLaunchKernelGGL(qkv_rope_append_kernel<KBACK>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, B, Lq, Hq, Hkv, D, (bf16_t*)qkv, ld, (const bf16_t*)rope_cos,
+                     (const bf16_t*)rope_sin, rope_ld, (bf16_t*)k_cache, ldk, bsk, (bf16_t*)v_cache, ldv, bsv, p0);
   return svla::check_launch("qkv_rope_append");
+}
+}  // namespace
+
+extern "C" int svla_qkv_rope_append(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                                    const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache,
+                                    int64_t ldk, int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0,
+                                    void* stream) {
+  return qkv_rope_append_impl<false>(B, Lq, Hq, Hkv, D, qkv, ld, rope_cos, rope_sin, rope_ld, k_cache, ldk, bsk,
+                                     v_cache, ldv, bsv, p0, stream);
+}
+
+extern "C" int svla_qkv_rope_fill(int32_t B, int32_t Lq, int32_t Hq, int32_t Hkv, int32_t D, void* qkv, int64_t ld,
+                                  const void* rope_cos, const void* rope_sin, int64_t rope_ld, void* k_cache,
+                                  int64_t ldk, int64_t bsk, void* v_cache, int64_t ldv, int64_t bsv, int32_t p0,
+                                  void* stream) {
+  return qkv_rope_append_impl<true>(B, Lq, Hq, Hkv, D, qkv, ld, rope_cos, rope_sin, rope_ld, k_cache, ldk, bsk,
+                                    v_cache, ldv, bsv, p0, stream);
 }

@@ -694,6 +694,13 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
             K.qkv_rope_append(qkv, B, Lq, cfg.Hq, cfg.Hkv, cfg.D, cos, sin, k_cache, v_cache, p0)
             K.attn_decode(qkv[:, :qd], Lq, k_cache, v_cache, p0 + Lq, cfg.Hq, cfg.Hkv, cfg.D, cfg.scale,
                           cfg.softcap, kv_class, cfg.window, attn)
+    elif PREFILL_ROPE_FILL[0]:
+        # the plain projection, then one launch rotates q and k in place and fills cache rows 0.. with k and v
+        # (svla_qkv_rope_fill: the ROPE epilogue's rounding, bitwise), instead of the RoPE epilogue + two cache copies
+        if cos.shape[0] != B * Lq:
+            cos, sin = cos.repeat(B, 1), sin.repeat(B, 1)
+        K.linear_fwd(x, [wq, wk, wv], qkv)
+        K.qkv_rope_append(qkv, B, Lq, cfg.Hq, cfg.Hkv, cfg.D, cos, sin, k_cache, v_cache, 0, k_back=True)
     else:
         K.linear_fwd(x, [wq, wk, wv], qkv, kind=L.EPI_ROPE, rope=(cos, sin, cos.shape[0], cfg.D, qd + kd))
         k_cache[:, :Lq].copy_(qkv[:, qd:qd + kd].view(B, Lq, kd))
@@ -709,6 +716,11 @@ def gemma_attention_cached(x, wq, wk, wv, wo, cos, sin, k_cache, v_cache, kv_cla
     out = _empty(M, wo.shape[0], like=like)
     K.linear_fwd(attn, [wo], out)
     return out
+
+
+# the prefill's q|k|v: plain GEMM + svla_qkv_rope_fill (one launch: RoPE of q and k, cache rows of k and v) instead
+# of the RoPE epilogue + two cache copies; SVLA_PREFILL_ROPE_FILL=0: the latter
+PREFILL_ROPE_FILL = [os.environ.get("SVLA_PREFILL_ROPE_FILL", "1") != "0"]
 
 
 # ... with the o projection inside the same launch (a second grid barrier) instead of its own GEMV: opt-in, measured

@@ -799,18 +799,19 @@ def attn_decode_rope(qkv, Lq, cos, sin, k_cache, v_cache, Lk, Hq, Hkv, D, scale,
             "attn_decode_rope")
 
 
-def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0):
-    """RoPE q in place, rotated k and v into cache rows p0.. (the decode step's q|k|v epilogue)."""
+def qkv_rope_append(qkv, B, Lq, Hq, Hkv, D, cos, sin, k_cache, v_cache, p0, k_back=False):
+    """RoPE q in place, rotated k and v into cache rows p0.. (the decode step's q|k|v epilogue); k_back: k rotated in
+    place as well (svla_qkv_rope_fill, the prefill: its flash attention reads q and k from the projection rows)."""
     _req(qkv.shape[0] == B * Lq and qkv.stride(1) == 1, "qkv_rope_append: qkv rows")
     _req(cos.shape[0] >= B * Lq and cos.shape == sin.shape and cos.stride(1) == 1,
          "qkv_rope_append: tables must hold one row per token row b*Lq+t")
     _req(k_cache.shape[1] >= p0 + Lq and v_cache.shape[1] >= p0 + Lq, "qkv_rope_append: cache too short")
     for t, n in ((qkv, "qkv"), (cos, "cos"), (sin, "sin"), (k_cache, "k_cache"), (v_cache, "v_cache")):
         _chk_bf16(t, n)
-    L.check(L.lib().svla_qkv_rope_append(B, Lq, Hq, Hkv, D, qkv.data_ptr(), qkv.stride(0), cos.data_ptr(),
-                                         sin.data_ptr(), cos.stride(0), k_cache.data_ptr(), k_cache.stride(1),
-                                         k_cache.stride(0), v_cache.data_ptr(), v_cache.stride(1), v_cache.stride(0),
-                                         int(p0), _stream()), "qkv_rope_append")
+    fn = L.lib().svla_qkv_rope_fill if k_back else L.lib().svla_qkv_rope_append
+    L.check(fn(B, Lq, Hq, Hkv, D, qkv.data_ptr(), qkv.stride(0), cos.data_ptr(), sin.data_ptr(), cos.stride(0),
+               k_cache.data_ptr(), k_cache.stride(1), k_cache.stride(0), v_cache.data_ptr(), v_cache.stride(1),
+               v_cache.stride(0), int(p0), _stream()), "qkv_rope_append")
 
 
 # head_dim-256 backward with dS stored by the dK/dV kernel and dQ = dS K (svla_attn_bwd_ds) instead of the dQ kernel

@@ -1261,3 +1261,32 @@ def test_gemm_deep_rope_pass_bitwise(cuda):
         outs[v] = o
     assert torch.equal(outs[3], outs[11])
     assert rel_l2(outs[14], outs[3]) < 2e-3 and rel_l2(outs[0], outs[3]) < 2e-3
+
+
+@pytest.mark.parametrize("B,Lq", [(1, 299), (2, 37)])
+def test_qkv_rope_fill_matches_rope_epilogue(cuda, B, Lq):
+    """svla_qkv_rope_fill (the prefill: plain q|k|v GEMM, then q and k rotated in place and k / v written to cache
+    rows 0..) == the GEMM's ROPE epilogue + copies of the k / v columns into the cache, bit for bit, per-sequence
+    position tables (row b*Lq+t)."""
+    from spatialvla_amd import kernels as Kn, _lib as L
+    torch.manual_seed(81)
+    Hq, Hkv, D, H, cap = 8, 4, 256, 512, 320
+    qd, kd = Hq * D, Hkv * D
+    M = B * Lq
+    x = _r(M, H)
+    ws = [_r(qd, H, scale=0.05), _r(kd, H, scale=0.05), _r(kd, H, scale=0.05)]
+    pos = torch.cat([torch.arange(Lq, device=cuda) + 3 * b for b in range(B)]).float()
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    fr = pos[:, None] * inv[None]
+    cos, sin = fr.cos().to(BF).contiguous(), fr.sin().to(BF).contiguous()
+    ref = torch.empty(M, qd + 2 * kd, dtype=BF, device=cuda)
+    Kn.linear_fwd(x, ws, ref, kind=L.EPI_ROPE, rope=(cos, sin, M, D, qd + kd))
+    got = torch.empty_like(ref)
+    Kn.linear_fwd(x, ws, got)
+    kc = torch.full((B, cap, kd), 3.0, dtype=BF, device=cuda)
+    vc = torch.full((B, cap, kd), 3.0, dtype=BF, device=cuda)
+    Kn.qkv_rope_append(got, B, Lq, Hq, Hkv, D, cos, sin, kc, vc, 0, k_back=True)
+    assert torch.equal(got, ref)
+    assert torch.equal(kc[:, :Lq], ref[:, qd:qd + kd].view(B, Lq, kd))
+    assert torch.equal(vc[:, :Lq], ref[:, qd + kd:].view(B, Lq, kd))
+    assert bool((kc[:, Lq:] == 3.0).all()) and bool((vc[:, Lq:] == 3.0).all())
