@@ -74,10 +74,25 @@ using CfgMid = Cfg<256, 128, 4, 2>;
 using CfgSmall = Cfg<128, 128, 2, 2>;
 using CfgTiny = Cfg<64, 64, 2, 2>;  // sub-wave grids of the B = 1 prefill (4x the blocks of 128x128)
 // deep-pipelined small tiles for the short-M GEMMs of the B = 1 prefill (launch_deep)
-using CfgTinyD = Cfg<64, 64, 2, 2, 8>;
-using CfgNarrowD = Cfg<64, 128, 2, 2, 6>;
-using CfgSmallD = Cfg<128, 128, 2, 2, 4>;
+// stages: 4 x 16 KiB (64x64) and 3 x 24 KiB (64x128) leave room for two workgroups per CU, which keep twice the
+// LDS-DMA in flight per CU -- 8 / 6 stages at one workgroup per CU measured slower (q|k|v 28.1 -> 24.5 us, o 18.5 ->
+// 16.4, down 39.4 -> 31.1 at 299 rows; profiles/r9j_deep_two_per_cu_ab.txt); 128x128 keeps 4 stages (one per CU)
+#ifndef TINY_NST
+#define TINY_NST 4
+#endif
+#ifndef NARROW_NST
+#define NARROW_NST 3
+#endif
+#ifndef SMALL_NST
+#define SMALL_NST 4
+#endif
+using CfgTinyD = Cfg<64, 64, 2, 2, TINY_NST>;
+using CfgNarrowD = Cfg<64, 128, 2, 2, NARROW_NST>;
+using CfgSmallD = Cfg<128, 128, 2, 2, SMALL_NST>;
 using CfgWideD = Cfg<128, 256, 2, 2, 3>;
+// workgroups of a deep-pipelined instance one CU holds (LDS-bound; the register counts allow two)
+template <typename C>
+constexpr int deep_bpc() { return C::LDS <= 78 * 1024 ? 2 : 1; }
 
 // RC image swizzle (even values 0..14, distinct over the 8 k-rows one tr-read half touches)
 __device__ __forceinline__ int rc_swz(int k) { return ((k & 3) | ((k & 8) >> 1)) << 1; }
@@ -2567,6 +2582,7 @@ template <typename C>
 int launch(int64_t M, int64_t N, int64_t K, const svla_operand& A, const svla_operand& B, const CDesc& Cd,
            const svla_epilogue& E, hipStream_t s, SplitArgs sp = SplitArgs{1, nullptr, nullptr}) {
   const int64_t tiles = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
+  SVLA_CHECK_ARG(sp.S == 1 || (C::NST > 2 && sp.slabs && sp.counters), "gemm: split-K needs a deep-pipelined tile");
   dim3 grid((unsigned)(tiles * sp.S)), block(C::NTH);
   const int la = A.layout, lb = B.layout;
 #define SVLA_LAUNCH(LA_, LB_)                                                                      \
@@ -3231,7 +3247,7 @@ size_t sk_workspace_bytes(int G) { return (size_t)2 * G * 32 * p8::NTH * 16 + (s
 // workspace's layout (slab region of 2G 256 KiB slabs, 2G counters behind it).  S = 1: no split.
 template <typename C>
 SplitArgs split_args(int64_t M, int64_t N, int64_t K, const GemmCtx& ctx) {
-  const int G = grid_cus();
+  const int G = grid_cus() * deep_bpc<C>();
   const int64_t tiles = ((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN);
   const int64_t nk = (K + BK - 1) / BK;
   int64_t S = tiles < G ? G / tiles : 1;
@@ -3692,19 +3708,19 @@ int gemm_dispatch(int64_t M, int64_t N, int64_t K, const svla_operand* A, const 
   // 18.2, BEiT fc2 33.2 -> 22.0.
   if (variant == 0 && M <= 1024 && A->layout == SVLA_LAYOUT_KC && B->layout == SVLA_LAYOUT_KC && !kseg &&
       ek != SVLA_EPI_SOFTCAP_CE && !(ek == SVLA_EPI_GEGLU && epi->mx_q)) {
-    const int G = grid_cus();
-    auto est = [&](int bm, int bn, int S) {
+    auto est = [&](int bm, int bn, int S, int bpc) {
+      const int G = grid_cus() * bpc;
       const double waves = (double)((tiles(bm, bn) * S + G - 1) / G);
       const double fill = (double)nk / S * BK * (bm + bn) * 2;
       return waves * (fill + (S > 1 ? (double)bm * bn * 4 * (1 + 2 * S) : 0.0));
     };
     const SplitArgs s64 = split_args<CfgTinyD>(M, N, K, ctx), s64n = split_args<CfgNarrowD>(M, N, K, ctx),
                     s128 = split_args<CfgSmallD>(M, N, K, ctx), s128w = split_args<CfgWideD>(M, N, K, ctx);
-    const double e64 = seg_ok(64, 64) ? est(64, 64, s64.S) : 1e30;
-    const double e64n = seg_ok(64, 128) ? est(64, 128, s64n.S) : 1e30;
-    const double e128 = seg_ok(128, 128) ? est(128, 128, s128.S) : 1e30;
-    const double e128w = (WIDE_DEEP && seg_ok(128, 256)) ? est(128, 256, s128w.S) : 1e30;
-    const double ebig = seg_ok(256, 256) ? est(256, 256, 1) : 1e30;
+    const double e64 = seg_ok(64, 64) ? est(64, 64, s64.S, deep_bpc<CfgTinyD>()) : 1e30;
+    const double e64n = seg_ok(64, 128) ? est(64, 128, s64n.S, deep_bpc<CfgNarrowD>()) : 1e30;
+    const double e128 = seg_ok(128, 128) ? est(128, 128, s128.S, deep_bpc<CfgSmallD>()) : 1e30;
+    const double e128w = (WIDE_DEEP && seg_ok(128, 256)) ? est(128, 256, s128w.S, deep_bpc<CfgWideD>()) : 1e30;
+    const double ebig = seg_ok(256, 256) ? est(256, 256, 1, 1) : 1e30;
     const double best = std::min(std::min(e64, e64n), std::min(e128, e128w));
     if (best < ebig) {
       if (best == e64n) return launch_deep<CfgNarrowD>(M, N, K, *A, *B, C, *epi, s, s64n);
