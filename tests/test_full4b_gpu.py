@@ -155,7 +155,8 @@ _NORM_SUFFIXES = ("layernorm.weight", "layer_norm1.weight", "layer_norm2.weight"
 
 DRIFT_MAX = 3.2e-2     # largest non-q/k full-tensor gradient error (measured 3.11e-2 r3, 3.12e-2 r4)
 DRIFT_MEDIAN = 2.8e-2  # median over all tensors (measured 2.72e-2 r3 and r4)
-DRIFT_COUNT = 11       # non-q/k tensors above 3e-2: measured 9 (r5i) + 2 (12 r3; 10 r4p -> 14 r4r -> 9 r5i)
+DRIFT_COUNT = 17       # non-q/k tensors above 3e-2: measured 15 (r9m) + 2 (12 r3; 10 r4p -> 14 r4r -> 9 r5i -> 15 r9m)
+DRIFT_P95 = 2.95e-2    # 95th percentile of the non-q/k errors (measured 2.87e-2 r5i, 2.90e-2 r9m)
 
 
 def _full_tol(name: str) -> float:
@@ -252,6 +253,11 @@ def test_full4b_train_step_vs_reference(model4b, gold, cuda):
           f"median {med:.4f}")
     assert not over or over[-1][0] <= DRIFT_MAX, over[-6:]
     assert med <= DRIFT_MEDIAN, med
+    # r9m: the B = 1 step's forward projections (M = 312) moved to the short-M split-K tiles: the median fell (2.67 ->
+    # 2.60e-2 all tensors) while six tensors crossed 3e-2 from just below (3.00-3.16e-2); the tail is bounded by its
+    # 95th percentile as well, which a general loss of accuracy would move
+    nq = sorted(e for n, e in full_rel.items() if not _qk_exception(n))
+    assert _pct(nq, 95) <= DRIFT_P95, _pct(nq, 95)
     assert len(over) <= DRIFT_COUNT, over
 
 
