@@ -549,6 +549,10 @@ typedef struct {
   const void* res1;   /* NULL or [B,OH,OW,Cout] */
   const void* res2;   /* NULL or [B,OH,OW,Cout] */
   void* out;
+  /* optional: the caller's svla_gemm_bf16 workspace for this stream (NULL = no split-K).  Grids of 64x64 tiles under
+   * one wave (the B = 1 DPT neck) split K over workgroups into its fp32 slabs + arrival counters */
+  void* workspace;
+  size_t ws_bytes;
 } svla_conv_args;
 int svla_conv2d_nhwc(const svla_conv_args* a, void* stream);
 

@@ -59,7 +59,7 @@ class ConvArgs(ctypes.Structure):
     _fields_ = [("B", c_i32), ("H", c_i32), ("W", c_i32), ("Cin", c_i32), ("OH", c_i32), ("OW", c_i32),
                 ("Cout", c_i32), ("KH", c_i32), ("KW", c_i32), ("stride", c_i32), ("pad", c_i32),
                 ("flags", c_i32), ("factor", c_i32), ("_pad", c_i32), ("x", c_vp), ("w", c_vp), ("bias", c_vp),
-                ("res1", c_vp), ("res2", c_vp), ("out", c_vp)]
+                ("res1", c_vp), ("res2", c_vp), ("out", c_vp), ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t)]
 
 
 CONV_PRE_RELU, CONV_POST_RELU, CONV_TRANSPOSED = 1, 2, 4

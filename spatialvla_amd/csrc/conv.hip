@@ -20,6 +20,9 @@
 
 namespace {
 
+#ifndef CONV_SPLIT_MAX
+#define CONV_SPLIT_MAX 8  // split-K factor cap of the sub-wave 64x64 grids (diagnostic A/B: 1 = no split)
+#endif
 #ifndef CONV_SMALL
 #define CONV_SMALL 1  // 64 x 64 tiles for sub-wave grids (diagnostic A/B: 0 = always 128 x 128)
 #endif
@@ -38,6 +41,9 @@ struct ConvK {
   int RH, RW;  // the GEMM rows are B x RH x RW pixels: the output pixels, or the input pixels (transposed form)
   int N, K;
   int64_t M;
+  int S;           // split-K factor (1 = none): slabs / counters in the caller's GEMM workspace
+  float* slabs;
+  int* counters;
 };
 
 template <int BM_, int BN_, int WGM_, int WGN_>
@@ -82,15 +88,28 @@ __global__ __launch_bounds__(C::NTH, 2) void conv_kernel(ConvK p) {
   constexpr int BM = C::BM, BN = C::BN, NTH = C::NTH, TM = C::TM, TN = C::TN, IA = C::IA, IB = C::IB;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  __shared__ int sflag;
   const int tiles_m = (int)((p.M + BM - 1) / BM), tiles_n = (p.N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
-  const int pid = xcd_remap(blockIdx.x, total);
-  constexpr int GM = 8;
-  const int group = GM * tiles_n;
-  const int first_m = (pid / group) * GM;
-  const int gsz = min(tiles_m - first_m, GM);
-  const int tm = first_m + (pid % group) % gsz;
-  const int tn = (pid % group) / gsz;
+  int tm, tn, split = 0;
+  if (p.S > 1) {  // gemm.hip's split-K hand-off: block (tile, split), the M tiles of a (split, column tile) adjacent
+    const int L = xcd_remap(blockIdx.x, total * p.S);
+    split = L / total;
+    const int tile = L % total;
+    tm = tile % tiles_m;
+    tn = tile / tiles_m;
+  } else {
+    const int pid = xcd_remap(blockIdx.x, total);
+    constexpr int GM = 8;
+    const int group = GM * tiles_n;
+    const int first_m = (pid / group) * GM;
+    const int gsz = min(tiles_m - first_m, GM);
+    tm = first_m + (pid % group) % gsz;
+    tn = (pid % group) / gsz;
+  }
+  const int nk_all = (p.K + CBK - 1) / CBK;
+  const int kb = (int)((int64_t)split * nk_all / p.S);
+  const int nk = (int)((int64_t)(split + 1) * nk_all / p.S) - kb;
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
   const int wr = w / C::WGN, wc = w % C::WGN;
@@ -115,7 +134,7 @@ __global__ __launch_bounds__(C::NTH, 2) void conv_kernel(ConvK p) {
       pb[i] = 0;
     }
   }
-  int kk = gc * 8;               // this lane's k within the current k-tile's stream
+  int kk = kb * CBK + gc * 8;    // this lane's k within the current k-tile's stream
   int tap = kk / p.Cin, ci = kk - tap * p.Cin;
   int ky = tap / p.KW, kx = tap - ky * p.KW;
   const int ntap = p.KH * p.KW;
@@ -161,12 +180,11 @@ __global__ __launch_bounds__(C::NTH, 2) void conv_kernel(ConvK p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   constexpr int NLD = IA + IB;
-  const int nk = (p.K + CBK - 1) / CBK;
   issue_a(smem);
-  issue_b(smem + C::A_BYTES, 0);
+  issue_b(smem + C::A_BYTES, kb * CBK);
   if (nk > 1) {
     issue_a(smem + C::STAGE);
-    issue_b(smem + C::STAGE + C::A_BYTES, CBK);
+    issue_b(smem + C::STAGE + C::A_BYTES, (kb + 1) * CBK);
   }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
@@ -194,7 +212,49 @@ __global__ __launch_bounds__(C::NTH, 2) void conv_kernel(ConvK p) {
     __builtin_amdgcn_s_barrier();
     if (kt + 2 < nk) {
       issue_a(smem + cur * C::STAGE);
-      issue_b(smem + cur * C::STAGE + C::A_BYTES, (kt + 2) * CBK);
+      issue_b(smem + cur * C::STAGE + C::A_BYTES, (kb + kt + 2) * CBK);
+    }
+  }
+  if (p.S > 1) {
+    // slab per (tile, split) stored write-through, arrival counter, the last arriver sums the slabs in split order
+    // (gemm.hip gemm_kernel's hand-off; deterministic whichever block is last) and runs the epilogue
+    const int tile = tm + tn * tiles_m;
+    constexpr int SLAB = TM * TN * NTH * 16;
+    const char* base = reinterpret_cast<const char*>(p.slabs) + (int64_t)tile * p.S * SLAB;
+    {
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)split * SLAB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 (uint32_t)((t + (i * TN + j) * NTH) * 16), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      int* cnt = p.counters + tile;
+      const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sflag = (old == p.S - 1);
+      if (old == p.S - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!sflag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (int sg = 0; sg < p.S; ++sg) {
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(base + (int64_t)sg * SLAB);
+      f32x4 x[TM][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          x[i][j] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((t + (i * TN + j) * NTH) * 16), 0, 16));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = sg == 0 ? x[i][j] : acc[i][j] + x[i][j];
     }
   }
 
@@ -273,7 +333,7 @@ __global__ __launch_bounds__(C::NTH, 2) void conv_kernel(ConvK p) {
 
 template <typename C>
 int launch_conv(const ConvK& k, bool pre_relu, hipStream_t s) {
-  const int64_t tiles = ((k.M + C::BM - 1) / C::BM) * ((k.N + C::BN - 1) / C::BN);
+  const int64_t tiles = ((k.M + C::BM - 1) / C::BM) * ((k.N + C::BN - 1) / C::BN) * k.S;
   if (tiles > 0x7fffffff) return SVLA_ERR_ARG;
   static bool set0 = false, set1 = false;
   if (pre_relu) {
@@ -308,6 +368,9 @@ extern "C" int svla_conv2d_nhwc(const svla_conv_args* a, void* stream) {
   SVLA_CHECK_ARG((int64_t)a->B * a->H * a->W * a->Cin * 2 < (1ll << 31),
                  "conv2d_nhwc: input over 2 GiB (split the batch)");
   ConvK k;
+  k.S = 1;
+  k.slabs = nullptr;
+  k.counters = nullptr;
   k.x = (const bf16_t*)a->x;
   k.w = (const bf16_t*)a->w;
   k.bias = (const bf16_t*)a->bias;
@@ -346,6 +409,24 @@ extern "C" int svla_conv2d_nhwc(const svla_conv_args* a, void* stream) {
   // a grid of 128 x 128 tiles under one wave of CUs (B = 1 prefill: the 12x12 .. 48x48 maps of the DPT neck): 4x the
   // workgroups on 64 x 64 tiles, each k-tile half the bytes (a small block's k-loop is bound by its CU's intake)
   const int64_t t128 = ((k.M + 127) / 128) * ((k.N + 127) / 128);
-  if (CONV_SMALL && t128 < svla::num_cus()) return launch_conv<ConvSmall>(k, pre, s);
+  if (CONV_SMALL && t128 < svla::num_cus()) {
+    // split-K while the 64x64 grid stays under one wave: S = G / tiles, >= 4 k-tiles a split, at most CONV_SPLIT_MAX
+    // (the reducer reads S 16 KiB slabs); slabs and counters in the caller's GEMM workspace (its chip-wide layout:
+    // counters behind 2 x CUs slabs of 256 KiB)
+    const int G = svla::num_cus();
+    const int64_t t64 = ((k.M + 63) / 64) * ((k.N + 63) / 64);
+    const int64_t nk = (k.K + CBK - 1) / CBK;
+    int64_t S = t64 < G ? G / t64 : 1;
+    S = std::min<int64_t>(S, std::min<int64_t>(nk / 4, CONV_SPLIT_MAX));
+    const size_t slab_region = (size_t)2 * G * 32 * 512 * 16;
+    constexpr int64_t SLAB = (int64_t)ConvSmall::TM * ConvSmall::TN * ConvSmall::NTH * 16;
+    if (S >= 2 && a->workspace && a->ws_bytes >= slab_region + (size_t)2 * G * sizeof(int) && t64 <= 2 * G &&
+        t64 * S * SLAB <= (int64_t)slab_region && (((uintptr_t)a->workspace) & 255) == 0) {
+      k.S = (int)S;
+      k.slabs = reinterpret_cast<float*>(a->workspace);
+      k.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(a->workspace) + slab_region);
+    }
+    return launch_conv<ConvSmall>(k, pre, s);
+  }
   return launch_conv<ConvMid>(k, pre, s);
 }

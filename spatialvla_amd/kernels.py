@@ -1121,6 +1121,10 @@ def geglu_bwd_mx(dh: torch.Tensor, g: torch.Tensor, u: torch.Tensor, dg: torch.T
 
 
 # ---------------------------------------------------------------------------------------- NHWC convolution
+# split-K of the sub-wave convolution grids (the stream's GEMM workspace); SVLA_CONV_SPLIT=0: none
+CONV_SPLIT = [os.environ.get("SVLA_CONV_SPLIT", "1") != "0"]
+
+
 def conv_weight_khwc(weight: torch.Tensor, transposed: bool = False) -> torch.Tensor:
     """torch conv weight -> the svla_conv2d_nhwc layout: Conv2d [Cout, Cin, KH, KW] -> [Cout, KH, KW, Cin];
     ConvTranspose2d [Cin, Cout, f, f] -> [f, f, Cout, Cin]."""
@@ -1161,5 +1165,8 @@ def conv2d_cl(x: torch.Tensor, w_khwc: torch.Tensor, bias: Optional[torch.Tensor
     a.flags |= (L.CONV_PRE_RELU if pre_relu else 0) | (L.CONV_POST_RELU if post_relu else 0)
     a.x, a.w, a.bias, a.res1, a.res2, a.out = (x.data_ptr(), w_khwc.data_ptr(), _ptr(bias), _ptr(res1), _ptr(res2),
                                                out.data_ptr())
+    if CONV_SPLIT[0]:
+        ws = gemm_workspace()
+        a.workspace, a.ws_bytes = ws.data_ptr(), ws.numel()
     L.check(L.lib().svla_conv2d_nhwc(ctypes.byref(a), _stream()), "svla_conv2d_nhwc")
     return out

@@ -70,3 +70,32 @@ def test_conv2d_nhwc_rejects_bad_args(cuda):
     w = K.conv_weight_khwc(torch.randn(16, 12, 3, 3, device=cuda).to(BF))
     with pytest.raises(RuntimeError):
         K.conv2d_cl(x, w, None, pad=1)
+
+
+@pytest.mark.parametrize("B,Cin,H,W,Cout,k,s,p", [(1, 256, 24, 24, 256, 3, 1, 1), (1, 256, 12, 12, 256, 3, 1, 1),
+                                                (1, 512, 48, 48, 256, 1, 1, 0), (1, 256, 12, 12, 256, 3, 2, 1)])
+def test_conv2d_split_k_matches_unsplit(cuda, B, Cin, H, W, Cout, k, s, p):
+    """Sub-wave 64x64 convolution grids split K over workgroups (the B = 1 DPT neck; slabs + counters in the stream's
+    GEMM workspace): against fp32 torch, within fp32 reordering of the unsplit result, and bitwise reproducible
+    (deterministic reduction order, counters left zero) -- with pre-activation ReLU and two residuals."""
+    from spatialvla_amd import kernels as K
+    torch.manual_seed(3)
+    x = torch.randn(B, Cin, H, W, device=cuda).to(BF)
+    w = (torch.randn(Cout, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5).to(BF)
+    b = torch.randn(Cout, device=cuda).to(BF)
+    OH = (H + 2 * p - k) // s + 1
+    r1 = _cl(torch.randn(B, Cout, OH, OH, device=cuda).to(BF))
+    r2 = _cl(torch.randn(B, Cout, OH, OH, device=cuda).to(BF))
+    wk = K.conv_weight_khwc(w)
+    outs = []
+    for split in (False, True, True):
+        K.CONV_SPLIT[0] = split
+        try:
+            outs.append(K.conv2d_cl(_cl(x), wk, b, stride=s, pad=p, pre_relu=True, res1=r1, res2=r2))
+        finally:
+            K.CONV_SPLIT[0] = True
+    torch.cuda.synchronize()
+    ref = F.conv2d(F.relu(x).float(), w.float(), b.float(), stride=s, padding=p) + r1.float() + r2.float()
+    assert rel_l2(outs[1], ref) < 8e-3
+    assert rel_l2(outs[1], outs[0]) < 4e-3
+    assert torch.equal(outs[1], outs[2])
